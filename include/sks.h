@@ -1,0 +1,180 @@
+/*
+ * sks.h — C ABI of the MI355X spaced-k-mer sketch + ANI engine (libsks.so).
+ *
+ * Plain pointers and sizes only.  "d_" arguments are device (HBM) pointers on
+ * the context's device; everything else is host memory owned by the caller.
+ * Every entry point returns an sks_status (0 = OK); the message of the last
+ * failure on the calling thread is available from sks_last_error().
+ *
+ * Each entry point names the reference interface it replaces
+ * (bensonlzl/spaced-kmer-sketching @ 2024-10-22, paths under src/).
+ * The reference is a source-level C++ API with no FFI; the C++ facade in
+ * spaced-kmer-sketching_amd/cpp/ re-exposes the reference names on top of
+ * this ABI (see INTEGRATION.md for the binding a maintainer would add).
+ */
+#ifndef SKS_H
+#define SKS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SKS_ABI_VERSION 1
+
+typedef enum sks_status {
+  SKS_OK = 0,
+  SKS_E_ARG = 1,         /* invalid argument (the reference has UB here)        */
+  SKS_E_HIP = 2,         /* HIP runtime error / no device                        */
+  SKS_E_IO = 3,          /* unreadable FASTA (reference: stderr + exit(1))       */
+  SKS_E_NOMEM = 4,       /* host or device allocation failed                    */
+  SKS_E_UNSUPPORTED = 5, /* valid in the reference, not implemented here (yet)   */
+  SKS_E_LENGTH = 6       /* pair lists of different lengths (kmer_set.cpp:147)   */
+} sks_status;
+
+/* Sketch selection policy: the device-side replacement for the reference's
+ * std::function<bool(const kmer)> sketching_cond (kmer.hpp:97, kmer_sliding.cpp:183),
+ * which is a host callback and cannot run in a kernel. */
+typedef enum sks_policy_kind {
+  SKS_FRAC_MOD = 0, /* keep iff frac_min_hash(k) % param == 0 (kmer-sketching.cpp:30-34) */
+  SKS_BOTTOM_S = 1  /* the `param` distinct k-mers with the smallest frac_min_hash
+                       (ties by k-mer value) — build-defined, no reference equivalent */
+} sks_policy_kind;
+
+/* boost::hash_value(dynamic_bitset) flavour used by frac_min_hash (kmer.hpp:137-146).
+ * The reference does not pin its Boost version; see DESIGN.md "hash parity". */
+typedef enum sks_hash_flavour {
+  SKS_HASH_BOOST_MIX = 0,   /* Boost >= 1.81: hash_combine = hash_mix(seed + 0x9e3779b9 + v) */
+  SKS_HASH_BOOST_LEGACY = 1 /* Boost 1.71-1.80: MurmurHash2-style hash_combine_impl          */
+} sks_hash_flavour;
+
+typedef struct sks_policy {
+  int32_t kind;    /* sks_policy_kind                                   */
+  int32_t flavour; /* sks_hash_flavour                                  */
+  uint64_t param;  /* SKS_FRAC_MOD: c (> 0); SKS_BOTTOM_S: s (> 0)       */
+  int64_t nonce;   /* frac_min_hash nonce; the reference uses fmh(1)     */
+} sks_policy;
+
+/* ---- library ---------------------------------------------------------------- */
+int sks_abi_version(void);
+const char* sks_last_error(void);
+
+/* ---- host helpers (no device needed) ---------------------------------------------- */
+/* generate_random_spaced_seed_mask(w, k, seed) — kmer_bitset.cpp:132-152.
+ * mask[0] = bits 0..63, mask[1] = bits 64..127.  1 <= k <= w <= 64. */
+int sks_mask_generate(int window, int k, uint64_t seed, uint64_t mask[2]);
+/* contiguous_kmer(l) — kmer_bitset.cpp:50-56 (l > 64 -> SKS_E_ARG like its runtime_error). */
+int sks_mask_contiguous(int length, uint64_t mask[2]);
+/* frac_min_hash::operator() — kmer.hpp:144-148 (kmer = masked canonical bits). */
+uint64_t sks_frac_min_hash(const uint64_t kmer[2], const uint64_t mask[2], int window,
+                           int64_t nonce, int flavour);
+/* containment / binomial_estimator — ani_estimation.cpp:24-28, :38-42. */
+double sks_containment(int intersection, int set_size);
+double sks_binomial_estimator(double containment, int kmer_num_ones);
+/* Vector form of kmer-sketching.cpp:195-200: cont[i] = containment(inter[i], size_first[i]),
+ * ani[i] = binomial_estimator(cont[i], kmer_num_ones).  Either output may be NULL. */
+int sks_ani_from_counts(const int32_t* inter, const int32_t* size_first, uint64_t n,
+                        int kmer_num_ones, double* cont, double* ani);
+
+/* ---- FASTA ingress (host) — fasta_processing.cpp:79-211 ----------------------------- */
+typedef struct sks_fasta sks_fasta;
+/* strings_from_fasta(): parses the file with the reference's record rules.
+ * Unreadable file -> SKS_E_IO (the reference prints to stderr and exit(1)s). */
+int sks_fasta_open(const char* path, sks_fasta** out);
+void sks_fasta_close(sks_fasta* f);
+uint64_t sks_fasta_num_records(const sks_fasta* f);
+/* Record i's raw content (the i-th string of strings_from_fasta). */
+int sks_fasta_record(const sks_fasta* f, uint64_t i, const uint8_t** data, uint64_t* len);
+/* The record stream handed to the device: every record followed by one '\n'
+ * separator (a non-ACGT byte, so k-mers never span records). */
+const uint8_t* sks_fasta_stream(const sks_fasta* f);
+uint64_t sks_fasta_stream_bytes(const sks_fasta* f);
+/* cut_nucleotide_strings(): ACGT runs as codes 0..3 (one byte each).  Call with
+ * NULL buffers to get *n_codes / *n_runs, then again with buffers that large. */
+int sks_fasta_runs(const sks_fasta* f, uint8_t* codes, uint64_t* run_lens, uint64_t* n_codes,
+                   uint64_t* n_runs);
+
+/* ---- device context ---------------------------------------------------------------- */
+typedef struct sks_ctx sks_ctx;
+/* stream: a hipStream_t (may be NULL = the default stream). */
+int sks_ctx_create(int device, void* stream, sks_ctx** out);
+int sks_ctx_destroy(sks_ctx* ctx);
+int sks_ctx_set_stream(sks_ctx* ctx, void* stream);
+int sks_ctx_synchronize(sks_ctx* ctx);
+
+/* Per-phase device times of the last sketch build / intersection on this
+ * context, measured with hipEvents on the context's stream. */
+typedef struct sks_timings {
+  float scan_ms;      /* fused extract/canonicalise/hash/select kernel(s) */
+  float post_ms;      /* sort + unique + bottom-s selection               */
+  float total_ms;     /* whole call, first launch to last                 */
+  uint64_t windows;   /* k-mer windows hashed                             */
+  uint64_t scan_launches;
+  uint64_t survivors; /* records emitted by the scan kernel               */
+} sks_timings;
+int sks_ctx_last_timings(const sks_ctx* ctx, sks_timings* out);
+
+/* ---- sketch build: kmer_sliding.cpp:112-238 + kmer.hpp:135-190 + kmer_set.cpp:54-133 ---
+ * d_seq: n_bytes of sequence bytes in device memory.  Non-ACGT bytes split runs
+ * exactly as fasta_processing.cpp:144-179 does, so an sks_fasta stream can be
+ * uploaded as is.  The bytes are cut into n_seg segments (genomes) by the host
+ * array seg_off[n_seg + 1]; one sketch is built per segment (the reference
+ * builds one kmer_set per FASTA file, kmer_set.cpp:112-133).
+ * Result: an opaque device-resident sketch set (sorted unique canonical masked
+ * k-mers per segment; one u64 word per k-mer when window <= 32, two (lo, hi)
+ * when 32 < window <= 64). */
+typedef struct sks_sketch_set sks_sketch_set;
+int sks_sketch_build(sks_ctx* ctx, const uint8_t* d_seq, uint64_t n_bytes, const uint64_t* seg_off,
+                     uint32_t n_seg, int window, const uint64_t mask[2], const sks_policy* policy,
+                     sks_sketch_set** out);
+int sks_sketch_set_free(sks_sketch_set* set);
+uint32_t sks_sketch_set_num(const sks_sketch_set* set);
+int sks_sketch_set_elem_words(const sks_sketch_set* set); /* 1 or 2 */
+/* Host copies of per-sketch sizes (kmer_set::kmer_set_size, kmer.hpp:186-189)
+ * and windows hashed per sketch. */
+int sks_sketch_set_sizes(const sks_sketch_set* set, uint32_t* sizes);
+int sks_sketch_set_windows(const sks_sketch_set* set, uint64_t* windows);
+/* Device layout: sketch i = d_data()[start[i]*elem_words ...], sizes[i] elements. */
+const uint64_t* sks_sketch_set_device_data(const sks_sketch_set* set);
+const uint64_t* sks_sketch_set_device_starts(const sks_sketch_set* set);
+const uint32_t* sks_sketch_set_device_sizes(const sks_sketch_set* set);
+int sks_sketch_set_starts(const sks_sketch_set* set, uint64_t* starts);
+/* Copy sketch i to host (sizes[i] * elem_words u64). */
+int sks_sketch_set_copy(const sks_sketch_set* set, uint32_t i, uint64_t* out);
+/* Write all sketches into a caller-owned fixed-stride device layout
+ * (d_dst[i * stride * elem_words ...], d_sizes[i]) — the all-gather shape. */
+int sks_sketch_set_export(const sks_sketch_set* set, uint64_t* d_dst, uint64_t stride,
+                          uint32_t* d_sizes);
+
+/* ---- intersection: kmer_set.cpp:23-41, :143-184 ----------------------------------
+ * Sketches in device memory: sketch i = d_data[d_starts[i]*elem_words ...],
+ * d_sizes[i] elements, each sorted ascending and unique (as built above). */
+/* Pair list (compute_pairwise_kmer_set_intersections): d_out[p] = |S[a[p]] ∩ S[b[p]]|. */
+int sks_intersect_pairs(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
+                        const uint32_t* d_sizes, int elem_words, const int32_t* d_a,
+                        const int32_t* d_b, uint64_t n_pairs, int32_t* d_out);
+/* All ordered pairs of a row block (generate_all_pairs_from_vector, generators.hpp:44-58):
+ * d_out[(i - row_begin) * n + j] = |S[i] ∩ S[j]| for row_begin <= i < row_end, 0 <= j < n. */
+int sks_intersect_all(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
+                      const uint32_t* d_sizes, int elem_words, uint32_t n, uint32_t row_begin,
+                      uint32_t row_end, int32_t* d_out);
+
+/* ---- diagnostics / tuning ------------------------------------------------------------- */
+/* Device time (ms) between the first and last launch of the last
+ * sks_intersect_* call on this context (waits for it to finish). */
+int sks_ctx_last_intersect_ms(sks_ctx* ctx, float* ms);
+/* Fix the scan kernel's persistent grid size (0 = derive from occupancy). */
+int sks_ctx_set_scan_grid(sks_ctx* ctx, int grid);
+
+/* ---- synthetic genomes (bench / test utility; no reference equivalent) ----------------- */
+/* Fills d_out[0..n) with ACGT bytes: base(p) = splitmix64(seed ^ (p * golden)) >> 62;
+ * if mut_rate > 0 a position mutates with probability mut_rate. */
+int sks_synth_bases(sks_ctx* ctx, uint8_t* d_out, uint64_t n, uint64_t seed, uint64_t mut_seed,
+                    double mut_rate, uint64_t pos_offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKS_H */

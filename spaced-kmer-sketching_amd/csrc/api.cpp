@@ -1,0 +1,818 @@
+// C-ABI implementation (include/sks.h): contexts, sketch build orchestration,
+// intersection launches and the host-side helpers of the reference API.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "sks.h"
+#include "sks_api_internal.hpp"
+#include "sks_hash.hpp"
+#include "sks_internal.hpp"
+
+namespace sks {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+}  // namespace sks
+
+#define SKS_HIP(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return sks::fail(SKS_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+#define SKS_TRY(expr)              \
+  do {                             \
+    int rc_ = (expr);              \
+    if (rc_ != SKS_OK) return rc_; \
+  } while (0)
+
+struct sks_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_s0 = nullptr, ev_s1 = nullptr;
+  sks::Scratch tmp;                 // rocPRIM temporary storage
+  sks::Scratch rec[3];              // scan records (key, val, hi)
+  sks::Scratch buf[10];             // dense working columns
+  sks::Scratch flag, pos;
+  sks::Scratch meta;                // small per-segment device arrays
+  std::vector<uint64_t> meta_host;  // staging for `meta`
+  sks_timings last{};
+  int grid_override = 0;
+};
+
+struct sks_sketch_set {
+  int device = 0;
+  int elem_words = 1;
+  uint32_t n = 0;
+  uint64_t* d_data = nullptr;    // elements (elem_words u64 each)
+  uint64_t* d_starts = nullptr;  // [n] element index of each sketch
+  uint32_t* d_sizes = nullptr;   // [n]
+  std::vector<uint32_t> sizes;
+  std::vector<uint64_t> starts;
+  std::vector<uint64_t> windows;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Packs small host arrays into ctx->meta with one H2D copy.
+class MetaArena {
+ public:
+  explicit MetaArena(sks_ctx* c) : c_(c) { c_->meta_host.clear(); }
+  // reserve n words; returns the word offset
+  size_t add(const std::vector<uint64_t>& v) {
+    size_t o = c_->meta_host.size();
+    c_->meta_host.insert(c_->meta_host.end(), v.begin(), v.end());
+    c_->meta_host.push_back(0);  // keep every array non-empty
+    return o;
+  }
+  size_t add_zero(size_t n) {
+    size_t o = c_->meta_host.size();
+    c_->meta_host.resize(o + n + 1, 0);
+    return o;
+  }
+  int upload() {
+    size_t bytes = c_->meta_host.size() * sizeof(uint64_t);
+    SKS_HIP(c_->meta.reserve(bytes));
+    SKS_HIP(hipMemcpyAsync(c_->meta.ptr, c_->meta_host.data(), bytes, hipMemcpyHostToDevice,
+                           c_->stream));
+    return SKS_OK;
+  }
+  uint64_t* ptr(size_t off) const { return reinterpret_cast<uint64_t*>(c_->meta.ptr) + off; }
+
+ private:
+  sks_ctx* c_;
+};
+
+uint64_t* col(sks_ctx* c, int i) { return reinterpret_cast<uint64_t*>(c->buf[i].ptr); }
+
+int reserve_cols(sks_ctx* c, std::initializer_list<int> ids, uint64_t words) {
+  for (int i : ids) SKS_HIP(c->buf[i].reserve(std::max<uint64_t>(words, 1) * sizeof(uint64_t)));
+  return SKS_OK;
+}
+
+int end_bit_of(uint64_t max_value) {
+  int b = 64 - __builtin_clzll(max_value | 1);
+  return b < 1 ? 1 : b;
+}
+
+std::vector<uint64_t> prefix(const std::vector<uint64_t>& v) {
+  std::vector<uint64_t> o(v.size() + 1, 0);
+  for (size_t i = 0; i < v.size(); ++i) o[i + 1] = o[i] + v[i];
+  return o;
+}
+
+// One completed pass: final sketches of `segs` (global segment ids) in CSR.
+struct PassOut {
+  uint64_t* d = nullptr;          // elements (elem_words u64 each)
+  std::vector<uint32_t> segs;
+  std::vector<uint64_t> off;      // CSR in elements, size segs.size() + 1
+};
+
+void free_passes(std::vector<PassOut>& passes) {
+  for (auto& p : passes)
+    if (p.d) (void)hipFree(p.d);
+  passes.clear();
+}
+
+int alloc_u64(uint64_t** p, uint64_t words) {
+  SKS_HIP(hipMalloc(reinterpret_cast<void**>(p), std::max<uint64_t>(words, 1) * sizeof(uint64_t)));
+  return SKS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sks_abi_version(void) { return SKS_ABI_VERSION; }
+
+const char* sks_last_error(void) { return sks::g_last_error.c_str(); }
+
+// ---- host helpers -----------------------------------------------------------------------
+
+// kmer_bitset.cpp:132-152 — std::shuffle(iota(w), std::mt19937(seed)); the
+// first k shuffled indices j set mask bits 2j and 2j+1.  libstdc++ is used on
+// purpose: the reference's masks are defined by its shuffle algorithm.
+int sks_mask_generate(int window, int k, uint64_t seed, uint64_t mask[2]) {
+  if (!mask) return sks::fail(SKS_E_ARG, "sks_mask_generate: null mask");
+  if (window < 1 || window > 64 || k < 0 || k > window)
+    return sks::fail(SKS_E_ARG, "sks_mask_generate: need 0 <= k <= window <= 64");
+  std::vector<int> idx(window);
+  std::iota(idx.begin(), idx.end(), 0);
+  std::shuffle(idx.begin(), idx.end(), std::mt19937((std::mt19937::result_type)seed));
+  mask[0] = mask[1] = 0;
+  for (int i = 0; i < k; ++i) {
+    int b = 2 * idx[i];
+    mask[b >> 6] |= 3ull << (b & 63);
+  }
+  return SKS_OK;
+}
+
+// kmer_bitset.cpp:50-56 — 2l low bits set; l > 64 throws in the reference.
+int sks_mask_contiguous(int length, uint64_t mask[2]) {
+  if (!mask) return sks::fail(SKS_E_ARG, "sks_mask_contiguous: null mask");
+  if (length > 64) return sks::fail(SKS_E_ARG, "Given k-mer length exceeds maximum k-mer length");
+  if (length < 0) return sks::fail(SKS_E_ARG, "sks_mask_contiguous: negative length");
+  int bits = 2 * length;
+  mask[0] = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+  mask[1] = bits <= 64 ? 0 : (bits >= 128 ? ~0ull : ((1ull << (bits - 64)) - 1));
+  return SKS_OK;
+}
+
+uint64_t sks_frac_min_hash(const uint64_t kmer[2], const uint64_t mask[2], int window,
+                           int64_t nonce, int flavour) {
+  return sks::hash_bitset128_rt(kmer[0], kmer[1], flavour) ^
+         sks::fmh_const(mask[0], mask[1], window, nonce, flavour);
+}
+
+double sks_containment(int intersection, int set_size) {
+  if (intersection == 0) return 0;
+  return ((double)intersection) / ((double)set_size);
+}
+
+double sks_binomial_estimator(double containment, int kmer_num_ones) {
+  if (containment <= 0) return 0;
+  return std::pow(containment, ((double)1.0) / ((double)kmer_num_ones));
+}
+
+int sks_ani_from_counts(const int32_t* inter, const int32_t* size_first, uint64_t n,
+                        int kmer_num_ones, double* cont, double* ani) {
+  if (n && (!inter || !size_first)) return sks::fail(SKS_E_ARG, "sks_ani_from_counts: null input");
+  for (uint64_t i = 0; i < n; ++i) {
+    double c = sks_containment(inter[i], size_first[i]);
+    if (cont) cont[i] = c;
+    if (ani) ani[i] = sks_binomial_estimator(c, kmer_num_ones);
+  }
+  return SKS_OK;
+}
+
+// ---- contexts -----------------------------------------------------------------------------
+
+int sks_ctx_create(int device, void* stream, sks_ctx** out) {
+  if (!out) return sks::fail(SKS_E_ARG, "sks_ctx_create: null out");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return sks::fail(SKS_E_HIP, "sks_ctx_create: no HIP device available (the engine has no CPU path)");
+  if (device < 0 || device >= n) return sks::fail(SKS_E_ARG, "sks_ctx_create: bad device index");
+  DeviceGuard g(device);
+  sks_ctx* c = new (std::nothrow) sks_ctx();
+  if (!c) return sks::fail(SKS_E_NOMEM, "sks_ctx_create: out of memory");
+  c->device = device;
+  c->stream = reinterpret_cast<hipStream_t>(stream);
+  if (hipEventCreate(&c->ev_begin) != hipSuccess || hipEventCreate(&c->ev_end) != hipSuccess ||
+      hipEventCreate(&c->ev_s0) != hipSuccess || hipEventCreate(&c->ev_s1) != hipSuccess) {
+    delete c;
+    return sks::fail(SKS_E_HIP, "sks_ctx_create: hipEventCreate failed");
+  }
+  *out = c;
+  return SKS_OK;
+}
+
+int sks_ctx_destroy(sks_ctx* c) {
+  if (!c) return SKS_OK;
+  DeviceGuard g(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  c->tmp.release();
+  for (auto& r : c->rec) r.release();
+  for (auto& b : c->buf) b.release();
+  c->flag.release();
+  c->pos.release();
+  c->meta.release();
+  (void)hipEventDestroy(c->ev_begin);
+  (void)hipEventDestroy(c->ev_end);
+  (void)hipEventDestroy(c->ev_s0);
+  (void)hipEventDestroy(c->ev_s1);
+  delete c;
+  return SKS_OK;
+}
+
+int sks_ctx_set_stream(sks_ctx* c, void* stream) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_set_stream: null ctx");
+  c->stream = reinterpret_cast<hipStream_t>(stream);
+  return SKS_OK;
+}
+
+int sks_ctx_synchronize(sks_ctx* c) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_synchronize: null ctx");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipStreamSynchronize(c->stream));
+  return SKS_OK;
+}
+
+int sks_ctx_last_timings(const sks_ctx* c, sks_timings* out) {
+  if (!c || !out) return sks::fail(SKS_E_ARG, "sks_ctx_last_timings: null argument");
+  *out = c->last;
+  return SKS_OK;
+}
+
+// Test/bench knob (not in sks.h): fixed scan grid size, 0 = occupancy-derived.
+int sks_ctx_set_scan_grid(sks_ctx* c, int grid) {
+  if (!c) return sks::fail(SKS_E_ARG, "null ctx");
+  c->grid_override = grid;
+  return SKS_OK;
+}
+
+}  // extern "C"
+
+// ---- sketch build ---------------------------------------------------------------------------
+namespace {
+
+struct BuildState {
+  sks_ctx* c;
+  int w;
+  bool wide;
+  int ew;
+  uint64_t mask_lo, mask_hi;
+  sks_policy pol;
+  uint64_t kconst;
+  sks::DivTest dt;
+};
+
+// Post-process the segments `ok` (pass-local indices into the pass arrays) whose
+// survivors sit in the record regions [out_off[i], out_off[i] + count[i]).
+// Appends a PassOut; for bottom-s reports segments that need a larger threshold.
+int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
+                 const std::vector<uint64_t>& out_off, const std::vector<uint64_t>& counts,
+                 const std::vector<uint64_t>& thresh, const std::vector<uint32_t>& ok,
+                 std::vector<PassOut>& passes, std::vector<uint32_t>& retry_local,
+                 std::vector<uint64_t>& final_size_local) {
+  sks_ctx* c = S.c;
+  hipStream_t st = c->stream;
+  const uint32_t k = (uint32_t)ok.size();
+  if (k == 0) return SKS_OK;
+  std::vector<uint64_t> src_off(k), cnt(k);
+  uint64_t max_len = 0;
+  for (uint32_t i = 0; i < k; ++i) {
+    src_off[i] = out_off[ok[i]];
+    cnt[i] = counts[ok[i]];
+    max_len = std::max(max_len, cnt[i]);
+  }
+  std::vector<uint64_t> csr = prefix(cnt);
+  const uint64_t T = csr[k];
+  const bool bottom = S.pol.kind == SKS_BOTTOM_S;
+
+  MetaArena arena(c);
+  size_t o_src = arena.add(src_off), o_csr = arena.add(csr), o_uniq = arena.add_zero(k);
+  SKS_TRY(arena.upload());
+  uint64_t* d_src = arena.ptr(o_src);
+  uint64_t* d_csr = arena.ptr(o_csr);
+  uint64_t* d_uniq = arena.ptr(o_uniq);
+
+  SKS_TRY(reserve_cols(c, {0, 1, 2, 3, 4, 5, 6, 7, 8, 9}, T + 1));
+  SKS_HIP(c->flag.reserve((T + 1) * sizeof(uint32_t)));
+  SKS_HIP(c->pos.reserve((T + 1) * sizeof(uint64_t)));
+  uint32_t* d_flag = reinterpret_cast<uint32_t*>(c->flag.ptr);
+  uint64_t* d_pos = reinterpret_cast<uint64_t*>(c->pos.ptr);
+  const uint64_t* rk = reinterpret_cast<uint64_t*>(c->rec[0].ptr);
+  const uint64_t* rv = reinterpret_cast<uint64_t*>(c->rec[1].ptr);
+  const uint64_t* rh = reinterpret_cast<uint64_t*>(c->rec[2].ptr);
+
+  // dense columns
+  SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st));
+  const bool has_val = bottom || S.wide;
+  if (has_val) SKS_HIP(sks::compact_regions(rv, col(c, 1), d_src, d_csr, k, max_len, st));
+  if (bottom && S.wide) SKS_HIP(sks::compact_regions(rh, col(c, 2), d_src, d_csr, k, max_len, st));
+
+  const int mask_lo_bits = end_bit_of(S.mask_lo);
+  const int mask_hi_bits = end_bit_of(S.mask_hi);
+  uint64_t max_thr = 0;
+  for (uint32_t i = 0; i < k; ++i) max_thr = std::max(max_thr, thresh[ok[i]]);
+
+  PassOut po;
+  for (uint32_t i = 0; i < k; ++i) po.segs.push_back(seg_ids[ok[i]]);
+  std::vector<uint64_t> uniq(k);
+
+  if (!bottom) {
+    const uint64_t* K;   // sorted unique columns source
+    const uint64_t* K2 = nullptr;
+    if (!S.wide) {
+      SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, mask_lo_bits, c->tmp, st));
+      K = col(c, 3);
+    } else {
+      // (lo, hi) -> sort by lo, then stable by hi  => ascending 128-bit order
+      SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), T, csr, d_csr, 64,
+                                  c->tmp, st));
+      SKS_HIP(sks::seg_sort_pairs(col(c, 4), col(c, 5), col(c, 3), col(c, 6), T, csr, d_csr,
+                                  mask_hi_bits, c->tmp, st));
+      K = col(c, 5);   // hi
+      K2 = col(c, 6);  // lo
+    }
+    SKS_HIP(sks::seg_unique_scan(K, K2, T, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
+    SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    SKS_HIP(hipStreamSynchronize(st));
+    po.off = prefix(uniq);
+    const uint64_t U = po.off[k];
+    SKS_TRY(alloc_u64(&po.d, U * S.ew));
+    if (!S.wide) {
+      SKS_HIP(sks::seg_unique_scatter(K, nullptr, T, d_csr, k, d_flag, d_pos, nullptr, nullptr,
+                                      po.d, nullptr, st));
+    } else {
+      SKS_HIP(sks::seg_unique_scatter(K2, K, T, d_csr, k, d_flag, d_pos, nullptr, nullptr,
+                                      col(c, 7), col(c, 8), st));
+      SKS_HIP(sks::launch_interleave(col(c, 7), col(c, 8), U, po.d, st));
+    }
+    for (uint32_t i = 0; i < k; ++i) final_size_local[ok[i]] = uniq[i];
+    passes.push_back(po);
+    return SKS_OK;
+  }
+
+  // bottom-s
+  const uint64_t s = S.pol.param;
+  const uint64_t* LO;  // columns ordered by (fmh, C)
+  const uint64_t* HI = nullptr;
+  if (!S.wide) {
+    SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), T, csr, d_csr,
+                                end_bit_of(max_thr), c->tmp, st));
+    LO = col(c, 4);
+    SKS_HIP(sks::seg_unique_scan(col(c, 3), nullptr, T, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
+  } else {
+    // order (fmh, hi, lo) by an index permutation (LSD: lo, hi, fmh)
+    uint64_t* idx = col(c, 9);
+    SKS_HIP(sks::launch_iota(idx, T, st));
+    SKS_HIP(sks::seg_sort_pairs(col(c, 1), col(c, 3), idx, col(c, 4), T, csr, d_csr, 64, c->tmp, st));
+    SKS_HIP(sks::launch_gather(col(c, 2), col(c, 4), T, col(c, 5), st));
+    SKS_HIP(sks::seg_sort_pairs(col(c, 5), col(c, 3), col(c, 4), col(c, 6), T, csr, d_csr,
+                                mask_hi_bits, c->tmp, st));
+    SKS_HIP(sks::launch_gather(col(c, 0), col(c, 6), T, col(c, 5), st));
+    SKS_HIP(sks::seg_sort_pairs(col(c, 5), col(c, 3), col(c, 6), col(c, 4), T, csr, d_csr,
+                                end_bit_of(max_thr), c->tmp, st));
+    SKS_HIP(sks::launch_gather(col(c, 1), col(c, 4), T, col(c, 7), st));  // lo
+    SKS_HIP(sks::launch_gather(col(c, 2), col(c, 4), T, col(c, 8), st));  // hi
+    LO = col(c, 7);
+    HI = col(c, 8);
+    SKS_HIP(sks::seg_unique_scan(LO, HI, T, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
+  }
+  SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SKS_HIP(hipStreamSynchronize(st));
+  std::vector<uint64_t> limit(k, 0);
+  std::vector<uint32_t> keep_segs;
+  std::vector<uint64_t> keep_off(1, 0);
+  for (uint32_t i = 0; i < k; ++i) {
+    const bool done = uniq[i] >= s || thresh[ok[i]] == ~0ull;
+    if (done) {
+      limit[i] = std::min<uint64_t>(s, uniq[i]);
+      final_size_local[ok[i]] = limit[i];
+      keep_segs.push_back(seg_ids[ok[i]]);
+      keep_off.push_back(keep_off.back() + limit[i]);
+    } else {
+      retry_local.push_back(ok[i]);  // too few candidates under the threshold
+    }
+  }
+  // not-done segments get limit 0, so this prefix is also keep_off's layout
+  std::vector<uint64_t> dst = prefix(limit);
+  const uint64_t U = dst[k];
+  MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
+  size_t o_csr2 = arena2.add(csr), o_lim = arena2.add(limit), o_dst = arena2.add(dst);
+  SKS_TRY(arena2.upload());
+  d_csr = arena2.ptr(o_csr2);
+  uint64_t* d_lim = arena2.ptr(o_lim);
+  uint64_t* d_dst = arena2.ptr(o_dst);
+  SKS_TRY(alloc_u64(&po.d, U * S.ew));
+  po.segs = keep_segs;
+  po.off = keep_off;
+  if (!S.wide) {
+    SKS_HIP(sks::seg_unique_scatter(LO, nullptr, T, d_csr, k, d_flag, d_pos, d_lim, d_dst,
+                                    col(c, 5), nullptr, st));
+    SKS_HIP(sks::seg_sort_keys(col(c, 5), po.d, U, dst, d_dst, mask_lo_bits, c->tmp, st));
+  } else {
+    SKS_HIP(sks::seg_unique_scatter(LO, HI, T, d_csr, k, d_flag, d_pos, d_lim, d_dst, col(c, 0),
+                                    col(c, 1), st));
+    SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), U, dst, d_dst, 64,
+                                c->tmp, st));
+    SKS_HIP(sks::seg_sort_pairs(col(c, 4), col(c, 5), col(c, 3), col(c, 6), U, dst, d_dst,
+                                mask_hi_bits, c->tmp, st));
+    SKS_HIP(sks::launch_interleave(col(c, 6), col(c, 5), U, po.d, st));
+  }
+  SKS_HIP(hipStreamSynchronize(st));
+  passes.push_back(po);
+  return SKS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const uint64_t* seg_off,
+                     uint32_t n_seg, int window, const uint64_t mask[2], const sks_policy* policy,
+                     sks_sketch_set** out) {
+  if (!c || !mask || !policy || !out || (!seg_off && n_seg))
+    return sks::fail(SKS_E_ARG, "sks_sketch_build: null argument");
+  *out = nullptr;
+  if (window < 1 || window > 64)
+    return sks::fail(SKS_E_ARG, "sks_sketch_build: window must be in [1, 64] (MAX_KMER_LENGTH)");
+  if (policy->kind != SKS_FRAC_MOD && policy->kind != SKS_BOTTOM_S)
+    return sks::fail(SKS_E_ARG, "sks_sketch_build: unknown policy kind");
+  if (policy->flavour != 0 && policy->flavour != 1)
+    return sks::fail(SKS_E_ARG, "sks_sketch_build: unknown hash flavour");
+  if (policy->param == 0) return sks::fail(SKS_E_ARG, "sks_sketch_build: policy param must be > 0");
+  {
+    const int bits = 2 * window;
+    uint64_t lo_allowed = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+    uint64_t hi_allowed = bits <= 64 ? 0 : (bits >= 128 ? ~0ull : ((1ull << (bits - 64)) - 1));
+    if ((mask[0] & ~lo_allowed) || (mask[1] & ~hi_allowed))
+      return sks::fail(SKS_E_UNSUPPORTED,
+                       "sks_sketch_build: mask has bits at or above 2*window (the reference's "
+                       "generate_random_spaced_seed_mask never produces such masks)");
+  }
+  if (n_bytes && !d_seq) return sks::fail(SKS_E_ARG, "sks_sketch_build: null sequence");
+  for (uint32_t g = 0; g < n_seg; ++g)
+    if (seg_off[g] > seg_off[g + 1] || seg_off[g + 1] > n_bytes)
+      return sks::fail(SKS_E_ARG, "sks_sketch_build: segment offsets must be non-decreasing and <= n_bytes");
+
+  DeviceGuard guard(c->device);
+  hipStream_t st = c->stream;
+  BuildState S{c, window, window > 32, window > 32 ? 2 : 1, mask[0], mask[1], *policy,
+               sks::fmh_const(mask[0], mask[1], window, policy->nonce, policy->flavour), {}};
+  if (policy->kind == SKS_FRAC_MOD) S.dt = sks::make_div_test(policy->param);
+  const bool bottom = policy->kind == SKS_BOTTOM_S;
+  const double alpha = 2.0;
+
+  sks_timings tm{};
+  SKS_HIP(hipEventRecord(c->ev_begin, st));
+
+  std::vector<uint64_t> thresh_g(n_seg, ~0ull), cap_g(n_seg), windows_g(n_seg, 0);
+  std::vector<uint64_t> final_size(n_seg, ~0ull);
+  for (uint32_t g = 0; g < n_seg; ++g) {
+    const uint64_t L = seg_off[g + 1] - seg_off[g];
+    double expect;
+    if (!bottom) {
+      expect = (double)L / (double)policy->param;
+    } else {
+      double want = alpha * (double)policy->param;
+      if ((double)L <= want) {
+        thresh_g[g] = ~0ull;
+        expect = (double)L;
+      } else {
+        long double t = (long double)want / (long double)L * 18446744073709551616.0L;
+        thresh_g[g] = t >= 18446744073709551615.0L ? ~0ull : (uint64_t)t;
+        expect = want;
+      }
+    }
+    double cap = expect + 6.0 * std::sqrt(expect) + 4096.0;
+    cap_g[g] = (uint64_t)std::min<double>(cap, (double)L + 1.0);
+  }
+
+  std::vector<PassOut> passes;
+  std::vector<uint32_t> pending(n_seg);
+  std::iota(pending.begin(), pending.end(), 0);
+  int guard_passes = 0;
+  while (!pending.empty()) {
+    if (++guard_passes > 64) {
+      free_passes(passes);
+      return sks::fail(SKS_E_HIP, "sks_sketch_build: selection did not converge");
+    }
+    const uint32_t m = (uint32_t)pending.size();
+    std::vector<uint64_t> beg(m), end(m), tp(m + 1, 0), thr(m), cap(m), ooff(m);
+    uint64_t total_cap = 0;
+    for (uint32_t i = 0; i < m; ++i) {
+      uint32_t g = pending[i];
+      beg[i] = seg_off[g];
+      end[i] = seg_off[g + 1];
+      tp[i + 1] = tp[i] + sks::scan_tiles_for(end[i] - beg[i]);
+      thr[i] = thresh_g[g];
+      cap[i] = cap_g[g];
+      ooff[i] = total_cap;
+      total_cap += cap[i];
+    }
+    const uint64_t n_tiles = tp[m];
+    for (int r = 0; r < (bottom && S.wide ? 3 : (bottom || S.wide ? 2 : 1)); ++r)
+      SKS_HIP(c->rec[r].reserve(std::max<uint64_t>(total_cap, 1) * sizeof(uint64_t)));
+    MetaArena arena(c);
+    size_t o_beg = arena.add(beg), o_end = arena.add(end), o_tp = arena.add(tp),
+           o_thr = arena.add(thr), o_cap = arena.add(cap), o_off = arena.add(ooff),
+           o_cnt = arena.add_zero(m), o_win = arena.add_zero(m);
+    SKS_TRY(arena.upload());
+
+    sks::ScanParams p{};
+    p.seq = d_seq;
+    p.seg_begin = arena.ptr(o_beg);
+    p.seg_end = arena.ptr(o_end);
+    p.tile_prefix = arena.ptr(o_tp);
+    p.n_seg = m;
+    p.n_tiles = n_tiles;
+    p.w = window;
+    p.mask_lo = S.mask_lo;
+    p.mask_hi = S.mask_hi;
+    p.kconst = S.kconst;
+    p.low_mask = S.dt.low_mask;
+    p.shift = S.dt.shift;
+    p.dinv = S.dt.dinv;
+    p.dlim = S.dt.dlim;
+    p.seg_thresh = arena.ptr(o_thr);
+    p.out_key = reinterpret_cast<uint64_t*>(c->rec[0].ptr);
+    p.out_val = reinterpret_cast<uint64_t*>(c->rec[1].ptr);
+    p.out_hi = reinterpret_cast<uint64_t*>(c->rec[2].ptr);
+    p.seg_out_off = arena.ptr(o_off);
+    p.seg_out_cap = arena.ptr(o_cap);
+    p.seg_count = reinterpret_cast<unsigned long long*>(arena.ptr(o_cnt));
+    p.seg_windows = reinterpret_cast<unsigned long long*>(arena.ptr(o_win));
+
+    SKS_HIP(hipEventRecord(c->ev_s0, st));
+    SKS_HIP(sks::launch_scan(p, bottom ? sks::kModeBottom : sks::kModeFrac, policy->flavour,
+                             S.wide, c->device, st, c->grid_override));
+    SKS_HIP(hipEventRecord(c->ev_s1, st));
+    tm.scan_launches += n_tiles ? 1 : 0;
+    std::vector<uint64_t> counts(m), wins(m);
+    SKS_HIP(hipMemcpyAsync(counts.data(), p.seg_count, m * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    SKS_HIP(hipMemcpyAsync(wins.data(), p.seg_windows, m * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    SKS_HIP(hipStreamSynchronize(st));
+    float ms = 0;
+    SKS_HIP(hipEventElapsedTime(&ms, c->ev_s0, c->ev_s1));
+    tm.scan_ms += ms;
+
+    std::vector<uint32_t> ok, next;
+    for (uint32_t i = 0; i < m; ++i) {
+      tm.survivors += counts[i];
+      if (counts[i] > cap[i]) {
+        cap_g[pending[i]] = counts[i];
+        next.push_back(pending[i]);
+      } else {
+        ok.push_back(i);
+        windows_g[pending[i]] = wins[i];
+      }
+    }
+    std::vector<uint32_t> retry_local;
+    std::vector<uint64_t> fsz(m, ~0ull);
+    int rc = post_process(S, pending, ooff, counts, thr, ok, passes, retry_local, fsz);
+    if (rc != SKS_OK) {
+      free_passes(passes);
+      return rc;
+    }
+    for (uint32_t i : ok)
+      if (fsz[i] != ~0ull) final_size[pending[i]] = fsz[i];
+    for (uint32_t i : retry_local) {
+      uint32_t g = pending[i];
+      uint64_t t = thresh_g[g];
+      thresh_g[g] = t > (~0ull >> 3) ? ~0ull : t * 8;
+      uint64_t L = seg_off[g + 1] - seg_off[g];
+      cap_g[g] = std::min<uint64_t>(L + 1, std::max<uint64_t>(cap_g[g], counts[i]) * 8 + 4096);
+      next.push_back(g);
+    }
+    std::sort(next.begin(), next.end());
+    pending.swap(next);
+  }
+
+  // assemble the final set in segment order
+  sks_sketch_set* set = new (std::nothrow) sks_sketch_set();
+  if (!set) {
+    free_passes(passes);
+    return sks::fail(SKS_E_NOMEM, "sks_sketch_build: out of memory");
+  }
+  set->device = c->device;
+  set->elem_words = S.ew;
+  set->n = n_seg;
+  set->sizes.resize(n_seg);
+  set->starts.resize(n_seg);
+  set->windows = windows_g;
+  uint64_t total = 0;
+  for (uint32_t g = 0; g < n_seg; ++g) {
+    set->starts[g] = total;
+    set->sizes[g] = (uint32_t)final_size[g];
+    total += final_size[g];
+  }
+  int rc = SKS_OK;
+  const bool single_in_order =
+      passes.size() == 1 && passes[0].segs.size() == n_seg &&
+      std::is_sorted(passes[0].segs.begin(), passes[0].segs.end());
+  if (single_in_order) {
+    set->d_data = passes[0].d;
+    passes[0].d = nullptr;
+  } else {
+    rc = alloc_u64(&set->d_data, total * S.ew);
+    for (size_t pi = 0; rc == SKS_OK && pi < passes.size(); ++pi) {
+      const PassOut& po = passes[pi];
+      const uint32_t k = (uint32_t)po.segs.size();
+      if (k == 0) continue;
+      std::vector<uint64_t> src(k + 1), dst(k + 1);
+      uint64_t max_len = 0;
+      for (uint32_t i = 0; i < k; ++i) {
+        src[i] = po.off[i] * S.ew;
+        dst[i] = set->starts[po.segs[i]] * S.ew;
+        max_len = std::max(max_len, (po.off[i + 1] - po.off[i]) * S.ew);
+      }
+      // compact_regions reads len from dst_off[g+1]-dst_off[g]: run one segment at a time
+      // via a per-segment CSR pair (dst, dst + len)
+      for (uint32_t i = 0; i < k && rc == SKS_OK; ++i) {
+        uint64_t len = (po.off[i + 1] - po.off[i]) * S.ew;
+        if (!len) continue;
+        if (hipMemcpyAsync(set->d_data + dst[i], po.d + src[i], len * sizeof(uint64_t),
+                           hipMemcpyDeviceToDevice, st) != hipSuccess)
+          rc = sks::fail(SKS_E_HIP, "sks_sketch_build: assembling copy failed");
+      }
+      (void)max_len;
+    }
+  }
+  if (rc == SKS_OK) rc = alloc_u64(&set->d_starts, n_seg);
+  if (rc == SKS_OK && hipMalloc(reinterpret_cast<void**>(&set->d_sizes),
+                                std::max<uint32_t>(n_seg, 1) * sizeof(uint32_t)) != hipSuccess)
+    rc = sks::fail(SKS_E_HIP, "sks_sketch_build: hipMalloc failed");
+  if (rc == SKS_OK && n_seg) {
+    if (hipMemcpyAsync(set->d_starts, set->starts.data(), n_seg * sizeof(uint64_t),
+                       hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(set->d_sizes, set->sizes.data(), n_seg * sizeof(uint32_t),
+                       hipMemcpyHostToDevice, st) != hipSuccess)
+      rc = sks::fail(SKS_E_HIP, "sks_sketch_build: metadata upload failed");
+  }
+  if (rc == SKS_OK && hipEventRecord(c->ev_end, st) != hipSuccess)
+    rc = sks::fail(SKS_E_HIP, "hipEventRecord failed");
+  if (rc == SKS_OK && hipStreamSynchronize(st) != hipSuccess)
+    rc = sks::fail(SKS_E_HIP, "hipStreamSynchronize failed");
+  free_passes(passes);
+  if (rc != SKS_OK) {
+    sks_sketch_set_free(set);
+    return rc;
+  }
+  float tot = 0;
+  (void)hipEventElapsedTime(&tot, c->ev_begin, c->ev_end);
+  tm.total_ms = tot;
+  tm.post_ms = tot - tm.scan_ms;
+  for (uint64_t wv : windows_g) tm.windows += wv;
+  c->last = tm;
+  *out = set;
+  return SKS_OK;
+}
+
+int sks_sketch_set_free(sks_sketch_set* set) {
+  if (!set) return SKS_OK;
+  DeviceGuard g(set->device);
+  if (set->d_data) (void)hipFree(set->d_data);
+  if (set->d_starts) (void)hipFree(set->d_starts);
+  if (set->d_sizes) (void)hipFree(set->d_sizes);
+  delete set;
+  return SKS_OK;
+}
+
+uint32_t sks_sketch_set_num(const sks_sketch_set* set) { return set ? set->n : 0; }
+
+int sks_sketch_set_elem_words(const sks_sketch_set* set) { return set ? set->elem_words : 0; }
+
+int sks_sketch_set_sizes(const sks_sketch_set* set, uint32_t* sizes) {
+  if (!set || !sizes) return sks::fail(SKS_E_ARG, "sks_sketch_set_sizes: null argument");
+  std::copy(set->sizes.begin(), set->sizes.end(), sizes);
+  return SKS_OK;
+}
+
+int sks_sketch_set_windows(const sks_sketch_set* set, uint64_t* windows) {
+  if (!set || !windows) return sks::fail(SKS_E_ARG, "sks_sketch_set_windows: null argument");
+  std::copy(set->windows.begin(), set->windows.end(), windows);
+  return SKS_OK;
+}
+
+int sks_sketch_set_starts(const sks_sketch_set* set, uint64_t* starts) {
+  if (!set || !starts) return sks::fail(SKS_E_ARG, "sks_sketch_set_starts: null argument");
+  std::copy(set->starts.begin(), set->starts.end(), starts);
+  return SKS_OK;
+}
+
+const uint64_t* sks_sketch_set_device_data(const sks_sketch_set* set) { return set ? set->d_data : nullptr; }
+const uint64_t* sks_sketch_set_device_starts(const sks_sketch_set* set) { return set ? set->d_starts : nullptr; }
+const uint32_t* sks_sketch_set_device_sizes(const sks_sketch_set* set) { return set ? set->d_sizes : nullptr; }
+
+int sks_sketch_set_copy(const sks_sketch_set* set, uint32_t i, uint64_t* out) {
+  if (!set) return sks::fail(SKS_E_ARG, "sks_sketch_set_copy: null set");
+  if (i >= set->n) return sks::fail(SKS_E_ARG, "sks_sketch_set_copy: index out of range");
+  if (!out && set->sizes[i]) return sks::fail(SKS_E_ARG, "sks_sketch_set_copy: null output");
+  DeviceGuard g(set->device);
+  uint64_t words = (uint64_t)set->sizes[i] * set->elem_words;
+  if (words)
+    SKS_HIP(hipMemcpy(out, set->d_data + set->starts[i] * set->elem_words, words * sizeof(uint64_t),
+                      hipMemcpyDeviceToHost));
+  return SKS_OK;
+}
+
+int sks_sketch_set_export(const sks_sketch_set* set, uint64_t* d_dst, uint64_t stride,
+                          uint32_t* d_sizes) {
+  if (!set || !d_dst || !d_sizes) return sks::fail(SKS_E_ARG, "sks_sketch_set_export: null argument");
+  for (uint32_t s : set->sizes)
+    if (s > stride) return sks::fail(SKS_E_ARG, "sks_sketch_set_export: stride smaller than a sketch");
+  DeviceGuard g(set->device);
+  SKS_HIP(sks::launch_export(set->d_data, set->d_starts, set->d_sizes, set->n, set->elem_words,
+                             d_dst, stride, d_sizes, nullptr));
+  SKS_HIP(hipStreamSynchronize(nullptr));
+  return SKS_OK;
+}
+
+// ---- intersections ----------------------------------------------------------------------------
+
+int sks_intersect_pairs(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
+                        const uint32_t* d_sizes, int elem_words, const int32_t* d_a,
+                        const int32_t* d_b, uint64_t n_pairs, int32_t* d_out) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_pairs: null ctx");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (n_pairs && (!d_starts || !d_sizes || !d_a || !d_b || !d_out))
+    return sks::fail(SKS_E_ARG, "sks_intersect_pairs: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  SKS_HIP(sks::launch_intersect_pairs(d_data, d_starts, d_sizes, elem_words, d_a, d_b, n_pairs,
+                                      d_out, c->stream));
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_intersect_all(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
+                      const uint32_t* d_sizes, int elem_words, uint32_t n, uint32_t row_begin,
+                      uint32_t row_end, int32_t* d_out) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_all: null ctx");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (row_begin > row_end || row_end > n) return sks::fail(SKS_E_ARG, "sks_intersect_all: bad row range");
+  if (row_end > row_begin && (!d_starts || !d_sizes || !d_out))
+    return sks::fail(SKS_E_ARG, "sks_intersect_all: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  SKS_HIP(sks::launch_intersect_all(d_data, d_starts, d_sizes, elem_words, n, row_begin, row_end,
+                                    d_out, c->stream));
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+// Device time of the last intersection call (after the stream has reached it).
+int sks_ctx_last_intersect_ms(sks_ctx* c, float* ms) {
+  if (!c || !ms) return sks::fail(SKS_E_ARG, "null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventSynchronize(c->ev_end));
+  SKS_HIP(hipEventElapsedTime(ms, c->ev_begin, c->ev_end));
+  return SKS_OK;
+}
+
+// ---- synthetic genomes ------------------------------------------------------------------------
+
+int sks_synth_bases(sks_ctx* c, uint8_t* d_out, uint64_t n, uint64_t seed, uint64_t mut_seed,
+                    double mut_rate, uint64_t pos_offset) {
+  if (!c || (n && !d_out)) return sks::fail(SKS_E_ARG, "sks_synth_bases: null argument");
+  uint64_t thr = 0;
+  if (mut_rate > 0) {
+    long double t = (long double)mut_rate * 18446744073709551616.0L;
+    thr = t >= 18446744073709551615.0L ? ~0ull : (uint64_t)t;
+  }
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::launch_synth(d_out, n, seed, mut_seed, thr, pos_offset, c->stream));
+  return SKS_OK;
+}
+
+}  // extern "C"

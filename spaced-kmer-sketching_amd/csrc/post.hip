@@ -1,0 +1,299 @@
+// Post-scan stages of the sketch build: survivor compaction, per-genome radix
+// sort, unique, bottom-s selection, export to a fixed-stride layout, and the
+// synthetic-genome generator used by the bench and tests.
+//
+// The reference collapses duplicate selected k-mers by inserting them into an
+// std::unordered_map (kmer.hpp:170-178).  Here a genome's survivors are
+// radix-sorted (rocPRIM) and run-length uniqued, which yields the same set and
+// leaves it sorted for the merge-based intersection kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "sks_hash.hpp"
+#include "sks_internal.hpp"
+
+namespace sks {
+
+hipError_t Scratch::reserve(size_t n) {
+  if (n <= bytes) return hipSuccess;
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  bytes = 0;
+  size_t want = std::max<size_t>(n, 1 << 20);
+  hipError_t e = hipMalloc(&ptr, want);
+  if (e == hipSuccess) bytes = want;
+  return e;
+}
+
+void Scratch::release() {
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  bytes = 0;
+}
+
+namespace {
+
+constexpr int kB = 256;
+constexpr uint64_t kBigSegment = 1ull << 21;  // device-wide sort per segment above this
+
+template <bool PAIRS>
+hipError_t sort_impl(const uint64_t* keys_in, uint64_t* keys_out, const uint64_t* vals_in,
+                     uint64_t* vals_out, uint64_t total, const std::vector<uint64_t>& host_off,
+                     const uint64_t* d_off, int end_bit, Scratch& tmp, hipStream_t s) {
+  const size_t n_seg = host_off.size() - 1;
+  if (total == 0) return hipSuccess;
+  uint64_t max_len = 0;
+  for (size_t g = 0; g < n_seg; ++g) max_len = std::max(max_len, host_off[g + 1] - host_off[g]);
+  if (end_bit < 1) end_bit = 1;
+  if (n_seg == 1 || max_len > kBigSegment || total >= (1ull << 32)) {
+    for (size_t g = 0; g < n_seg; ++g) {
+      uint64_t b = host_off[g], len = host_off[g + 1] - b;
+      if (len == 0) continue;
+      size_t need = 0;
+      hipError_t e;
+      if constexpr (PAIRS)
+        e = rocprim::radix_sort_pairs(nullptr, need, keys_in + b, keys_out + b, vals_in + b,
+                                      vals_out + b, len, 0, end_bit, s);
+      else
+        e = rocprim::radix_sort_keys(nullptr, need, keys_in + b, keys_out + b, len, 0, end_bit, s);
+      if (e != hipSuccess) return e;
+      if ((e = tmp.reserve(need)) != hipSuccess) return e;
+      need = tmp.bytes;
+      if constexpr (PAIRS)
+        e = rocprim::radix_sort_pairs(tmp.ptr, need, keys_in + b, keys_out + b, vals_in + b,
+                                      vals_out + b, len, 0, end_bit, s);
+      else
+        e = rocprim::radix_sort_keys(tmp.ptr, need, keys_in + b, keys_out + b, len, 0, end_bit, s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  size_t need = 0;
+  hipError_t e;
+  if constexpr (PAIRS)
+    e = rocprim::segmented_radix_sort_pairs(nullptr, need, keys_in, keys_out, vals_in, vals_out,
+                                            (unsigned)total, (unsigned)n_seg, d_off, d_off + 1, 0,
+                                            end_bit, s);
+  else
+    e = rocprim::segmented_radix_sort_keys(nullptr, need, keys_in, keys_out, (unsigned)total,
+                                           (unsigned)n_seg, d_off, d_off + 1, 0, end_bit, s);
+  if (e != hipSuccess) return e;
+  if ((e = tmp.reserve(need)) != hipSuccess) return e;
+  need = tmp.bytes;
+  if constexpr (PAIRS)
+    return rocprim::segmented_radix_sort_pairs(tmp.ptr, need, keys_in, keys_out, vals_in, vals_out,
+                                               (unsigned)total, (unsigned)n_seg, d_off, d_off + 1,
+                                               0, end_bit, s);
+  else
+    return rocprim::segmented_radix_sort_keys(tmp.ptr, need, keys_in, keys_out, (unsigned)total,
+                                              (unsigned)n_seg, d_off, d_off + 1, 0, end_bit, s);
+}
+
+__global__ void k_compact(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                          const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ dst_off) {
+  const uint32_t g = blockIdx.y;
+  const uint64_t len = dst_off[g + 1] - dst_off[g];
+  const uint64_t so = src_off[g], d0 = dst_off[g];
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < len; i += (uint64_t)gridDim.x * kB)
+    dst[d0 + i] = src[so + i];
+}
+
+__global__ void k_flags(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ keys2,
+                        const uint64_t* __restrict__ off, uint32_t* __restrict__ flag) {
+  const uint32_t g = blockIdx.y;
+  const uint64_t b = off[g], e = off[g + 1];
+  for (uint64_t i = b + (uint64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (uint64_t)gridDim.x * kB) {
+    bool first = (i == b) || keys[i] != keys[i - 1] || (keys2 && keys2[i] != keys2[i - 1]);
+    flag[i] = first ? 1u : 0u;
+  }
+}
+
+__global__ void k_uniq_counts(const uint64_t* __restrict__ pos, const uint64_t* __restrict__ off,
+                              uint32_t n_seg, uint64_t* __restrict__ uniq) {
+  uint32_t g = blockIdx.x * kB + threadIdx.x;
+  if (g < n_seg) uniq[g] = pos[off[g + 1]] - pos[off[g]];
+}
+
+__global__ void k_scatter(const uint64_t* __restrict__ vals, const uint64_t* __restrict__ vals2,
+                          const uint64_t* __restrict__ off, const uint32_t* __restrict__ flag,
+                          const uint64_t* __restrict__ pos, const uint64_t* __restrict__ limit,
+                          const uint64_t* __restrict__ dst_off, uint64_t* __restrict__ out,
+                          uint64_t* __restrict__ out2) {
+  const uint32_t g = blockIdx.y;
+  const uint64_t b = off[g], e = off[g + 1];
+  const uint64_t p0 = pos[b], lim = limit ? limit[g] : ~0ull, d0 = dst_off ? dst_off[g] : p0;
+  for (uint64_t i = b + (uint64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (uint64_t)gridDim.x * kB) {
+    if (!flag[i]) continue;
+    uint64_t r = pos[i] - p0;
+    if (r < lim) {
+      out[d0 + r] = vals[i];
+      if (out2) out2[d0 + r] = vals2[i];
+    }
+  }
+}
+
+__global__ void k_synth(uint8_t* __restrict__ out, uint64_t n, uint64_t seed, uint64_t mut_seed,
+                        uint64_t mut_thresh, uint64_t pos_offset) {
+  // 16 bytes per thread, one 16-B store
+  const uint64_t i0 = ((uint64_t)blockIdx.x * kB + threadIdx.x) * 16;
+  if (i0 >= n) return;
+  uint32_t w[4] = {0, 0, 0, 0};
+  const uint32_t lut = 0x54474341u;  // "ACGT"
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint64_t p = pos_offset + i0 + k;
+    uint32_t b = (uint32_t)(splitmix64_at(seed, p) >> 62);
+    if (mut_thresh) {
+      uint64_t u = splitmix64_at(mut_seed, p);
+      if (u < mut_thresh) b = (b + 1 + (uint32_t)((u >> 32) % 3)) & 3;
+    }
+    w[k >> 2] |= ((lut >> (8 * b)) & 0xFFu) << (8 * (k & 3));
+  }
+  if (i0 + 16 <= n) {
+    *reinterpret_cast<uint4*>(out + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+    for (int k = 0; i0 + k < n; ++k) out[i0 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+__global__ void k_export(const uint64_t* __restrict__ data, const uint64_t* __restrict__ starts,
+                         const uint32_t* __restrict__ sizes, int ew, uint64_t* __restrict__ dst,
+                         uint64_t stride, uint32_t* __restrict__ dst_sizes) {
+  const uint32_t g = blockIdx.y;
+  const uint64_t n = (uint64_t)sizes[g] * ew, src = starts[g] * ew, d = (uint64_t)g * stride * ew;
+  const uint64_t cap = stride * ew;
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * kB)
+    dst[d + i] = i < n ? data[src + i] : ~0ull;
+  if (blockIdx.x == 0 && threadIdx.x == 0) dst_sizes[g] = sizes[g];
+}
+
+__global__ void k_interleave(const uint64_t* __restrict__ lo, const uint64_t* __restrict__ hi,
+                             uint64_t n, uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kB) {
+    out[2 * i] = lo[i];
+    out[2 * i + 1] = hi[i];
+  }
+}
+
+__global__ void k_iota(uint64_t* __restrict__ out, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kB)
+    out[i] = i;
+}
+
+__global__ void k_gather(const uint64_t* __restrict__ src, const uint64_t* __restrict__ idx,
+                         uint64_t n, uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kB)
+    out[i] = src[idx[i]];
+}
+
+inline unsigned grid_for(uint64_t n) {
+  uint64_t g = (n + kB - 1) / kB;
+  return (unsigned)std::min<uint64_t>(std::max<uint64_t>(g, 1), 65535);
+}
+
+}  // namespace
+
+hipError_t seg_sort_keys(const uint64_t* keys_in, uint64_t* keys_out, uint64_t total,
+                         const std::vector<uint64_t>& host_off, const uint64_t* d_off, int end_bit,
+                         Scratch& tmp, hipStream_t s) {
+  return sort_impl<false>(keys_in, keys_out, nullptr, nullptr, total, host_off, d_off, end_bit,
+                          tmp, s);
+}
+
+hipError_t seg_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const uint64_t* vals_in,
+                          uint64_t* vals_out, uint64_t total, const std::vector<uint64_t>& host_off,
+                          const uint64_t* d_off, int end_bit, Scratch& tmp, hipStream_t s) {
+  return sort_impl<true>(keys_in, keys_out, vals_in, vals_out, total, host_off, d_off, end_bit,
+                         tmp, s);
+}
+
+hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d_src_off,
+                           const uint64_t* d_dst_off, uint32_t n_seg, uint64_t max_len,
+                           hipStream_t s) {
+  if (n_seg == 0 || max_len == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_compact, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, src, dst,
+                     d_src_off, d_dst_off);
+  return hipGetLastError();
+}
+
+hipError_t seg_unique_scan(const uint64_t* keys, const uint64_t* keys2, uint64_t total,
+                           const uint64_t* d_off, uint32_t n_seg, uint32_t* d_flag, uint64_t* d_pos,
+                           uint64_t* d_uniq, Scratch& tmp, hipStream_t s) {
+  if (n_seg == 0) return hipSuccess;
+  hipError_t e;
+  if (total) {
+    // max segment length bound: total (grid-stride loop covers any length)
+    hipLaunchKernelGGL(k_flags, dim3(grid_for(std::min<uint64_t>(total, 1ull << 24)), n_seg),
+                       dim3(kB), 0, s, keys, keys2, d_off, d_flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if ((e = hipMemsetAsync(d_flag + total, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+  size_t need = 0;
+  e = rocprim::exclusive_scan(nullptr, need, d_flag, d_pos, (uint64_t)0, (size_t)(total + 1),
+                              rocprim::plus<uint64_t>(), s);
+  if (e != hipSuccess) return e;
+  if ((e = tmp.reserve(need)) != hipSuccess) return e;
+  need = tmp.bytes;
+  e = rocprim::exclusive_scan(tmp.ptr, need, d_flag, d_pos, (uint64_t)0, (size_t)(total + 1),
+                              rocprim::plus<uint64_t>(), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_uniq_counts, dim3((n_seg + kB - 1) / kB), dim3(kB), 0, s, d_pos, d_off,
+                     n_seg, d_uniq);
+  return hipGetLastError();
+}
+
+hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint64_t total,
+                              const uint64_t* d_off, uint32_t n_seg, const uint32_t* d_flag,
+                              const uint64_t* d_pos, const uint64_t* d_limit,
+                              const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
+                              hipStream_t s) {
+  if (n_seg == 0 || total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter, dim3(grid_for(std::min<uint64_t>(total, 1ull << 24)), n_seg),
+                     dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos, d_limit, d_dst_off, out,
+                     out2);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,
+                        uint64_t mut_thresh, uint64_t pos_offset, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint64_t threads = (n + 15) / 16;
+  uint64_t blocks = (threads + kB - 1) / kB;
+  hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(kB), 0, s, out, n, seed, mut_seed,
+                     mut_thresh, pos_offset);
+  return hipGetLastError();
+}
+
+hipError_t launch_export(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                         uint32_t n, int elem_words, uint64_t* dst, uint64_t stride,
+                         uint32_t* dst_sizes, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_export, dim3(grid_for(stride * elem_words), n), dim3(kB), 0, s, data, starts,
+                     sizes, elem_words, dst, stride, dst_sizes);
+  return hipGetLastError();
+}
+
+hipError_t launch_iota(uint64_t* out, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_iota, dim3(grid_for(n)), dim3(kB), 0, s, out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
+                         hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(kB), 0, s, src, idx, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_interleave(const uint64_t* lo, const uint64_t* hi, uint64_t n, uint64_t* out,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_interleave, dim3(grid_for(n)), dim3(kB), 0, s, lo, hi, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace sks

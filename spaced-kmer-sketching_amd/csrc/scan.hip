@@ -1,0 +1,498 @@
+// Kernel 1 — fused spaced-seed sketch scan for gfx950.
+//
+// One pass over the sequence bytes computes, for every window start, exactly
+// what the reference's hot loop computes (kmer_sliding.cpp:112-186):
+//   forward window F  (kmer_sliding.cpp:26-31:  F <<= 2; F[0..1] = base)
+//   reverse-complement window R (:42-47: R >>= 2; R[2w-2..2w-1] = base ^ 3)
+//   canonical C = min(F & M, R & M), ties -> R & M (same value)   (:159-175)
+//   fmh = H(C) ^ H(M) ^ w ^ nonce   (kmer.hpp:141-148, boost hash flavour)
+// and applies the selection policy (FracMinHash `fmh % c == 0`, or the
+// bottom-s pre-filter `fmh <= threshold`) in the same kernel.  Bytes that are
+// not A/C/G/T (either case) split runs exactly like
+// fasta_processing.cpp:144-179; a window is valid iff all its w bytes are
+// ACGT and lie inside its segment, so k-mers never span runs or genomes.
+//
+// Structure (MI355X): persistent grid, each workgroup streams a contiguous
+// range of 4096-window tiles.  A tile's bytes arrive with 16-B coalesced
+// loads (prefetched one tile ahead into registers), are packed once into
+// 2-bit words in LDS (a big-endian stream for F, a complemented little-endian
+// stream for R, a 1-bit invalid map), and every lane then owns 16 consecutive
+// window starts, extracting F and R with funnel shifts (v_alignbit_b32).
+// Survivors (~1/c of windows) go to an LDS queue flushed with one global
+// atomic per flush, so the global counters see a few thousand atomics per
+// launch instead of one per survivor.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sks_hash.hpp"
+#include "sks_internal.hpp"
+
+namespace sks {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWPT = 16;                  // windows per lane
+constexpr int kTile = kBlock * kWPT;      // 4096 window starts per tile
+constexpr int kHaloWords = 4;             // 64 extra bases (>= w - 1 for w <= 64)
+constexpr int kWords = kBlock + kHaloWords;            // 2-bit words per tile (16 bases each)
+constexpr int kLoadVecs = (kWords * 16 + 16) / 16;      // 16-B loads per tile (+1 for alignment)
+constexpr int kQCap = 2048;               // LDS survivor queue entries
+constexpr unsigned char kSep = '\n';      // any non-ACGT byte
+
+struct Geom {
+  uint64_t win0;    // byte index of the tile's first window start
+  uint64_t seg_end; // end byte of the segment
+  uint32_t seg;
+};
+
+// Scalar (wave-uniform) segment cursor: advance `seg` until tile is inside it.
+__device__ __forceinline__ Geom tile_geom(const ScanParams& p, uint64_t tile, uint32_t& seg) {
+  while (seg + 1 < p.n_seg && tile >= p.tile_prefix[seg + 1]) ++seg;
+  Geom g;
+  g.seg = seg;
+  g.win0 = p.seg_begin[seg] + (tile - p.tile_prefix[seg]) * (uint64_t)kTile;
+  g.seg_end = p.seg_end[seg];
+  return g;
+}
+
+// Load the 16-B vector #k of a tile: bytes [base + 16k, base + 16k + 16) where
+// `base` (relative to seq, possibly negative) is 16-B aligned in absolute
+// address terms, so every vector load is aligned even when the caller's
+// sequence pointer is not.  Bytes at or past seg_end read as a separator.
+__device__ __forceinline__ uint4 load_vec(const uint8_t* __restrict__ seq, int64_t base, int k,
+                                          int64_t seg_end) {
+  int64_t a = base + 16 * (int64_t)k;
+  if (a + 16 <= seg_end) return *reinterpret_cast<const uint4*>(seq + a);
+  uint32_t wv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      int64_t pos = a + 4 * q + b;
+      uint32_t ch = pos < seg_end ? seq[pos] : kSep;
+      v |= ch << (8 * b);
+    }
+    wv[q] = v;
+  }
+  return make_uint4(wv[0], wv[1], wv[2], wv[3]);
+}
+
+// Offset of win0 inside its absolutely aligned 16-B chunk.
+__device__ __forceinline__ uint32_t align_shift(const uint8_t* seq, uint64_t win0) {
+  return (uint32_t)(((uintptr_t)seq + win0) & 15u);
+}
+
+// 4 ASCII bytes -> 8 bits of little-endian 2-bit codes + 4 invalid bits.
+// code = ((c >> 1) ^ (c >> 2)) & 3 maps A/a C/c G/g T/t to 0 1 2 3
+// (fasta_processing.cpp:35-69); a byte is valid iff it equals "acgt"[code]
+// after lower-casing.
+__device__ __forceinline__ void encode4(uint32_t x, uint32_t& le8, uint32_t& inv4) {
+  uint32_t low = x | 0x20202020u;
+  uint32_t code = ((low >> 1) ^ (low >> 2)) & 0x03030303u;
+  uint32_t expect = __builtin_amdgcn_perm(0u, 0x74676361u, code);  // bytes 'a','c','g','t'
+  uint32_t eq = expect ^ low;
+  uint32_t t = (eq & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  t = ~(t | eq | 0x7F7F7F7Fu);             // 0x80 in every byte where eq == 0
+  uint32_t bad = (~t) & 0x80808080u;       // 0x80 in every invalid byte
+  inv4 = (bad * 0x00204081u) >> 28;        // gather bits 7,15,23,31 -> 0..3
+  uint32_t y = code | (code >> 6);
+  le8 = (y | (y >> 12)) & 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t rev_pairs(uint32_t x) {
+  uint32_t r = __builtin_bitreverse32(x);
+  return ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+template <int MODE>
+struct Queue {
+  uint64_t key[kQCap];
+  uint64_t val[MODE == kModeBottom ? kQCap : 1];
+  uint32_t n;
+  unsigned long long base;
+};
+
+template <int MODE>
+__device__ __forceinline__ void emit(const ScanParams& p, Queue<MODE>& q, uint32_t seg,
+                                     uint64_t key, uint64_t val) {
+  uint32_t slot = atomicAdd(&q.n, 1u);
+  if (slot < kQCap) {
+    q.key[slot] = key;
+    if constexpr (MODE == kModeBottom) q.val[slot] = val;
+  } else {  // queue full: rare direct path
+    unsigned long long g = atomicAdd(&p.seg_count[seg], 1ull);
+    if (g < p.seg_out_cap[seg]) {
+      uint64_t o = p.seg_out_off[seg] + g;
+      p.out_key[o] = key;
+      if constexpr (MODE == kModeBottom) p.out_val[o] = val;
+    }
+  }
+}
+
+// Block-wide flush of the LDS queue to segment `seg` (call from all threads).
+template <int MODE>
+__device__ __forceinline__ void flush(const ScanParams& p, Queue<MODE>& q, uint32_t seg) {
+  __syncthreads();
+  uint32_t n = q.n < kQCap ? q.n : kQCap;
+  if (n) {
+    if (threadIdx.x == 0) q.base = atomicAdd(&p.seg_count[seg], (unsigned long long)n);
+    __syncthreads();
+    uint64_t base = q.base;
+    uint64_t cap = p.seg_out_cap[seg];
+    uint64_t off = p.seg_out_off[seg];
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+      if (base + i < cap) {
+        p.out_key[off + base + i] = q.key[i];
+        if constexpr (MODE == kModeBottom) p.out_val[off + base + i] = q.val[i];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) q.n = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void add_windows(const ScanParams& p, uint32_t seg, uint32_t cnt) {
+  // wave reduction, one atomic per wave
+  uint32_t v = cnt;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&p.seg_windows[seg], (unsigned long long)v);
+}
+
+// Hash + selection predicate + emit for one canonical k-mer (w <= 32).
+template <int MODE, int FLAVOUR>
+__device__ __forceinline__ void select_window(const ScanParams& p, Queue<MODE>& q, uint32_t seg,
+                                              uint64_t thresh, bool valid, uint64_t c) {
+  uint64_t h;
+  if constexpr (FLAVOUR == 0) {
+    h = hash_mix(c + kGolden32);                // combine(0, lo)
+    h = hash_mix(h + kGolden32);                // combine(h, hi = 0)
+    h = hash_mix(h + (128 + kGolden32));        // combine(num_bits = 128, h)
+  } else {
+    h = hash_bitset128<1>(c, 0);
+  }
+  uint64_t f = h ^ p.kconst;
+  bool keep;
+  if constexpr (MODE == kModeFrac) keep = div_test(f, p.low_mask, p.shift, p.dinv, p.dlim);
+  else keep = f <= thresh;
+  if (valid && keep) {
+    if constexpr (MODE == kModeFrac) emit<MODE>(p, q, seg, c, 0);
+    else emit<MODE>(p, q, seg, f, c);
+  }
+}
+
+template <int MODE, int FLAVOUR>
+__global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
+  __shared__ uint32_t s_raw[kLoadVecs * 4];
+  __shared__ uint32_t s_be[kWords + 2];
+  __shared__ uint32_t s_lc[kWords + 2];
+  __shared__ uint32_t s_inv[kWords + 2];
+  __shared__ Queue<MODE> q;
+
+  const int tid = threadIdx.x;
+  const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
+  const uint64_t t_end = (uint64_t)(blockIdx.x + 1) * p.n_tiles / gridDim.x;
+  if (tid == 0) q.n = 0;
+  if (t_begin >= t_end) return;
+
+  const int w = p.w;
+  const uint32_t fshift = 64 - 2 * w;            // F right-alignment (w <= 32)
+  const uint64_t wmask_bits = (w >= 64) ? ~0ull : ((1ull << w) - 1);
+  const uint64_t region_bits = (kWPT - 1 + w >= 64) ? ~0ull : ((1ull << (kWPT - 1 + w)) - 1);
+
+  // segment cursors (wave-uniform) for the current tile and the prefetch
+  uint32_t seg_lo = 0, seg_hi = p.n_seg;
+  while (seg_lo + 1 < seg_hi) {  // last segment with tile_prefix[seg] <= t_begin
+    uint32_t mid = (seg_lo + seg_hi) >> 1;
+    if (p.tile_prefix[mid] <= t_begin) seg_lo = mid; else seg_hi = mid;
+  }
+  uint32_t cur_seg = seg_lo, pf_seg = seg_lo;
+
+  // prefetch the first tile
+  Geom pg = tile_geom(p, t_begin, pf_seg);
+  int64_t pf_base = (int64_t)pg.win0 - align_shift(p.seq, pg.win0);
+  uint4 v0 = load_vec(p.seq, pf_base, tid, (int64_t)pg.seg_end);
+  uint4 v1 = make_uint4(0, 0, 0, 0);
+  if (tid < kLoadVecs - kBlock) v1 = load_vec(p.seq, pf_base, kBlock + tid, (int64_t)pg.seg_end);
+
+  uint32_t win_count = 0;
+  uint32_t count_seg = cur_seg;
+
+  for (uint64_t tile = t_begin; tile < t_end; ++tile) {
+    Geom g = tile_geom(p, tile, cur_seg);
+    if (g.seg != count_seg) {  // segment change: publish the previous segment
+      add_windows(p, count_seg, win_count);
+      win_count = 0;
+      flush<MODE>(p, q, count_seg);
+      count_seg = g.seg;
+    }
+    const uint32_t shift = align_shift(p.seq, g.win0);
+    const uint64_t thresh = (MODE == kModeBottom) ? p.seg_thresh[g.seg] : 0;
+
+    // 1) raw bytes -> LDS
+    reinterpret_cast<uint4*>(s_raw)[tid] = v0;
+    if (tid < kLoadVecs - kBlock) reinterpret_cast<uint4*>(s_raw)[kBlock + tid] = v1;
+    __syncthreads();
+
+    // 2) pack: word i covers bases [16 i, 16 i + 16) of the tile
+    for (int i = tid; i < kWords; i += kBlock) {
+      const uint32_t b0 = 16 * i + shift;  // byte offset in s_raw
+      const uint32_t wi = b0 >> 2, sb = (b0 & 3) * 8;
+      uint32_t x[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) x[k] = s_raw[wi + k];
+      uint32_t le = 0, inv = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t word = sb ? funnel(x[k + 1], x[k], sb) : x[k];
+        uint32_t le8, inv4;
+        encode4(word, le8, inv4);
+        le |= le8 << (8 * k);
+        inv |= inv4 << (4 * k);
+      }
+      s_be[i] = rev_pairs(le);
+      s_lc[i] = ~le;
+      s_inv[i] = inv;
+    }
+    __syncthreads();
+
+    // 3) prefetch the next tile while this one is hashed
+    if (tile + 1 < t_end) {
+      Geom ng = tile_geom(p, tile + 1, pf_seg);
+      pf_base = (int64_t)ng.win0 - align_shift(p.seq, ng.win0);
+      v0 = load_vec(p.seq, pf_base, tid, (int64_t)ng.seg_end);
+      if (tid < kLoadVecs - kBlock) v1 = load_vec(p.seq, pf_base, kBlock + tid, (int64_t)ng.seg_end);
+    }
+
+    // 4) 16 windows per lane: starts 16*tid + j
+    const uint32_t be0 = s_be[tid], be1 = s_be[tid + 1], be2 = s_be[tid + 2];
+    const uint32_t lc0 = s_lc[tid], lc1 = s_lc[tid + 1], lc2 = s_lc[tid + 2];
+    const uint64_t inv64 = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) |
+                           ((uint64_t)s_inv[tid + 2] << 32) | ((uint64_t)s_inv[tid + 3] << 48);
+    const bool lane_clean = (inv64 & region_bits) == 0;
+    const bool wave_clean = __all(lane_clean);
+
+#pragma unroll
+    for (int j = 0; j < kWPT; ++j) {
+      uint32_t fh = j ? funnel(be0, be1, 32 - 2 * j) : be0;
+      uint32_t fl = j ? funnel(be1, be2, 32 - 2 * j) : be1;
+      uint64_t F = ((((uint64_t)fh) << 32) | fl) >> fshift;
+      uint32_t rl = j ? funnel(lc1, lc0, 2 * j) : lc0;
+      uint32_t rh = j ? funnel(lc2, lc1, 2 * j) : lc1;
+      uint64_t R = (((uint64_t)rh) << 32) | rl;
+      uint64_t fm = F & p.mask_lo, rm = R & p.mask_lo;
+      uint64_t c = fm < rm ? fm : rm;
+      bool valid = wave_clean || (((inv64 >> j) & wmask_bits) == 0);
+      win_count += valid ? 1u : 0u;
+      select_window<MODE, FLAVOUR>(p, q, g.seg, thresh, valid, c);
+    }
+
+    // 5) flush the queue once it is half full
+    __syncthreads();
+    if (q.n >= kQCap / 2) flush<MODE>(p, q, g.seg);
+  }
+  add_windows(p, count_seg, win_count);
+  flush<MODE>(p, q, count_seg);
+}
+
+// ---- wide path: 32 < w <= 64 (128-bit windows) -------------------------------------
+// Same structure; F and R are 128-bit.  Survivors carry (lo, hi) in (key, val)
+// for FracMinHash and (fmh, lo) + hi in a side array for bottom-s.
+template <int MODE, int FLAVOUR>
+__global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
+  __shared__ uint32_t s_raw[kLoadVecs * 4];
+  __shared__ uint32_t s_be[kWords + 2];
+  __shared__ uint32_t s_lc[kWords + 2];
+  __shared__ uint32_t s_inv[kWords + 2];
+  __shared__ uint64_t q_a[kQCap / 2], q_b[kQCap / 2], q_c[kQCap / 2];
+  __shared__ uint32_t q_n;
+  __shared__ unsigned long long q_base;
+
+  const int tid = threadIdx.x;
+  const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
+  const uint64_t t_end = (uint64_t)(blockIdx.x + 1) * p.n_tiles / gridDim.x;
+  if (tid == 0) q_n = 0;
+  if (t_begin >= t_end) return;
+  constexpr uint32_t cap = kQCap / 2;
+
+  const int w = p.w;
+  const uint32_t fshift = 128 - 2 * w;  // 0..62
+  const uint64_t wmask_bits = (w >= 64) ? ~0ull : ((1ull << w) - 1);
+
+  uint32_t seg_lo = 0, seg_hi = p.n_seg;
+  while (seg_lo + 1 < seg_hi) {
+    uint32_t mid = (seg_lo + seg_hi) >> 1;
+    if (p.tile_prefix[mid] <= t_begin) seg_lo = mid; else seg_hi = mid;
+  }
+  uint32_t cur_seg = seg_lo, pf_seg = seg_lo;
+  Geom pg = tile_geom(p, t_begin, pf_seg);
+  int64_t pf_base = (int64_t)pg.win0 - align_shift(p.seq, pg.win0);
+  uint4 v0 = load_vec(p.seq, pf_base, tid, (int64_t)pg.seg_end);
+  uint4 v1 = make_uint4(0, 0, 0, 0);
+  if (tid < kLoadVecs - kBlock) v1 = load_vec(p.seq, pf_base, kBlock + tid, (int64_t)pg.seg_end);
+  uint32_t win_count = 0;
+  uint32_t count_seg = cur_seg;
+
+  auto wflush = [&](uint32_t seg) {
+    __syncthreads();
+    uint32_t n = q_n < cap ? q_n : cap;
+    if (n) {
+      if (tid == 0) q_base = atomicAdd(&p.seg_count[seg], (unsigned long long)n);
+      __syncthreads();
+      uint64_t base = q_base, c = p.seg_out_cap[seg], off = p.seg_out_off[seg];
+      for (uint32_t i = tid; i < n; i += kBlock)
+        if (base + i < c) {
+          p.out_key[off + base + i] = q_a[i];
+          p.out_val[off + base + i] = q_b[i];
+          if (MODE == kModeBottom) p.out_hi[off + base + i] = q_c[i];
+        }
+    }
+    __syncthreads();
+    if (tid == 0) q_n = 0;
+    __syncthreads();
+  };
+
+  for (uint64_t tile = t_begin; tile < t_end; ++tile) {
+    Geom g = tile_geom(p, tile, cur_seg);
+    if (g.seg != count_seg) {
+      add_windows(p, count_seg, win_count);
+      win_count = 0;
+      wflush(count_seg);
+      count_seg = g.seg;
+    }
+    const uint32_t shift = align_shift(p.seq, g.win0);
+    const uint64_t thresh = (MODE == kModeBottom) ? p.seg_thresh[g.seg] : 0;
+    reinterpret_cast<uint4*>(s_raw)[tid] = v0;
+    if (tid < kLoadVecs - kBlock) reinterpret_cast<uint4*>(s_raw)[kBlock + tid] = v1;
+    __syncthreads();
+    for (int i = tid; i < kWords; i += kBlock) {
+      const uint32_t b0 = 16 * i + shift;
+      const uint32_t wi = b0 >> 2, sb = (b0 & 3) * 8;
+      uint32_t x[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) x[k] = s_raw[wi + k];
+      uint32_t le = 0, inv = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t word = sb ? funnel(x[k + 1], x[k], sb) : x[k];
+        uint32_t le8, inv4;
+        encode4(word, le8, inv4);
+        le |= le8 << (8 * k);
+        inv |= inv4 << (4 * k);
+      }
+      s_be[i] = rev_pairs(le);
+      s_lc[i] = ~le;
+      s_inv[i] = inv;
+    }
+    __syncthreads();
+    if (tile + 1 < t_end) {
+      Geom ng = tile_geom(p, tile + 1, pf_seg);
+      pf_base = (int64_t)ng.win0 - align_shift(p.seq, ng.win0);
+      v0 = load_vec(p.seq, pf_base, tid, (int64_t)ng.seg_end);
+      if (tid < kLoadVecs - kBlock) v1 = load_vec(p.seq, pf_base, kBlock + tid, (int64_t)ng.seg_end);
+    }
+    uint32_t be[5], lc[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { be[k] = s_be[tid + k]; lc[k] = s_lc[tid + k]; }
+    // 80 invalid bits: bases [16 tid, 16 tid + 80)
+    const uint64_t inv_lo = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) |
+                            ((uint64_t)s_inv[tid + 2] << 32) | ((uint64_t)s_inv[tid + 3] << 48);
+    const uint64_t inv_hi = (uint64_t)s_inv[tid + 4];
+#pragma unroll
+    for (int j = 0; j < kWPT; ++j) {
+      // 128 BE bits of bases [16 tid + j, 16 tid + j + 64)
+      uint32_t f3 = j ? funnel(be[0], be[1], 32 - 2 * j) : be[0];
+      uint32_t f2 = j ? funnel(be[1], be[2], 32 - 2 * j) : be[1];
+      uint32_t f1 = j ? funnel(be[2], be[3], 32 - 2 * j) : be[2];
+      uint32_t f0 = j ? funnel(be[3], be[4], 32 - 2 * j) : be[3];
+      uint64_t Fh = ((uint64_t)f3 << 32) | f2, Fl = ((uint64_t)f1 << 32) | f0;
+      // >> fshift (0..62)
+      if (fshift) { Fl = (Fl >> fshift) | (Fh << (64 - fshift)); Fh >>= fshift; }
+      uint32_t r0 = j ? funnel(lc[1], lc[0], 2 * j) : lc[0];
+      uint32_t r1 = j ? funnel(lc[2], lc[1], 2 * j) : lc[1];
+      uint32_t r2 = j ? funnel(lc[3], lc[2], 2 * j) : lc[2];
+      uint32_t r3 = j ? funnel(lc[4], lc[3], 2 * j) : lc[3];
+      uint64_t Rl = ((uint64_t)r1 << 32) | r0, Rh = ((uint64_t)r3 << 32) | r2;
+      uint64_t fml = Fl & p.mask_lo, fmh = Fh & p.mask_hi;
+      uint64_t rml = Rl & p.mask_lo, rmh = Rh & p.mask_hi;
+      bool f_lt = (fmh < rmh) || (fmh == rmh && fml < rml);
+      uint64_t cl = f_lt ? fml : rml, ch = f_lt ? fmh : rmh;
+      // window bits [j, j + w) of the 80-bit invalid map
+      uint64_t iv = (inv_lo >> j) | (j ? (inv_hi << (64 - j)) : 0);
+      bool valid = (iv & wmask_bits) == 0;
+      win_count += valid ? 1u : 0u;
+      uint64_t h;
+      if constexpr (FLAVOUR == 0) {
+        h = hash_mix(cl + kGolden32);
+        h = hash_mix(h + kGolden32 + ch);
+        h = hash_mix(h + (128 + kGolden32));
+      } else {
+        h = hash_bitset128<1>(cl, ch);
+      }
+      uint64_t f = h ^ p.kconst;
+      bool keep = (MODE == kModeFrac) ? div_test(f, p.low_mask, p.shift, p.dinv, p.dlim)
+                                      : (f <= thresh);
+      if (valid && keep) {
+        uint32_t slot = atomicAdd(&q_n, 1u);
+        uint64_t a = (MODE == kModeFrac) ? cl : f;
+        uint64_t b = (MODE == kModeFrac) ? ch : cl;
+        if (slot < cap) {
+          q_a[slot] = a; q_b[slot] = b; q_c[slot] = ch;
+        } else {
+          unsigned long long gi = atomicAdd(&p.seg_count[g.seg], 1ull);
+          if (gi < p.seg_out_cap[g.seg]) {
+            uint64_t o = p.seg_out_off[g.seg] + gi;
+            p.out_key[o] = a; p.out_val[o] = b;
+            if (MODE == kModeBottom) p.out_hi[o] = ch;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (q_n >= cap / 2) wflush(g.seg);
+  }
+  add_windows(p, count_seg, win_count);
+  wflush(count_seg);
+}
+
+template <class K>
+int occupancy_grid(K kernel, int device) {
+  int per_cu = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0);
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (per_cu < 1) per_cu = 1;
+  if (cus < 1) cus = 1;
+  return per_cu * cus;
+}
+
+}  // namespace
+
+uint64_t scan_tiles_for(uint64_t seg_bytes) { return (seg_bytes + kTile - 1) / kTile; }
+
+hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, int device,
+                       hipStream_t stream, int grid_override) {
+  if (p.n_tiles == 0) return hipSuccess;
+  auto pick = [&](auto kernel) -> hipError_t {
+    int grid = grid_override > 0 ? grid_override : occupancy_grid(kernel, device);
+    if ((uint64_t)grid > p.n_tiles) grid = (int)p.n_tiles;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, p);
+    return hipGetLastError();
+  };
+  if (!wide) {
+    if (mode == kModeFrac) return flavour == 0 ? pick(scan_kernel<kModeFrac, 0>) : pick(scan_kernel<kModeFrac, 1>);
+    return flavour == 0 ? pick(scan_kernel<kModeBottom, 0>) : pick(scan_kernel<kModeBottom, 1>);
+  }
+  if (mode == kModeFrac) return flavour == 0 ? pick(scan_kernel_wide<kModeFrac, 0>) : pick(scan_kernel_wide<kModeFrac, 1>);
+  return flavour == 0 ? pick(scan_kernel_wide<kModeBottom, 0>) : pick(scan_kernel_wide<kModeBottom, 1>);
+}
+
+}  // namespace sks

@@ -1,0 +1,107 @@
+// Internal declarations shared by the kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace sks {
+
+constexpr int kModeFrac = 0;
+constexpr int kModeBottom = 1;
+
+// Arguments of the fused scan kernel (scan.hip).  All per-segment arrays are
+// device arrays indexed by the launch-local segment index.
+struct ScanParams {
+  const uint8_t* seq;
+  const uint64_t* seg_begin;    // [n_seg] first byte of each segment
+  const uint64_t* seg_end;      // [n_seg] end byte (exclusive)
+  const uint64_t* tile_prefix;  // [n_seg + 1] tiles before each segment
+  uint32_t n_seg;
+  uint64_t n_tiles;
+  int w;
+  uint64_t mask_lo, mask_hi;
+  uint64_t kconst;              // H(mask) ^ w ^ nonce
+  // FracMinHash divisibility test (sks_hash.hpp DivTest)
+  uint64_t low_mask;
+  uint32_t shift;
+  uint64_t dinv, dlim;
+  // bottom-s pre-filter: keep fmh <= seg_thresh[seg]
+  const uint64_t* seg_thresh;
+  // output records: frac narrow key=C; frac wide key=lo val=hi;
+  // bottom narrow key=fmh val=C; bottom wide key=fmh val=lo hi=hi
+  uint64_t* out_key;
+  uint64_t* out_val;
+  uint64_t* out_hi;
+  const uint64_t* seg_out_off;  // [n_seg] first record slot
+  const uint64_t* seg_out_cap;  // [n_seg] record capacity
+  unsigned long long* seg_count;    // [n_seg] records emitted (may exceed capacity)
+  unsigned long long* seg_windows;  // [n_seg] valid windows hashed
+};
+
+uint64_t scan_tiles_for(uint64_t seg_bytes);
+hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, int device,
+                       hipStream_t stream, int grid_override);
+
+// ---- post-processing (post.hip) -------------------------------------------------
+// Grow-only device scratch owned by a context.
+struct Scratch {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  hipError_t reserve(size_t n);
+  void release();
+};
+
+// Sort each CSR segment of keys ascending (optionally carrying values).
+// keys/vals are sorted in place via the alt buffers; results land in `*_out`.
+hipError_t seg_sort_keys(const uint64_t* keys_in, uint64_t* keys_out, uint64_t total,
+                         const std::vector<uint64_t>& host_off, const uint64_t* d_off,
+                         int end_bit, Scratch& tmp, hipStream_t s);
+hipError_t seg_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const uint64_t* vals_in,
+                          uint64_t* vals_out, uint64_t total, const std::vector<uint64_t>& host_off,
+                          const uint64_t* d_off, int end_bit, Scratch& tmp, hipStream_t s);
+
+// Compact sparse survivor regions [off[g], off[g] + cnt[g]) into dense CSR.
+hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d_src_off,
+                           const uint64_t* d_dst_off, uint32_t n_seg, uint64_t max_len,
+                           hipStream_t s);
+
+// Per-segment unique of sorted keys (optionally by a (key, key2) pair):
+// writes d_flag_pos (exclusive scan of "first of run" flags) and per-segment
+// unique counts d_uniq[g].  Keys equal in key (and key2 when non-null) are
+// one element.
+hipError_t seg_unique_scan(const uint64_t* keys, const uint64_t* keys2, uint64_t total,
+                           const uint64_t* d_off, uint32_t n_seg, uint32_t* d_flag,
+                           uint64_t* d_pos, uint64_t* d_uniq, Scratch& tmp, hipStream_t s);
+// Scatter the first `limit[g]` unique elements of each segment:
+// out[dst_off[g] + rank] = vals[i] (and out2 from vals2 when non-null).
+// limit == nullptr keeps every unique element; dst_off == nullptr places
+// segment g at pos[off[g]] (the global unique rank, i.e. dense CSR output).
+hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint64_t total,
+                              const uint64_t* d_off, uint32_t n_seg, const uint32_t* d_flag,
+                              const uint64_t* d_pos, const uint64_t* d_limit,
+                              const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
+                              hipStream_t s);
+
+// ---- intersection (intersect.hip) ---------------------------------------------------
+hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
+                                  const uint32_t* sizes, int elem_words, const int32_t* a,
+                                  const int32_t* b, uint64_t n_pairs, int32_t* out, hipStream_t s);
+hipError_t launch_intersect_all(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                                int elem_words, uint32_t n, uint32_t row_begin, uint32_t row_end,
+                                int32_t* out, hipStream_t s);
+
+// ---- misc kernels (post.hip) -------------------------------------------------------------
+hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,
+                        uint64_t mut_thresh, uint64_t pos_offset, hipStream_t s);
+hipError_t launch_export(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                         uint32_t n, int elem_words, uint64_t* dst, uint64_t stride,
+                         uint32_t* dst_sizes, hipStream_t s);
+hipError_t launch_iota(uint64_t* out, uint64_t n, hipStream_t s);
+hipError_t launch_gather(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
+                         hipStream_t s);
+hipError_t launch_interleave(const uint64_t* lo, const uint64_t* hi, uint64_t n, uint64_t* out,
+                             hipStream_t s);
+
+}  // namespace sks

@@ -1,0 +1,325 @@
+"""ctypes binding of libsks.so (include/sks.h) for the tests and bench.py.
+
+This is plumbing only: every computation happens in libsks.so (HIP kernels for
+gfx950 + host ingress).  There is deliberately no CPU fallback — if the library
+or a GPU is missing, the calls below raise.  Device buffers are torch tensors
+on `cuda:N` whose data_ptr() is handed to the C ABI.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libsks.so")
+
+SKS_FRAC_MOD = 0
+SKS_BOTTOM_S = 1
+FLAVOUR_BOOST_MIX = 0
+FLAVOUR_BOOST_LEGACY = 1
+
+
+class SksError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"sks error {code}: {msg}")
+        self.code = code
+
+
+class Policy(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("flavour", C.c_int32), ("param", C.c_uint64),
+                ("nonce", C.c_int64)]
+
+
+class Timings(C.Structure):
+    _fields_ = [("scan_ms", C.c_float), ("post_ms", C.c_float), ("total_ms", C.c_float),
+                ("windows", C.c_uint64), ("scan_launches", C.c_uint64),
+                ("survivors", C.c_uint64)]
+
+
+EXPORTED = [
+    "sks_abi_version", "sks_last_error", "sks_mask_generate", "sks_mask_contiguous",
+    "sks_frac_min_hash", "sks_containment", "sks_binomial_estimator", "sks_ani_from_counts",
+    "sks_fasta_open", "sks_fasta_close", "sks_fasta_num_records", "sks_fasta_record",
+    "sks_fasta_stream", "sks_fasta_stream_bytes", "sks_fasta_runs", "sks_ctx_create",
+    "sks_ctx_destroy", "sks_ctx_set_stream", "sks_ctx_synchronize", "sks_ctx_last_timings",
+    "sks_sketch_build", "sks_sketch_set_free", "sks_sketch_set_num", "sks_sketch_set_elem_words",
+    "sks_sketch_set_sizes", "sks_sketch_set_windows", "sks_sketch_set_device_data",
+    "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
+    "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
+    "sks_synth_bases",
+]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libsks.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    u64p = C.POINTER(C.c_uint64)
+    vp = C.c_void_p
+    L.sks_last_error.restype = C.c_char_p
+    L.sks_mask_generate.argtypes = [C.c_int, C.c_int, C.c_uint64, u64p]
+    L.sks_mask_contiguous.argtypes = [C.c_int, u64p]
+    L.sks_frac_min_hash.argtypes = [u64p, u64p, C.c_int, C.c_int64, C.c_int]
+    L.sks_frac_min_hash.restype = C.c_uint64
+    L.sks_containment.argtypes = [C.c_int, C.c_int]
+    L.sks_containment.restype = C.c_double
+    L.sks_binomial_estimator.argtypes = [C.c_double, C.c_int]
+    L.sks_binomial_estimator.restype = C.c_double
+    L.sks_ani_from_counts.argtypes = [vp, vp, C.c_uint64, C.c_int, vp, vp]
+    L.sks_fasta_open.argtypes = [C.c_char_p, C.POINTER(vp)]
+    L.sks_fasta_close.argtypes = [vp]
+    L.sks_fasta_close.restype = None
+    L.sks_fasta_num_records.argtypes = [vp]
+    L.sks_fasta_num_records.restype = C.c_uint64
+    L.sks_fasta_record.argtypes = [vp, C.c_uint64, C.POINTER(vp), u64p]
+    L.sks_fasta_stream.argtypes = [vp]
+    L.sks_fasta_stream.restype = vp
+    L.sks_fasta_stream_bytes.argtypes = [vp]
+    L.sks_fasta_stream_bytes.restype = C.c_uint64
+    L.sks_fasta_runs.argtypes = [vp, vp, vp, u64p, u64p]
+    L.sks_ctx_create.argtypes = [C.c_int, vp, C.POINTER(vp)]
+    L.sks_ctx_destroy.argtypes = [vp]
+    L.sks_ctx_set_stream.argtypes = [vp, vp]
+    L.sks_ctx_synchronize.argtypes = [vp]
+    L.sks_ctx_last_timings.argtypes = [vp, C.POINTER(Timings)]
+    L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
+    L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.sks_sketch_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
+                                   C.POINTER(Policy), C.POINTER(vp)]
+    L.sks_sketch_set_free.argtypes = [vp]
+    L.sks_sketch_set_num.argtypes = [vp]
+    L.sks_sketch_set_num.restype = C.c_uint32
+    L.sks_sketch_set_elem_words.argtypes = [vp]
+    L.sks_sketch_set_sizes.argtypes = [vp, vp]
+    L.sks_sketch_set_windows.argtypes = [vp, vp]
+    L.sks_sketch_set_starts.argtypes = [vp, vp]
+    for f in ("sks_sketch_set_device_data", "sks_sketch_set_device_starts",
+              "sks_sketch_set_device_sizes"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = vp
+    L.sks_sketch_set_copy.argtypes = [vp, C.c_uint32, vp]
+    L.sks_sketch_set_export.argtypes = [vp, vp, C.c_uint64, vp]
+    L.sks_intersect_pairs.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, C.c_uint64, vp]
+    L.sks_intersect_all.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    vp]
+    L.sks_synth_bases.argtypes = [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double,
+                                  C.c_uint64]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise SksError(rc, lib().sks_last_error().decode(errors="replace"))
+
+
+def _mask_arr(mask):
+    return (C.c_uint64 * 2)(mask & (2**64 - 1), mask >> 64)
+
+
+# ---- host helpers -------------------------------------------------------------------
+def mask_generate(window, k, seed=0):
+    out = (C.c_uint64 * 2)()
+    check(lib().sks_mask_generate(window, k, seed, out))
+    return int(out[0]) | (int(out[1]) << 64)
+
+
+def mask_contiguous(length):
+    out = (C.c_uint64 * 2)()
+    check(lib().sks_mask_contiguous(length, out))
+    return int(out[0]) | (int(out[1]) << 64)
+
+
+def frac_min_hash(kmer, mask, window, nonce=1, flavour=0):
+    return int(lib().sks_frac_min_hash(_mask_arr(kmer), _mask_arr(mask), window, nonce, flavour))
+
+
+def containment(inter, size):
+    return float(lib().sks_containment(inter, size))
+
+
+def binomial_estimator(c, k):
+    return float(lib().sks_binomial_estimator(c, k))
+
+
+def ani_from_counts(inter, size_first, k):
+    inter = np.ascontiguousarray(inter, dtype=np.int32)
+    size_first = np.ascontiguousarray(size_first, dtype=np.int32)
+    cont = np.zeros(inter.shape, dtype=np.float64)
+    ani = np.zeros(inter.shape, dtype=np.float64)
+    check(lib().sks_ani_from_counts(inter.ctypes.data, size_first.ctypes.data, inter.size, k,
+                                    cont.ctypes.data, ani.ctypes.data))
+    return cont, ani
+
+
+class Fasta:
+    """sks_fasta_open: the reference's strings_from_fasta record rules."""
+
+    def __init__(self, path):
+        h = C.c_void_p()
+        check(lib().sks_fasta_open(os.fsencode(path), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().sks_fasta_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def num_records(self):
+        return int(lib().sks_fasta_num_records(self.h))
+
+    def records(self):
+        out = []
+        for i in range(self.num_records()):
+            p = C.c_void_p()
+            n = C.c_uint64()
+            check(lib().sks_fasta_record(self.h, i, C.byref(p), C.byref(n)))
+            out.append(C.string_at(p, n.value) if n.value else b"")
+        return out
+
+    def stream(self):
+        n = int(lib().sks_fasta_stream_bytes(self.h))
+        if n == 0:
+            return np.zeros(0, dtype=np.uint8)
+        p = lib().sks_fasta_stream(self.h)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n,)).copy()
+
+    def runs(self):
+        nc, nr = C.c_uint64(0), C.c_uint64(0)
+        check(lib().sks_fasta_runs(self.h, None, None, C.byref(nc), C.byref(nr)))
+        codes = np.zeros(max(nc.value, 1), dtype=np.uint8)
+        lens = np.zeros(max(nr.value, 1), dtype=np.uint64)
+        check(lib().sks_fasta_runs(self.h, codes.ctypes.data, lens.ctypes.data, C.byref(nc),
+                                   C.byref(nr)))
+        codes, lens = codes[:nc.value], lens[:nr.value]
+        out, o = [], 0
+        for n in lens:
+            out.append(codes[o:o + int(n)].tobytes())
+            o += int(n)
+        return out
+
+
+# ---- device ---------------------------------------------------------------------------------
+class Context:
+    def __init__(self, device=0, stream=None):
+        h = C.c_void_p()
+        check(lib().sks_ctx_create(device, C.c_void_p(stream) if stream else None, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def set_stream(self, stream):
+        check(lib().sks_ctx_set_stream(self.h, C.c_void_p(stream) if stream else None))
+
+    def set_scan_grid(self, grid):
+        check(lib().sks_ctx_set_scan_grid(self.h, grid))
+
+    def synchronize(self):
+        check(lib().sks_ctx_synchronize(self.h))
+
+    def timings(self):
+        t = Timings()
+        check(lib().sks_ctx_last_timings(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in Timings._fields_}
+
+    def last_intersect_ms(self):
+        ms = C.c_float()
+        check(lib().sks_ctx_last_intersect_ms(self.h, C.byref(ms)))
+        return float(ms.value)
+
+    def close(self):
+        if self.h:
+            lib().sks_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sketch_build(self, d_seq_ptr, n_bytes, seg_off, window, mask, kind=SKS_FRAC_MOD,
+                     param=200, nonce=1, flavour=0):
+        seg = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        pol = Policy(kind, flavour, param, nonce)
+        h = C.c_void_p()
+        check(lib().sks_sketch_build(self.h, C.c_void_p(d_seq_ptr), n_bytes, seg.ctypes.data,
+                                     len(seg) - 1, window, _mask_arr(mask), C.byref(pol),
+                                     C.byref(h)))
+        return SketchSet(h)
+
+    def intersect_pairs(self, data_ptr, starts_ptr, sizes_ptr, elem_words, a_ptr, b_ptr,
+                        n_pairs, out_ptr):
+        check(lib().sks_intersect_pairs(self.h, data_ptr, starts_ptr, sizes_ptr, elem_words,
+                                        a_ptr, b_ptr, n_pairs, out_ptr))
+
+    def intersect_all(self, data_ptr, starts_ptr, sizes_ptr, elem_words, n, row_begin, row_end,
+                      out_ptr):
+        check(lib().sks_intersect_all(self.h, data_ptr, starts_ptr, sizes_ptr, elem_words, n,
+                                      row_begin, row_end, out_ptr))
+
+    def synth_bases(self, d_out_ptr, n, seed, mut_seed=0, mut_rate=0.0, pos_offset=0):
+        check(lib().sks_synth_bases(self.h, C.c_void_p(d_out_ptr), n, seed, mut_seed, mut_rate,
+                                    pos_offset))
+
+
+class SketchSet:
+    def __init__(self, h):
+        self.h = h
+        self.n = int(lib().sks_sketch_set_num(h))
+        self.elem_words = int(lib().sks_sketch_set_elem_words(h))
+
+    def free(self):
+        if self.h:
+            lib().sks_sketch_set_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def sizes(self):
+        out = np.zeros(max(self.n, 1), dtype=np.uint32)
+        check(lib().sks_sketch_set_sizes(self.h, out.ctypes.data))
+        return out[:self.n]
+
+    def windows(self):
+        out = np.zeros(max(self.n, 1), dtype=np.uint64)
+        check(lib().sks_sketch_set_windows(self.h, out.ctypes.data))
+        return out[:self.n]
+
+    def starts(self):
+        out = np.zeros(max(self.n, 1), dtype=np.uint64)
+        check(lib().sks_sketch_set_starts(self.h, out.ctypes.data))
+        return out[:self.n]
+
+    def sketch(self, i):
+        """Sketch i as a uint64 array of shape (size, 2) = (lo, hi)."""
+        n = int(self.sizes()[i])
+        buf = np.zeros(max(n * self.elem_words, 1), dtype=np.uint64)
+        check(lib().sks_sketch_set_copy(self.h, i, buf.ctypes.data))
+        buf = buf[:n * self.elem_words]
+        if self.elem_words == 1:
+            return np.stack([buf, np.zeros_like(buf)], axis=1)
+        return buf.reshape(-1, 2)
+
+    def device_ptrs(self):
+        L = lib()
+        return (L.sks_sketch_set_device_data(self.h), L.sks_sketch_set_device_starts(self.h),
+                L.sks_sketch_set_device_sizes(self.h))
+
+    def export(self, d_dst_ptr, stride, d_sizes_ptr):
+        check(lib().sks_sketch_set_export(self.h, C.c_void_p(d_dst_ptr), stride,
+                                          C.c_void_p(d_sizes_ptr)))

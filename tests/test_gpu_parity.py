@@ -1,0 +1,253 @@
+"""GPU parity: libsks.so (HIP, gfx950) against the oracle, through the C ABI.
+
+Every comparison is bit-exact (sketch membership, sizes, windows hashed,
+intersection counts); ANI is computed on the host from the exact counts.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+import sksffi
+import synth
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN_FASTA = os.path.join(ROOT, "tests", "golden", "fasta")
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch_cuda):
+    c = sksffi.Context(0)
+    yield c
+    c.close()
+
+
+def upload(torch, data: bytes):
+    t = torch.frombuffer(bytearray(data) if data else bytearray(b"\n"), dtype=torch.uint8)
+    return t.to("cuda:0")
+
+
+def build(torch, ctx, genomes, w, mask, kind="frac", param=200, flavour=0, nonce=1):
+    """genomes: list of bytes; each segment is genome + '\\n'."""
+    stream = b"".join(g + b"\n" for g in genomes)
+    offs = [0]
+    for g in genomes:
+        offs.append(offs[-1] + len(g) + 1)
+    dev = upload(torch, stream)
+    k = sksffi.SKS_FRAC_MOD if kind == "frac" else sksffi.SKS_BOTTOM_S
+    ss = ctx.sketch_build(dev.data_ptr(), len(stream), offs, w, mask, k, param, nonce, flavour)
+    return ss, dev
+
+
+def check_against_oracle(ss, genomes, w, mask, kind, param, flavour=0, nonce=1):
+    sizes = ss.sizes()
+    wins = ss.windows()
+    for i, g in enumerate(genomes):
+        want, nw = O.sketch(O.cut_runs(g), w, mask, kind, param, nonce, flavour)
+        got = ss.sketch(i)
+        assert int(wins[i]) == nw, (i, w, kind, param)
+        assert int(sizes[i]) == len(want), (i, w, kind, param)
+        assert np.array_equal(got, want), (i, w, kind, param, flavour)
+
+
+def test_synth_device_matches_numpy(torch_cuda, ctx):
+    torch = torch_cuda
+    for (n, seed, ms, rate, off) in [(100003, 5, 0, 0.0, 0), (65536, 9, 77, 0.05, 12345)]:
+        d = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        ctx.synth_bases(d.data_ptr(), n, seed, ms, rate, off)
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy(), synth.bases(n, seed, ms, rate, off))
+
+
+def test_c1_golden(torch_cuda, ctx, golden):
+    g = golden("c1_sketch.json")
+    f = sksffi.Fasta(os.path.join(GOLDEN_FASTA, g["file"]))
+    stream = f.stream().tobytes()
+    dev = upload(torch_cuda, stream)
+    for case in g["cases"]:
+        k = sksffi.SKS_FRAC_MOD if case["kind"] == "frac" else sksffi.SKS_BOTTOM_S
+        m = int(case["mask"], 16)
+        ss = ctx.sketch_build(dev.data_ptr(), len(stream), [0, len(stream)], case["w"], m, k,
+                              case["param"], case["nonce"], case["flavour"])
+        got = [hex(int(lo) | int(hi) << 64) for lo, hi in ss.sketch(0)]
+        assert int(ss.windows()[0]) == case["windows"]
+        assert got == case["sketch"], case
+
+
+def test_fasta_edge_corpus(torch_cuda, ctx, golden):
+    for name in golden("fasta_cases.json")["cases"]:
+        f = sksffi.Fasta(os.path.join(GOLDEN_FASTA, name))
+        stream = f.stream().tobytes()
+        dev = upload(torch_cuda, stream)
+        for w in (1, 3, 4, 8):
+            m = O.mask(w, w, 0)
+            ss = ctx.sketch_build(dev.data_ptr(), len(stream), [0, len(stream)], w, m,
+                                  sksffi.SKS_FRAC_MOD, 1)
+            want, nw = O.sketch(f.runs(), w, m, "frac", 1)
+            assert int(ss.windows()[0]) == nw, (name, w)
+            assert np.array_equal(ss.sketch(0), want), (name, w)
+
+
+def _genomes(seed, lens, n_frac=0.001, lower=False):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i, L in enumerate(lens):
+        g = synth.bases(L, seed=seed * 1000 + i)
+        if L:
+            k = max(1, int(L * n_frac))
+            g[rng.integers(0, L, k)] = ord("N")
+            if lower:
+                idx = rng.integers(0, L, L // 10)
+                g[idx] = g[idx] | 0x20
+        out.append(g.tobytes())
+    return out
+
+
+@pytest.mark.parametrize("w,k", [(1, 1), (2, 2), (5, 3), (16, 16), (17, 11), (21, 21), (31, 21),
+                                 (32, 32), (32, 20)])
+def test_frac_narrow_windows(torch_cuda, ctx, w, k):
+    genomes = _genomes(w, [0, 3, w - 1 if w > 1 else 0, w, 4095, 4096, 4097, 20000, 131071],
+                       lower=True)
+    m = O.mask(w, k, 7)
+    for flavour in (0, 1):
+        for c in (1, 7, 200):
+            ss, _ = build(torch_cuda, ctx, genomes, w, m, "frac", c, flavour)
+            check_against_oracle(ss, genomes, w, m, "frac", c, flavour)
+
+
+@pytest.mark.parametrize("w,k", [(33, 33), (40, 21), (50, 40), (63, 30), (64, 64)])
+def test_frac_wide_windows(torch_cuda, ctx, w, k):
+    genomes = _genomes(w, [0, w, 4096 + w, 30000, 70001], lower=True)
+    m = O.mask(w, k, 3)
+    for flavour in (0, 1):
+        for c in (1, 50):
+            ss, _ = build(torch_cuda, ctx, genomes, w, m, "frac", c, flavour)
+            check_against_oracle(ss, genomes, w, m, "frac", c, flavour)
+
+
+@pytest.mark.parametrize("w,k", [(21, 21), (31, 21), (8, 8), (45, 21)])
+def test_bottom_s(torch_cuda, ctx, w, k):
+    genomes = _genomes(100 + w, [0, 10, 500, 9000, 60000, 250000])
+    m = O.mask(w, k, 0)
+    for flavour in (0, 1):
+        for s in (1, 10, 1000, 20000):
+            ss, _ = build(torch_cuda, ctx, genomes, w, m, "bottom", s, flavour)
+            check_against_oracle(ss, genomes, w, m, "bottom", s, flavour)
+
+
+def test_bottom_s_low_complexity_forces_threshold_retry(torch_cuda, ctx):
+    # periodic genome: few distinct k-mers, so the first threshold pass finds
+    # fewer than s candidates and the build must raise the threshold
+    unit = synth.bases(37, seed=4).tobytes()
+    genomes = [unit * 5000, (unit * 300) + synth.bases(50000, seed=5).tobytes()]
+    m = O.mask(21, 21, 0)
+    for s in (30, 5000):
+        ss, _ = build(torch_cuda, ctx, genomes, 21, m, "bottom", s)
+        check_against_oracle(ss, genomes, 21, m, "bottom", s)
+
+
+def test_frac_capacity_overflow_retry(torch_cuda, ctx):
+    # c = 1 keeps every window; a homopolymer produces one k-mer many times
+    genomes = [b"A" * 300000, synth.bases(100000, seed=8).tobytes()]
+    m = O.mask(15, 15, 0)
+    ss, _ = build(torch_cuda, ctx, genomes, 15, m, "frac", 1)
+    check_against_oracle(ss, genomes, 15, m, "frac", 1)
+
+
+def test_config2_5mb_bottom_s(torch_cuda, ctx):
+    g = synth.bases(5_000_000, seed=2).tobytes()
+    m = O.mask(31, 21, 0)
+    assert m == 0x03FF3CCFFF3C33F3
+    ss, _ = build(torch_cuda, ctx, [g], 31, m, "bottom", 10000)
+    check_against_oracle(ss, [g], 31, m, "bottom", 10000)
+    ss, _ = build(torch_cuda, ctx, [g], 31, m, "frac", 1000)
+    check_against_oracle(ss, [g], 31, m, "frac", 1000)
+
+
+def test_intersections_match_oracle(torch_cuda, ctx):
+    torch = torch_cuda
+    anc = synth.bases(40000, seed=50)
+    genomes = [synth.bases(40000, seed=50, mut_seed=60 + i, mut_rate=0.004 * i).tobytes()
+               for i in range(6)] + [b"", synth.bases(40000, seed=51).tobytes()]
+    del anc
+    for (w, k, kind, p) in [(21, 21, "frac", 20), (31, 21, "bottom", 500), (40, 30, "frac", 10)]:
+        m = O.mask(w, k, 0)
+        ss, _ = build(torch, ctx, genomes, w, m, kind, p)
+        sk = [O.sketch(O.cut_runs(g), w, m, kind, p)[0] for g in genomes]
+        data, starts, sizes = ss.device_ptrs()
+        n = len(genomes)
+        out = torch.zeros(n * n, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_all(data, starts, sizes, ss.elem_words, n, 0, n, out.data_ptr())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().reshape(n, n)
+        want = np.array([[O.intersect(sk[i], sk[j]) for j in range(n)] for i in range(n)])
+        assert np.array_equal(got, want), (w, kind)
+        # row block form
+        out2 = torch.zeros(3 * n, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_all(data, starts, sizes, ss.elem_words, n, 2, 5, out2.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(out2.cpu().numpy().reshape(3, n), want[2:5])
+        # pair-list form (compute_pairwise_kmer_set_intersections)
+        a = torch.tensor([0, 1, 7, 6, 3], dtype=torch.int32, device="cuda:0")
+        b = torch.tensor([1, 0, 7, 2, 6], dtype=torch.int32, device="cuda:0")
+        o3 = torch.zeros(5, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_pairs(data, starts, sizes, ss.elem_words, a.data_ptr(), b.data_ptr(), 5,
+                            o3.data_ptr())
+        torch.cuda.synchronize()
+        assert o3.cpu().tolist() == [want[x][y] for x, y in zip(a.tolist(), b.tolist())]
+
+
+def test_frac_chunk_union_property(torch_cuda, ctx):
+    """Size-independent property at scale: the sketch of a genome equals the
+    union of the sketches of overlapping chunks ((w-1)-base halos), and the
+    c=1000 sketch is exactly the c=200 sketch filtered by fmh % 1000 == 0."""
+    torch = torch_cuda
+    L, w = 40_000_000, 31
+    m = O.mask(31, 21, 0)
+    dev = torch.empty(L + 1, dtype=torch.uint8, device="cuda:0")
+    ctx.synth_bases(dev.data_ptr(), L, 33)
+    dev[L] = ord("\n")
+    dev[1000:1100] = ord("N")
+    whole = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, sksffi.SKS_FRAC_MOD, 200)
+    S200 = whole.sketch(0)
+    cuts = [0, 7_000_003, 19_999_999, 31_000_000, L + 1]
+    offs = []
+    for i in range(len(cuts) - 1):
+        offs.append((cuts[i], min(L + 1, cuts[i + 1] + w - 1)))
+    # overlapping segments: build each separately
+    parts = []
+    for (a, b) in offs:
+        ss = ctx.sketch_build(dev.data_ptr() + a, b - a, [0, b - a], w, m, sksffi.SKS_FRAC_MOD, 200)
+        parts.append(ss.sketch(0))
+    union = np.unique(np.concatenate([p[:, 0] for p in parts]))
+    assert np.array_equal(union, S200[:, 0])
+    assert int(whole.windows()[0]) == (1000 - w + 1) + (L - 1100 - w + 1)
+    s1000 = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, sksffi.SKS_FRAC_MOD, 1000)
+    S1000 = s1000.sketch(0)
+    keep = [x for x in S200[:, 0] if sksffi.frac_min_hash(int(x), m, w, 1, 0) % 1000 == 0]
+    assert np.array_equal(np.array(keep, dtype=np.uint64), S1000[:, 0])
+    for x in S1000[:50, 0]:
+        assert sksffi.frac_min_hash(int(x), m, w, 1, 0) % 1000 == 0
+
+
+def test_argument_errors(torch_cuda, ctx):
+    torch = torch_cuda
+    d = upload(torch, b"ACGTACGT\n")
+    m = O.mask(4, 4, 0)
+    for (w, mask, param, code) in [(0, m, 5, 1), (65, m, 5, 1), (4, m, 0, 1),
+                                   (2, m, 5, 5)]:  # mask bits >= 2w
+        with pytest.raises(sksffi.SksError) as e:
+            ctx.sketch_build(d.data_ptr(), 9, [0, 9], w, mask, sksffi.SKS_FRAC_MOD, param)
+        assert e.value.code == code
+    with pytest.raises(sksffi.SksError):
+        ctx.sketch_build(d.data_ptr(), 9, [0, 10], 4, m, sksffi.SKS_FRAC_MOD, 5)
