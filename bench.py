@@ -1,0 +1,317 @@
+"""bench.py — spaced-k-mer sketch + ANI engine on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Headline (`value`): k-mers hashed/s, whole job, on config 3 of BASELINE.json
+(one 3 Gb human-scale synthetic genome per GPU: 24 contigs x 125 Mb, four 10 kb
+N-runs per contig, spaced seed w=31/k=21 mask seed 0, FracMinHash 1/1000).
+A step = one complete sketch build of that genome (fused scan kernel + sort +
+unique, host syncs included) with the bytes already resident in HBM.
+Genomes are independent, so ranks shard them with no collective: weak scaling.
+
+Secondary (`pairs`): genome-pairs ANI/s on config 4 (1000 x 5 Mb genomes =
+10 ancestors x 100 mutated descendants, w=31/k=21, bottom-s s=10000), strong
+scaling: rank r sketches its share of genomes, the padded sketches are
+all-gathered over RCCL (torch.distributed "nccl"), and rank r counts the
+intersections of its row block against all 1000 sketches; containment and
+ANI for every ordered pair are computed on the host from the exact counts.
+
+`cpu_baseline`: the reference-faithful CPU port (oracle/ref_port.cpp, see
+BASELINE.md) timed on this box's host cores on a bounded sample of the same
+workload (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "spaced-kmer-sketching_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import sksffi  # noqa: E402
+import synth  # noqa: E402
+
+METRIC = "k-mers hashed/s + genome-pairs ANI/s at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+W, K, MASK_SEED = 31, 21, 0
+C3_CONTIGS, C3_CONTIG_LEN, C3_NRUN, C3_NRUN_LEN, C3_FRAC = 24, 125_000_000, 4, 10_000, 1000
+C4_GENOMES, C4_LEN, C4_ANCESTORS, C4_S = 1000, 5_000_000, 10, 10000
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# ---- config 3 ---------------------------------------------------------------------
+def c3_layout():
+    """Byte layout of one genome: contigs separated by '\\n'; N-run offsets."""
+    contig_starts = [i * (C3_CONTIG_LEN + 1) for i in range(C3_CONTIGS)]
+    n_bytes = C3_CONTIGS * (C3_CONTIG_LEN + 1)
+    nrun_off = [int(C3_CONTIG_LEN * (j + 1) / (C3_NRUN + 1)) for j in range(C3_NRUN)]
+    return contig_starts, n_bytes, nrun_off
+
+
+def c3_windows():
+    # per contig: runs cut by the N-runs; windows = sum(max(0, L - w + 1))
+    _, _, nrun_off = c3_layout()
+    edges = [0]
+    for o in nrun_off:
+        edges += [o, o + C3_NRUN_LEN]
+    edges.append(C3_CONTIG_LEN)
+    per = sum(max(0, edges[i + 1] - edges[i] - W + 1) for i in range(0, len(edges), 2))
+    return per * C3_CONTIGS
+
+
+def make_c3(ctx, seed_base):
+    contig_starts, n_bytes, nrun_off = c3_layout()
+    buf = torch.empty(n_bytes, dtype=torch.uint8, device="cuda")
+    for i, s in enumerate(contig_starts):
+        ctx.synth_bases(buf.data_ptr() + s, C3_CONTIG_LEN, seed_base + i)
+        for o in nrun_off:
+            buf[s + o:s + o + C3_NRUN_LEN] = ord("N")
+        buf[s + C3_CONTIG_LEN] = ord("\n")
+    torch.cuda.synchronize()
+    return buf, n_bytes
+
+
+def cpu_baseline_c3(mask, budget_bases):
+    """Reference-faithful port, 1 core (the reference sketches one genome on one
+    worker, kmer_set.cpp:124), on the first `budget_bases` of contig 0."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    _, _, nrun_off = c3_layout()
+    seq = synth.bases(budget_bases, seed=3)
+    for o in nrun_off:
+        if o < budget_bases:
+            seq[o:min(budget_bases, o + C3_NRUN_LEN)] = ord("N")
+    runs = pyoracle.cut_runs(seq.tobytes())
+    codes = np.frombuffer(b"".join(runs), dtype=np.uint8)
+    lens = np.array([len(r) for r in runs], dtype=np.uint64)
+    windows = int(sum(max(0, int(L) - W + 1) for L in lens))
+    t0 = time.perf_counter()
+    s = pyoracle.refport_sketch_codes(codes, lens, W, mask, C3_FRAC, 1, 0)
+    dt = time.perf_counter() - t0
+    size = s.size()
+    del s
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": f"first {budget_bases / 1e6:.0f} Mb of config-3 contig 0 "
+                      f"({windows} windows, FracMinHash 1/{C3_FRAC}, set size {size}), "
+                      f"oracle/ref_port.cpp, {dt:.1f} s"}
+
+
+# ---- config 4 ------------------------------------------------------------------------
+def c4_genome_seeds(g):
+    anc = g // (C4_GENOMES // C4_ANCESTORS)
+    desc = g % (C4_GENOMES // C4_ANCESTORS)
+    return 100 + anc, 1000 + g, desc * 0.001
+
+
+def run_pairs(ctx, world, rank, mask, steps, warmup):
+    import torch.distributed as dist
+    per = (C4_GENOMES + world - 1) // world
+    g0, g1 = rank * per, min(C4_GENOMES, (rank + 1) * per)
+    n_local = max(0, g1 - g0)
+    seg = [0]
+    for _ in range(n_local):
+        seg.append(seg[-1] + C4_LEN + 1)
+    buf = torch.empty(max(seg[-1], 1), dtype=torch.uint8, device="cuda")
+    for i in range(n_local):
+        anc_seed, mut_seed, rate = c4_genome_seeds(g0 + i)
+        ctx.synth_bases(buf.data_ptr() + seg[i], C4_LEN, anc_seed, mut_seed, rate)
+        buf[seg[i] + C4_LEN] = ord("\n")
+    torch.cuda.synchronize()
+    stride = C4_S
+    local = torch.full((per, stride), -1, dtype=torch.int64, device="cuda")
+    local_sz = torch.zeros(per, dtype=torch.int32, device="cuda")
+    full = torch.empty((per * world, stride), dtype=torch.int64, device="cuda")
+    full_sz = torch.empty(per * world, dtype=torch.int32, device="cuda")
+    starts = torch.arange(per * world, dtype=torch.int64, device="cuda") * stride
+    rows = torch.empty((per, C4_GENOMES), dtype=torch.int32, device="cuda")
+    t_sketch = t_pairs = 0.0
+    timed = 0
+    for it in range(warmup + steps):
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, C4_S)
+        if n_local:
+            ss.export(local.data_ptr(), stride, local_sz.data_ptr())
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.all_gather_into_tensor(full, local)
+            dist.all_gather_into_tensor(full_sz, local_sz)
+            src, src_sz = full, full_sz
+        else:
+            src, src_sz = local, local_sz
+        if n_local:
+            ctx.intersect_all(src.data_ptr(), starts.data_ptr(), src_sz.data_ptr(), 1,
+                              C4_GENOMES, g0, g1, rows.data_ptr())
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ts, tp = max_over_ranks(t1 - t0, world), max_over_ranks(t2 - t1, world)
+        if it >= warmup:
+            t_sketch += ts
+            t_pairs += tp
+            timed += 1
+        del ss
+    # ANI for this rank's ordered pairs (host, double, from exact counts)
+    counts = rows[:n_local].cpu().numpy()
+    sizes = src_sz.cpu().numpy()[:C4_GENOMES]
+    size_first = np.repeat(sizes[g0:g1].astype(np.int32), C4_GENOMES)
+    kmer_ones = bin(mask).count("1") // 2
+    _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, kmer_ones)
+    k_ms = ctx.last_intersect_ms() if n_local else 0.0
+    t_sketch /= max(timed, 1)
+    t_pairs /= max(timed, 1)
+    # sanity on rank 0: diagonal = sizes, siblings of the same ancestor overlap
+    if rank == 0 and n_local > 1:
+        assert all(counts[i, g0 + i] == sizes[g0 + i] for i in range(n_local))
+        assert counts[0, 1] > 0
+    return {
+        "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
+        "unit": "ordered pairs/s", "scaling": "strong",
+        "ms_pair_phase": t_pairs * 1e3, "ms_sketch_phase": t_sketch * 1e3,
+        "pair_kernel_ms_rank0": k_ms,
+        "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - W + 1) / t_sketch,
+        "ani_mean_offdiag_rank0": float(np.mean(ani)),
+        "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
+                   "genome_len": C4_LEN, "s": C4_S, "w": W, "k": K,
+                   "collective": "all_gather_into_tensor (RCCL)" if world > 1 else "none"},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-sample-mb", type=int, default=60)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pairs", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"))
+    args = ap.parse_args()
+
+    world, rank, local = dist_setup(args.gpus)
+    ctx = sksffi.Context(local)
+    mask = sksffi.mask_generate(W, K, MASK_SEED)
+
+    buf, n_bytes = make_c3(ctx, seed_base=3 + 1000 * rank)
+    log(f"[rank {rank}] config 3 genome resident: {n_bytes / 1e9:.2f} GB")
+
+    def step():
+        return ctx.sketch_build(buf.data_ptr(), n_bytes, [0, n_bytes], W, mask,
+                                sksffi.SKS_FRAC_MOD, C3_FRAC)
+
+    for _ in range(args.warmup):
+        ss = step()
+        del ss
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    scan_ms, survivors, windows, sizes = [], [], 0, []
+    for _ in range(args.steps):
+        ss = step()
+        t = ctx.timings()
+        scan_ms.append(t["scan_ms"])
+        survivors.append(t["survivors"])
+        windows += int(ss.windows()[0])
+        sizes.append(int(ss.sizes()[0]))
+        del ss
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    total_windows = sum_over_ranks(windows, world)
+    assert windows == args.steps * c3_windows(), (windows, c3_windows())
+    value = total_windows / elapsed
+
+    # roofline of the dominant kernel (fused scan): algorithmic bytes per launch
+    # = input bytes read (1 B per sequence byte incl. separators) + 8 B per record written
+    scan_avg_ms = float(np.mean(scan_ms))
+    alg_bytes = n_bytes + 8 * float(np.mean(survivors))
+    achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("scan_hbm_bytes_per_launch")
+
+    pairs = None
+    if not args.no_pairs:
+        pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 3)),
+                          warmup=1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_c3(mask, args.cpu_sample_mb * 1_000_000)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "k-mers/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (device splitmix64 generator, resident in HBM)",
+            "config": {"workload": "config3: 1x3 Gb multi-contig genome per GPU, spaced seed "
+                                   "w=31/k=21 (mask seed 0), FracMinHash 1/1000",
+                       "genome_bytes": n_bytes, "windows_per_genome": c3_windows(),
+                       "sketch_size": sizes[0], "parallelism": f"genome-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "scan_kernel<frac, boost-mix>", "kernel_ms": scan_avg_ms,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "pairs": pairs,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
