@@ -161,6 +161,18 @@ int sks_intersect_all(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_st
                       const uint32_t* d_sizes, int elem_words, uint32_t n, uint32_t row_begin,
                       uint32_t row_end, int32_t* d_out);
 
+/* Symmetric all-vs-all for sharding across devices: the n x n matrix is cut
+ * into 64 x 64 tiles and the upper-triangle tiles (I <= J, row-major, count
+ * sks_intersect_sym_tiles(n)) in [tile_begin, tile_end) are computed; each
+ * count is written to both d_out[i * n + j] and d_out[j * n + i] of the n x n
+ * int32 matrix, which the call zeroes first.  Summing the matrices of calls
+ * that together cover [0, sks_intersect_sym_tiles(n)) gives the full
+ * generate_all_pairs_from_vector result (e.g. an all-reduce over ranks). */
+uint64_t sks_intersect_sym_tiles(uint32_t n);
+int sks_intersect_sym(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
+                      const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t tile_begin,
+                      uint64_t tile_end, int32_t* d_out);
+
 /* ---- diagnostics / tuning ------------------------------------------------------------- */
 /* Device time (ms) between the first and last launch of the last
  * sks_intersect_* call on this context (waits for it to finish). */

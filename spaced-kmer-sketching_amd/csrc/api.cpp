@@ -48,6 +48,7 @@ struct sks_ctx {
   sks::Scratch buf[10];             // dense working columns
   sks::Scratch flag, pos;
   sks::Scratch meta;                // small per-segment device arrays
+  sks::Scratch iwork;               // intersection bucket tables
   std::vector<uint64_t> meta_host;  // staging for `meta`
   sks_timings last{};
   int grid_override = 0;
@@ -244,6 +245,7 @@ int sks_ctx_destroy(sks_ctx* c) {
   c->flag.release();
   c->pos.release();
   c->meta.release();
+  c->iwork.release();
   (void)hipEventDestroy(c->ev_begin);
   (void)hipEventDestroy(c->ev_end);
   (void)hipEventDestroy(c->ev_s0);
@@ -363,17 +365,17 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
       K = col(c, 5);   // hi
       K2 = col(c, 6);  // lo
     }
-    SKS_HIP(sks::seg_unique_scan(K, K2, T, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
+    SKS_HIP(sks::seg_unique_scan(K, K2, T, max_len, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
     SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     SKS_HIP(hipStreamSynchronize(st));
     po.off = prefix(uniq);
     const uint64_t U = po.off[k];
     SKS_TRY(alloc_u64(&po.d, U * S.ew));
     if (!S.wide) {
-      SKS_HIP(sks::seg_unique_scatter(K, nullptr, T, d_csr, k, d_flag, d_pos, nullptr, nullptr,
+      SKS_HIP(sks::seg_unique_scatter(K, nullptr, T, max_len, d_csr, k, d_flag, d_pos, nullptr, nullptr,
                                       po.d, nullptr, st));
     } else {
-      SKS_HIP(sks::seg_unique_scatter(K2, K, T, d_csr, k, d_flag, d_pos, nullptr, nullptr,
+      SKS_HIP(sks::seg_unique_scatter(K2, K, T, max_len, d_csr, k, d_flag, d_pos, nullptr, nullptr,
                                       col(c, 7), col(c, 8), st));
       SKS_HIP(sks::launch_interleave(col(c, 7), col(c, 8), U, po.d, st));
     }
@@ -390,7 +392,8 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), T, csr, d_csr,
                                 end_bit_of(max_thr), c->tmp, st));
     LO = col(c, 4);
-    SKS_HIP(sks::seg_unique_scan(col(c, 3), nullptr, T, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
+    SKS_HIP(sks::seg_unique_scan(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos, d_uniq,
+                                 c->tmp, st));
   } else {
     // order (fmh, hi, lo) by an index permutation (LSD: lo, hi, fmh)
     uint64_t* idx = col(c, 9);
@@ -406,7 +409,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     SKS_HIP(sks::launch_gather(col(c, 2), col(c, 4), T, col(c, 8), st));  // hi
     LO = col(c, 7);
     HI = col(c, 8);
-    SKS_HIP(sks::seg_unique_scan(LO, HI, T, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
+    SKS_HIP(sks::seg_unique_scan(LO, HI, T, max_len, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
   }
   SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   SKS_HIP(hipStreamSynchronize(st));
@@ -437,11 +440,11 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   po.segs = keep_segs;
   po.off = keep_off;
   if (!S.wide) {
-    SKS_HIP(sks::seg_unique_scatter(LO, nullptr, T, d_csr, k, d_flag, d_pos, d_lim, d_dst,
+    SKS_HIP(sks::seg_unique_scatter(LO, nullptr, T, max_len, d_csr, k, d_flag, d_pos, d_lim, d_dst,
                                     col(c, 5), nullptr, st));
     SKS_HIP(sks::seg_sort_keys(col(c, 5), po.d, U, dst, d_dst, mask_lo_bits, c->tmp, st));
   } else {
-    SKS_HIP(sks::seg_unique_scatter(LO, HI, T, d_csr, k, d_flag, d_pos, d_lim, d_dst, col(c, 0),
+    SKS_HIP(sks::seg_unique_scatter(LO, HI, T, max_len, d_csr, k, d_flag, d_pos, d_lim, d_dst, col(c, 0),
                                     col(c, 1), st));
     SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), U, dst, d_dst, 64,
                                 c->tmp, st));
@@ -785,8 +788,41 @@ int sks_intersect_all(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
     return sks::fail(SKS_E_ARG, "sks_intersect_all: null argument");
   DeviceGuard g(c->device);
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
-  SKS_HIP(sks::launch_intersect_all(d_data, d_starts, d_sizes, elem_words, n, row_begin, row_end,
-                                    d_out, c->stream));
+  bool done = false;
+  if (elem_words == 1)
+    SKS_HIP(sks::launch_intersect_tiled(d_data, d_starts, d_sizes, n, false, row_begin, row_end, 0, 0,
+                                        d_out, c->iwork, c->stream, &done));
+  if (!done)
+    SKS_HIP(sks::launch_intersect_all_global(d_data, d_starts, d_sizes, elem_words, n, row_begin,
+                                             row_end, d_out, c->stream));
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+uint64_t sks_intersect_sym_tiles(uint32_t n) { return sks::intersect_sym_tiles(n); }
+
+int sks_intersect_sym(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
+                      const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t tile_begin,
+                      uint64_t tile_end, int32_t* d_out) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_sym: null ctx");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_sym: bad tile range");
+  if (n && (!d_starts || !d_sizes || !d_out)) return sks::fail(SKS_E_ARG, "sks_intersect_sym: null argument");
+  DeviceGuard g(c->device);
+  const uint64_t all = sks::intersect_sym_tiles(n);
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  bool done = false;
+  if (elem_words == 1)
+    SKS_HIP(sks::launch_intersect_tiled(d_data, d_starts, d_sizes, n, true, 0, n, tile_begin,
+                                        tile_end, d_out, c->iwork, c->stream, &done));
+  if (!done) {
+    if (tile_begin != 0 || tile_end < all)
+      return sks::fail(SKS_E_UNSUPPORTED,
+                       "sks_intersect_sym: partial tile ranges need u64 sketches without extreme "
+                       "value skew; use sks_intersect_all row blocks");
+    SKS_HIP(sks::launch_intersect_all_global(d_data, d_starts, d_sizes, elem_words, n, 0, n, d_out,
+                                             c->stream));
+  }
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;
 }

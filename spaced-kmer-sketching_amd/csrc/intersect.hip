@@ -3,13 +3,18 @@
 // The reference counts |A ∩ B| by iterating the smaller kmer_set and probing
 // the larger hash map (kmer_set.cpp:23-41), one pair per cilk_for iteration
 // (kmer_set.cpp:167-184).  Sketches here are sorted unique arrays, so a pair
-// is a sorted-merge count.  One 64-lane wavefront owns one pair: the smaller
-// sketch is split evenly over the lanes, each lane lower_bounds its first
-// element in the larger sketch and merges forward; a wave reduction gives the
-// count.  The result is the same integer the reference computes.
+// is a sorted-merge count — the same integer the reference computes.
+//   * k_tiles: the all-pairs path for u64 sketches (bucketed, LDS-tiled; see
+//     the comment above it).
+//   * k_pairs / k_all: one 64-lane wavefront per pair straight from global
+//     memory — pair lists, 128-bit k-mers, and the fallback for pathological
+//     value skew.  The smaller sketch is split evenly over the lanes, each lane
+//     lower_bounds its first element in the larger one and merges forward.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <vector>
 
 #include "sks_internal.hpp"
 
@@ -108,6 +113,161 @@ __global__ __launch_bounds__(kB) void k_all(const uint64_t* __restrict__ data,
   if ((threadIdx.x & 63) == 0) out[p] = c;
 }
 
+// ---- tiled all-pairs kernel (u64 sketches) ---------------------------------------------
+//
+// The value range is cut into B buckets by common boundaries (quantiles of the
+// largest sketch), so |S_i ∩ S_j| = Σ_b |S_i[b] ∩ S_j[b]|.  A workgroup owns a
+// 64 x 64 tile of (row, column) sketches and a group of buckets; per bucket it
+// stages the 128 bucket parts in LDS interleaved as lds[pos][slot] (slot =
+// sketch within the tile), then every lane merges one pair.  Lane l of a wave
+// always handles row l and column (l + k) mod 64, so the 32 lanes of each
+// ds_read_b64 group touch 32 distinct slots -> bank-conflict-free reads at any
+// merge positions.  Counts accumulate in registers across the bucket group and
+// leave with one atomicAdd per pair.
+constexpr int kTile = 64;
+constexpr int kSlots = 2 * kTile;
+constexpr int kMaxPart = 150;  // LDS: 150 * 128 * 8 = 153,600 B
+constexpr int kDiagPerWave = kTile / kWavesPerBlock;  // 16
+
+struct TileArgs {
+  const uint64_t* data;
+  const uint64_t* starts;
+  const uint32_t* sizes;
+  const uint32_t* pos;  // [n][B + 1] bucket boundaries (element index within sketch)
+  uint32_t n, B, buckets_per_group, n_groups;
+  uint32_t row_begin, row_end;  // rows mode: rows [row_begin, row_end) x all n columns
+  uint32_t n_col_blocks, n_row_blocks;
+  int sym;                      // 1: upper-triangle tiles, write both (i, j) and (j, i)
+  uint64_t tile_begin;
+  int32_t* out;
+  uint64_t ld;
+};
+
+__global__ void k_bounds(const uint64_t* __restrict__ data, uint64_t ref_start, uint32_t ref_size,
+                         uint32_t B, uint64_t* __restrict__ bounds) {
+  uint32_t b = blockIdx.x * kB + threadIdx.x;
+  if (b > B) return;
+  if (b == 0) bounds[0] = 0;
+  else if (b == B) bounds[B] = ~0ull;
+  else bounds[b] = data[ref_start + (uint64_t)b * ref_size / B];
+}
+
+__global__ void k_bucket_pos(const uint64_t* __restrict__ data, const uint64_t* __restrict__ starts,
+                             const uint32_t* __restrict__ sizes, uint32_t n, uint32_t B,
+                             const uint64_t* __restrict__ bounds, uint32_t* __restrict__ pos) {
+  uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  uint32_t i = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
+  if (i >= n) return;
+  uint32_t size = sizes[i];
+  uint32_t r;
+  if (b == 0) r = 0;
+  else if (b == B) r = size;
+  else {
+    const uint64_t* S = data + starts[i];
+    const uint64_t v = bounds[b];
+    uint32_t lo = 0, hi = size;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (S[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    r = lo;
+  }
+  pos[(uint64_t)i * (B + 1) + b] = r;
+}
+
+__device__ __forceinline__ void sym_tile(uint64_t t, uint32_t nb, uint32_t& I, uint32_t& J) {
+  uint32_t i = 0;
+  uint64_t rem = t;
+  while (rem >= nb - i) {  // row i of the upper triangle holds nb - i tiles
+    rem -= nb - i;
+    ++i;
+  }
+  I = i;
+  J = i + (uint32_t)rem;
+}
+
+__global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
+  __shared__ uint64_t lds[kMaxPart * kSlots];
+  __shared__ uint32_t s_len[kSlots];
+  const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
+  const uint32_t grp = blockIdx.x % a.n_groups;
+  uint32_t I, J;
+  if (a.sym) {
+    sym_tile(t, a.n_col_blocks, I, J);
+  } else {
+    I = (uint32_t)(t / a.n_col_blocks);
+    J = (uint32_t)(t % a.n_col_blocks);
+  }
+  const uint32_t row0 = (a.sym ? 0 : a.row_begin) + I * kTile;
+  const uint32_t row_lim = a.sym ? a.n : a.row_end;
+  const uint32_t col0 = J * kTile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // loader role: slot = sketch within the tile, par = which half of the positions
+  const uint32_t slot = tid & (kSlots - 1), par = tid >> 7;
+  const uint32_t sid = slot < kTile ? row0 + slot : col0 + (slot - kTile);
+  const bool sv = slot < kTile ? (sid < row_lim) : (sid < a.n);
+  const uint64_t sstart = sv ? a.starts[sid] : 0;
+  const uint32_t* spos = a.pos + (uint64_t)(sv ? sid : 0) * (a.B + 1);
+
+  uint32_t cnt[kDiagPerWave];
+#pragma unroll
+  for (int q = 0; q < kDiagPerWave; ++q) cnt[q] = 0;
+
+  const uint32_t b0 = grp * a.buckets_per_group;
+  const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
+  for (uint32_t b = b0; b < b1; ++b) {
+    uint32_t beg = 0, len = 0;
+    if (sv) {
+      beg = spos[b];
+      len = spos[b + 1] - beg;
+    }
+    if (par == 0) s_len[slot] = len;
+    const uint64_t* src = a.data + sstart + beg;
+    for (uint32_t j = par; j < len; j += 2) lds[j * kSlots + slot] = src[j];
+    __syncthreads();
+    // 16 independent merges per lane, advanced together so that 32 LDS reads
+    // are in flight per step (one wave per SIMD at this LDS footprint).
+    const uint32_t na = s_len[lane];
+    const uint64_t* A = lds + lane;
+    uint32_t ii[kDiagPerWave], jj[kDiagPerWave], nb[kDiagPerWave];
+#pragma unroll
+    for (int q = 0; q < kDiagPerWave; ++q) {
+      const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
+      nb[q] = s_len[kTile + c];
+      ii[q] = 0;
+      jj[q] = 0;
+    }
+    for (;;) {
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < kDiagPerWave; ++q) {
+        const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
+        const bool act = ii[q] < na && jj[q] < nb[q];
+        if (act) {
+          const uint64_t x = A[ii[q] * kSlots], y = lds[kTile + c + jj[q] * kSlots];
+          cnt[q] += (x == y);
+          ii[q] += (x <= y);
+          jj[q] += (y <= x);
+        }
+        any |= act;
+      }
+      if (!any) break;
+    }
+    __syncthreads();
+  }
+  const uint32_t r = row0 + lane;
+  if (r >= row_lim) return;
+#pragma unroll
+  for (int q = 0; q < kDiagPerWave; ++q) {
+    const uint32_t c = col0 + ((lane + wave * kDiagPerWave + q) & (kTile - 1));
+    if (c >= a.n || cnt[q] == 0) continue;
+    const uint64_t orow = a.sym ? r : (r - a.row_begin);
+    atomicAdd(&a.out[orow * a.ld + c], (int32_t)cnt[q]);
+    if (a.sym && I != J) atomicAdd(&a.out[(uint64_t)c * a.ld + r], (int32_t)cnt[q]);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
@@ -124,9 +284,10 @@ hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
   return hipGetLastError();
 }
 
-hipError_t launch_intersect_all(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                                int elem_words, uint32_t n, uint32_t row_begin, uint32_t row_end,
-                                int32_t* out, hipStream_t s) {
+hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* starts,
+                                       const uint32_t* sizes, int elem_words, uint32_t n,
+                                       uint32_t row_begin, uint32_t row_end, int32_t* out,
+                                       hipStream_t s) {
   uint64_t n_pairs = (uint64_t)(row_end - row_begin) * n;
   if (n_pairs == 0) return hipSuccess;
   uint64_t blocks = (n_pairs + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -137,6 +298,92 @@ hipError_t launch_intersect_all(const uint64_t* data, const uint64_t* starts, co
     hipLaunchKernelGGL(k_all<2>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, n,
                        row_begin, n_pairs, out);
   return hipGetLastError();
+}
+
+}  // namespace sks
+
+namespace sks {
+
+// Tiled all-pairs for u64 sketches.  Host-synchronous (reads sizes and bucket
+// positions back to pick the bucket count).  mode: sym (upper-triangle tiles
+// [tile_begin, tile_end) into a full n x n matrix) or rows.
+hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                                  uint32_t n, bool sym, uint32_t row_begin, uint32_t row_end,
+                                  uint64_t tile_begin, uint64_t tile_end, int32_t* out,
+                                  Scratch& work, hipStream_t s, bool* used_tiles) {
+  *used_tiles = false;
+  hipError_t e;
+  const uint64_t out_words = sym ? (uint64_t)n * n : (uint64_t)(row_end - row_begin) * n;
+  if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
+  if (n == 0 || out_words == 0) { *used_tiles = true; return hipSuccess; }
+  std::vector<uint32_t> h_sizes(n);
+  std::vector<uint64_t> h_starts(n);
+  if ((e = hipMemcpyAsync(h_sizes.data(), sizes, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(h_starts.data(), starts, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  uint32_t ref = 0;
+  for (uint32_t i = 1; i < n; ++i) if (h_sizes[i] > h_sizes[ref]) ref = i;
+  const uint32_t max_size = h_sizes[ref];
+  if (max_size == 0) { *used_tiles = true; return hipSuccess; }
+  uint32_t B = 1;
+  while ((uint64_t)B * 64 < max_size) B <<= 1;
+  std::vector<uint32_t> h_pos;
+  uint32_t P = 0;
+  for (;;) {
+    size_t bytes = sizeof(uint64_t) * (B + 1) + sizeof(uint32_t) * (uint64_t)n * (B + 1) + 64;
+    if ((e = work.reserve(bytes)) != hipSuccess) return e;
+    uint64_t* bounds = reinterpret_cast<uint64_t*>(work.ptr);
+    uint32_t* pos = reinterpret_cast<uint32_t*>(bounds + B + 1);
+    hipLaunchKernelGGL(k_bounds, dim3((B + 1 + kB - 1) / kB), dim3(kB), 0, s, data, h_starts[ref],
+                       max_size, B, bounds);
+    uint64_t items = (uint64_t)n * (B + 1);
+    hipLaunchKernelGGL(k_bucket_pos, dim3((unsigned)((items + kB - 1) / kB)), dim3(kB), 0, s, data,
+                       starts, sizes, n, B, bounds, pos);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    h_pos.resize(items);
+    if ((e = hipMemcpyAsync(h_pos.data(), pos, items * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    P = 0;
+    for (uint32_t i = 0; i < n; ++i)
+      for (uint32_t b = 0; b < B; ++b)
+        P = std::max(P, h_pos[(uint64_t)i * (B + 1) + b + 1] - h_pos[(uint64_t)i * (B + 1) + b]);
+    if (P <= (uint32_t)kMaxPart) break;
+    if (B >= (1u << 16)) return hipSuccess;  // pathological skew: caller falls back
+    B <<= 1;
+  }
+  TileArgs a{};
+  a.data = data;
+  a.starts = starts;
+  a.sizes = sizes;
+  a.pos = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(work.ptr) + B + 1);
+  a.n = n;
+  a.B = B;
+  a.sym = sym ? 1 : 0;
+  a.n_col_blocks = (n + kTile - 1) / kTile;
+  a.row_begin = row_begin;
+  a.row_end = row_end;
+  a.n_row_blocks = sym ? a.n_col_blocks : (row_end - row_begin + kTile - 1) / kTile;
+  const uint64_t all_tiles = sym ? (uint64_t)a.n_col_blocks * (a.n_col_blocks + 1) / 2
+                                 : (uint64_t)a.n_row_blocks * a.n_col_blocks;
+  if (!sym) { tile_begin = 0; tile_end = all_tiles; }
+  tile_end = std::min(tile_end, all_tiles);
+  if (tile_begin >= tile_end) { *used_tiles = true; return hipSuccess; }
+  const uint64_t tiles = tile_end - tile_begin;
+  uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (2048 + tiles - 1) / tiles));
+  a.buckets_per_group = (B + groups - 1) / groups;
+  a.n_groups = (B + a.buckets_per_group - 1) / a.buckets_per_group;
+  a.tile_begin = tile_begin;
+  a.out = out;
+  a.ld = n;
+  hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), 0, s, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  *used_tiles = true;
+  return hipSuccess;
+}
+
+uint64_t intersect_sym_tiles(uint32_t n) {
+  uint64_t nb = (n + kTile - 1) / kTile;
+  return nb * (nb + 1) / 2;
 }
 
 }  // namespace sks

@@ -220,13 +220,13 @@ hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d
 }
 
 hipError_t seg_unique_scan(const uint64_t* keys, const uint64_t* keys2, uint64_t total,
-                           const uint64_t* d_off, uint32_t n_seg, uint32_t* d_flag, uint64_t* d_pos,
-                           uint64_t* d_uniq, Scratch& tmp, hipStream_t s) {
+                           uint64_t max_len, const uint64_t* d_off, uint32_t n_seg, uint32_t* d_flag,
+                           uint64_t* d_pos, uint64_t* d_uniq, Scratch& tmp, hipStream_t s) {
   if (n_seg == 0) return hipSuccess;
   hipError_t e;
   if (total) {
     // max segment length bound: total (grid-stride loop covers any length)
-    hipLaunchKernelGGL(k_flags, dim3(grid_for(std::min<uint64_t>(total, 1ull << 24)), n_seg),
+    hipLaunchKernelGGL(k_flags, dim3(grid_for(std::min<uint64_t>(max_len, 1ull << 24)), n_seg),
                        dim3(kB), 0, s, keys, keys2, d_off, d_flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
@@ -246,12 +246,13 @@ hipError_t seg_unique_scan(const uint64_t* keys, const uint64_t* keys2, uint64_t
 }
 
 hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint64_t total,
-                              const uint64_t* d_off, uint32_t n_seg, const uint32_t* d_flag,
+                              uint64_t max_len, const uint64_t* d_off, uint32_t n_seg,
+                              const uint32_t* d_flag,
                               const uint64_t* d_pos, const uint64_t* d_limit,
                               const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
                               hipStream_t s) {
   if (n_seg == 0 || total == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter, dim3(grid_for(std::min<uint64_t>(total, 1ull << 24)), n_seg),
+  hipLaunchKernelGGL(k_scatter, dim3(grid_for(std::min<uint64_t>(max_len, 1ull << 24)), n_seg),
                      dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos, d_limit, d_dst_off, out,
                      out2);
   return hipGetLastError();

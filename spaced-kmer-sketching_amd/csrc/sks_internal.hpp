@@ -71,15 +71,17 @@ hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d
 // writes d_flag_pos (exclusive scan of "first of run" flags) and per-segment
 // unique counts d_uniq[g].  Keys equal in key (and key2 when non-null) are
 // one element.
+// max_len: longest segment (sizes the grid; segments are grid-strided).
 hipError_t seg_unique_scan(const uint64_t* keys, const uint64_t* keys2, uint64_t total,
-                           const uint64_t* d_off, uint32_t n_seg, uint32_t* d_flag,
+                           uint64_t max_len, const uint64_t* d_off, uint32_t n_seg, uint32_t* d_flag,
                            uint64_t* d_pos, uint64_t* d_uniq, Scratch& tmp, hipStream_t s);
 // Scatter the first `limit[g]` unique elements of each segment:
 // out[dst_off[g] + rank] = vals[i] (and out2 from vals2 when non-null).
 // limit == nullptr keeps every unique element; dst_off == nullptr places
 // segment g at pos[off[g]] (the global unique rank, i.e. dense CSR output).
 hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint64_t total,
-                              const uint64_t* d_off, uint32_t n_seg, const uint32_t* d_flag,
+                              uint64_t max_len, const uint64_t* d_off, uint32_t n_seg,
+                              const uint32_t* d_flag,
                               const uint64_t* d_pos, const uint64_t* d_limit,
                               const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
                               hipStream_t s);
@@ -88,9 +90,19 @@ hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint6
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
                                   const uint32_t* sizes, int elem_words, const int32_t* a,
                                   const int32_t* b, uint64_t n_pairs, int32_t* out, hipStream_t s);
-hipError_t launch_intersect_all(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                                int elem_words, uint32_t n, uint32_t row_begin, uint32_t row_end,
-                                int32_t* out, hipStream_t s);
+hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* starts,
+                                       const uint32_t* sizes, int elem_words, uint32_t n,
+                                       uint32_t row_begin, uint32_t row_end, int32_t* out,
+                                       hipStream_t s);
+// Tiled u64 all-pairs (intersect.hip).  sym: upper-triangle tiles
+// [tile_begin, tile_end) written to both halves of an n x n matrix; otherwise
+// rows [row_begin, row_end) x n.  Zeroes `out` first.  *used_tiles = false
+// means the value distribution was too skewed: use the global kernel.
+hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                                  uint32_t n, bool sym, uint32_t row_begin, uint32_t row_end,
+                                  uint64_t tile_begin, uint64_t tile_end, int32_t* out,
+                                  Scratch& work, hipStream_t s, bool* used_tiles);
+uint64_t intersect_sym_tiles(uint32_t n);
 
 // ---- misc kernels (post.hip) -------------------------------------------------------------
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,

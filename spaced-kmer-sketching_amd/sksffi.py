@@ -46,7 +46,7 @@ EXPORTED = [
     "sks_sketch_set_sizes", "sks_sketch_set_windows", "sks_sketch_set_device_data",
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
-    "sks_synth_bases",
+    "sks_synth_bases", "sks_intersect_sym", "sks_intersect_sym_tiles",
 ]
 
 _lib = None
@@ -107,6 +107,10 @@ def lib():
     L.sks_intersect_pairs.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp, C.c_uint64, vp]
     L.sks_intersect_all.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32,
                                     vp]
+    L.sks_intersect_sym.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint64, C.c_uint64,
+                                    vp]
+    L.sks_intersect_sym_tiles.argtypes = [C.c_uint32]
+    L.sks_intersect_sym_tiles.restype = C.c_uint64
     L.sks_synth_bases.argtypes = [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_double,
                                   C.c_uint64]
     _lib = L
@@ -137,6 +141,10 @@ def mask_contiguous(length):
 
 def frac_min_hash(kmer, mask, window, nonce=1, flavour=0):
     return int(lib().sks_frac_min_hash(_mask_arr(kmer), _mask_arr(mask), window, nonce, flavour))
+
+
+def intersect_sym_tiles(n):
+    return int(lib().sks_intersect_sym_tiles(n))
 
 
 def containment(inter, size):
@@ -267,6 +275,11 @@ class Context:
                       out_ptr):
         check(lib().sks_intersect_all(self.h, data_ptr, starts_ptr, sizes_ptr, elem_words, n,
                                       row_begin, row_end, out_ptr))
+
+    def intersect_sym(self, data_ptr, starts_ptr, sizes_ptr, elem_words, n, tile_begin, tile_end,
+                      out_ptr):
+        check(lib().sks_intersect_sym(self.h, data_ptr, starts_ptr, sizes_ptr, elem_words, n,
+                                      tile_begin, tile_end, out_ptr))
 
     def synth_bases(self, d_out_ptr, n, seed, mut_seed=0, mut_rate=0.0, pos_offset=0):
         check(lib().sks_synth_bases(self.h, C.c_void_p(d_out_ptr), n, seed, mut_seed, mut_rate,

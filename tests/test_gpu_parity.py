@@ -251,3 +251,40 @@ def test_argument_errors(torch_cuda, ctx):
         assert e.value.code == code
     with pytest.raises(sksffi.SksError):
         ctx.sketch_build(d.data_ptr(), 9, [0, 10], 4, m, sksffi.SKS_FRAC_MOD, 5)
+
+
+def test_many_sketches_tiled_and_symmetric(torch_cuda, ctx):
+    """130 sketches (3 tile blocks, ragged last block) of varied sizes: the
+    tiled all-pairs kernel, its row-block form, and the symmetric tile form
+    split across 3 'ranks' and summed, all equal the oracle's merge counts."""
+    torch = torch_cuda
+    n = 130
+    genomes = []
+    for i in range(n):
+        fam = i % 5
+        L = 3000 + 97 * (i % 23)
+        g = synth.bases(L, seed=700 + fam, mut_seed=900 + i, mut_rate=0.003 * (i % 7))
+        genomes.append(g.tobytes() if i % 31 else b"")
+    w = 21
+    m = O.mask(w, w, 0)
+    ss, _ = build(torch, ctx, genomes, w, m, "frac", 3)
+    sk = [O.sketch(O.cut_runs(g), w, m, "frac", 3)[0] for g in genomes]
+    want = np.array([[O.intersect(sk[i], sk[j]) for j in range(n)] for i in range(n)])
+    data, starts, sizes = ss.device_ptrs()
+    out = torch.full((n * n,), -7, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_all(data, starts, sizes, 1, n, 0, n, out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(n, n), want)
+    rows = torch.zeros(((70 - 65) * n,), dtype=torch.int32, device="cuda:0")
+    ctx.intersect_all(data, starts, sizes, 1, n, 65, 70, rows.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(rows.cpu().numpy().reshape(5, n), want[65:70])
+    T = sksffi.intersect_sym_tiles(n)
+    assert T == 6
+    acc = np.zeros((n, n), dtype=np.int64)
+    for (a, b) in [(0, 2), (2, 3), (3, T)]:
+        part = torch.full((n * n,), 5, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_sym(data, starts, sizes, 1, n, a, b, part.data_ptr())
+        torch.cuda.synchronize()
+        acc += part.cpu().numpy().reshape(n, n)
+    assert np.array_equal(acc, want)
