@@ -1,0 +1,125 @@
+// Drives the reference-named C++ facade the way the reference's own driver
+// does (kmer-sketching.cpp:151-212) and prints JSON for tests/test_facade.py.
+//   test_facade sketch <w> <k> <mask_seed> <c|s> <frac|bottom> <file>...
+//   test_facade errors
+//   test_facade missing <file>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ani_estimator.hpp"
+#include "fasta_processing.hpp"
+#include "generators.hpp"
+#include "kmer.hpp"
+
+static void hexset(const kmer_set& ks) {
+  std::printf("[");
+  for (size_t i = 0; i < ks.elements.size(); ++i) {
+    const kmer_bitset& e = ks.elements[i];
+    std::printf("%s\"%016llx%016llx\"", i ? "," : "", (unsigned long long)e.hi(),
+                (unsigned long long)e.lo());
+  }
+  std::printf("]");
+}
+
+static int sketch(int argc, char** argv) {
+  const int w = std::atoi(argv[2]), k = std::atoi(argv[3]);
+  const size_t seed = std::strtoull(argv[4], nullptr, 10);
+  const uint64_t param = std::strtoull(argv[5], nullptr, 10);
+  const bool bottom = std::string(argv[6]) == "bottom";
+  const int n = argc - 7;
+  char** files = argv + 7;
+
+  kmer_bitset mask = generate_random_spaced_seed_mask(w, k, seed);
+  const int kmer_num_indices = (int)(mask.count() / NUCLEOTIDE_BIT_SIZE);
+  frac_min_hash fmh(1);
+  sketch_policy policy = bottom ? sketch_policy::bottom(param) : sketch_policy(frac_mod_condition{fmh, param});
+  std::vector<kmer_set> data = parallel_kmer_sets_from_fasta_files(n, files, mask, w, policy);
+  std::vector<kmer_set> serial = kmer_sets_from_fasta_files(n, files, mask, w, policy);
+  std::vector<kmer_set*> ptrs;
+  for (auto& s : data) ptrs.push_back(&s);
+  auto pairs = generate_all_pairs_from_vector<kmer_set*>(ptrs);
+  std::vector<int> inter = parallel_compute_pairwise_kmer_set_intersections(pairs.first, pairs.second);
+  std::vector<int> inter2 = compute_pairwise_kmer_set_intersections(pairs.first, pairs.second);
+
+  std::printf("{\"mask\":\"%016llx%016llx\",\"k\":%d,\"sets\":[", (unsigned long long)mask.hi(),
+              (unsigned long long)mask.lo(), kmer_num_indices);
+  for (int i = 0; i < n; ++i) {
+    if (i) std::printf(",");
+    hexset(data[i]);
+  }
+  bool same = true;
+  for (int i = 0; i < n; ++i) same = same && data[i].elements == serial[i].elements;
+  std::printf("],\"serial_equal\":%s,\"inter\":[", same ? "true" : "false");
+  for (size_t i = 0; i < inter.size(); ++i) std::printf("%s%d", i ? "," : "", inter[i]);
+  std::printf("],\"inter_serial_equal\":%s,\"ani\":[", inter == inter2 ? "true" : "false");
+  for (size_t i = 0; i < inter.size(); ++i) {
+    double c = containment(inter[i], pairs.first[i]->kmer_set_size());
+    std::printf("%s\"%a\"", i ? "," : "", binomial_estimator(c, kmer_num_indices));
+  }
+  // single-pair API and membership
+  int single = n > 1 ? kmer_set_intersection(data[0], data[1]) : -1;
+  std::printf("],\"single01\":%d", single);
+  if (n > 0) {
+    auto runs = nucleotide_strings_from_fasta_file(files[0]);
+    kmer_set viaruns = nucleotide_string_list_to_kmer_set(runs, mask, w, policy);
+    std::printf(",\"runs_equal\":%s", viaruns.elements == data[0].elements ? "true" : "false");
+    auto raw = strings_from_fasta(files[0]);
+    auto cut = cut_nucleotide_strings(raw);
+    std::printf(",\"cut_equal\":%s,\"records\":%zu", cut == runs ? "true" : "false", raw.size());
+  }
+  std::printf("}\n");
+  return 0;
+}
+
+static int errors() {
+  int ok = 0;
+  try {
+    contiguous_kmer(65);
+  } catch (const std::runtime_error& e) {
+    ok += std::string(e.what()) == "Given k-mer length exceeds maximum k-mer length";
+  }
+  kmer_set a, b;
+  std::vector<kmer_set*> one{&a}, two{&a, &b};
+  try {
+    compute_pairwise_kmer_set_intersections(one, two);
+  } catch (const std::runtime_error& e) {
+    ok += std::string(e.what()) ==
+          "Lists of kmer sets for intersection computation have different lengths";
+  }
+  // canonical_kmer / reverse_complement on a palindromic contiguous mask (kmers.cpp)
+  kmer_bitset m = contiguous_kmer(4);
+  kmer x{4, kmer_bitset(0b00011011, 0), m, kmer_bitset(0b00011011, 0)};  // ACGT
+  kmer rc = reverse_complement(x);
+  ok += rc.masked_bits == kmer_bitset(0b00011011, 0);  // ACGT is its own reverse complement
+  kmer y{4, kmer_bitset(0b11111111, 0), m, kmer_bitset(0b11111111, 0)};  // TTTT -> AAAA
+  ok += canonical_kmer(y).masked_bits == kmer_bitset(0, 0);
+  // insert_kmers collapses duplicates; contains()
+  kmer_set s;
+  s.insert_kmers({y, y, x});
+  ok += s.kmer_set_size() == 2 && s.contains(x);
+  // frac_min_hash matches sks_frac_min_hash
+  frac_min_hash f(1);
+  uint64_t kk[2] = {x.masked_bits.lo(), 0}, mm[2] = {m.lo(), 0};
+  ok += f(x) == sks_frac_min_hash(kk, mm, 4, 1, 0);
+  std::printf("{\"errors_ok\":%d}\n", ok);
+  return ok == 6 ? 0 : 2;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 64;
+  std::string mode = argv[1];
+  if (mode == "sketch" && argc >= 8) return sketch(argc, argv);
+  if (mode == "errors") return errors();
+  if (mode == "missing" && argc == 3) {
+    char* f[1] = {argv[2]};
+    kmer_bitset mask = generate_random_spaced_seed_mask(21, 21, 0);
+    parallel_kmer_sets_from_fasta_files(1, f, mask, 21, frac_mod_condition{frac_min_hash(1), 200});
+    return 0;  // unreachable: exit(1) like fasta_processing.cpp:86-90
+  }
+  return 64;
+}

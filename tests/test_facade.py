@@ -1,0 +1,75 @@
+"""The reference-named C++ facade (spaced-kmer-sketching_amd/cpp/*.hpp) driven
+like the reference's own driver (kmer-sketching.cpp:151-212) by
+tests/cpp/test_facade.cpp, compared with the oracle."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_facade")
+
+
+def build_facade_test():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+
+
+@pytest.fixture(scope="module")
+def facade_bin():
+    if not os.path.exists(BIN):
+        build_facade_test()
+    return BIN
+
+
+def test_facade_host_semantics(facade_bin):
+    r = subprocess.run([facade_bin, "errors"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert json.loads(r.stdout)["errors_ok"] == 6
+
+
+def test_facade_missing_file_exits_like_reference(facade_bin, tmp_path):
+    missing = str(tmp_path / "nope.fa")
+    r = subprocess.run([facade_bin, "missing", missing], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1
+    assert r.stderr.startswith(f"Unable to open {missing}. \n Exiting...")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,k,seed,param,kind", [(21, 21, 0, 200, "frac"), (31, 21, 0, 50, "frac"),
+                                                 (31, 21, 3, 300, "bottom"), (40, 30, 0, 40, "frac")])
+def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
+    files = []
+    for i in range(4):
+        g = synth.bases(30000, seed=77, mut_seed=500 + i, mut_rate=0.01 * i)
+        if i == 3:
+            g[1000:1010] = ord("N")
+        p = tmp_path / f"g{i}.fa"
+        p.write_bytes(synth.fasta_text([(f"g{i}_a", g[:17000]), (f"g{i}_b", g[17000:])], width=70))
+        files.append(str(p))
+    r = subprocess.run([facade_bin, "sketch", str(w), str(k), str(seed), str(param), kind] + files,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    m = O.mask(w, k, seed)
+    assert int(out["mask"], 16) == m
+    sk = []
+    for i, f in enumerate(files):
+        want, _ = O.sketch(O.fasta_runs(f), w, m, kind, param)
+        got = [int(h, 16) for h in out["sets"][i]]
+        assert got == [int(lo) | int(hi) << 64 for lo, hi in want], (i, w, kind)
+        sk.append(want)
+    n = len(files)
+    inter = [O.intersect(sk[i], sk[j]) for i in range(n) for j in range(n)]
+    assert out["inter"] == inter
+    assert out["serial_equal"] and out["inter_serial_equal"] and out["runs_equal"] and out["cut_equal"]
+    assert out["single01"] == inter[1]
+    kk = bin(m).count("1") // 2
+    assert out["k"] == kk
+    for p, (i, j) in enumerate([(i, j) for i in range(n) for j in range(n)]):
+        c = O.containment(inter[p], len(sk[i]))
+        assert float.fromhex(out["ani"][p]) == O.binomial_estimator(c, kk)
