@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "sks_hash.hpp"
 #include "sks_internal.hpp"
@@ -189,10 +190,12 @@ __device__ __forceinline__ void select_window(const ScanParams& p, Queue<MODE>& 
   }
 }
 
+constexpr int kBeOff = 2;  // s_be[kBeOff + i] = word i; two zero words in front
+
 template <int MODE, int FLAVOUR>
 __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
   __shared__ uint32_t s_raw[kLoadVecs * 4];
-  __shared__ uint32_t s_be[kWords + 2];
+  __shared__ uint32_t s_be[kWords + 2 + kBeOff];
   __shared__ uint32_t s_lc[kWords + 2];
   __shared__ uint32_t s_inv[kWords + 2];
   __shared__ Queue<MODE> q;
@@ -204,9 +207,15 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
   if (t_begin >= t_end) return;
 
   const int w = p.w;
-  const uint32_t fshift = 64 - 2 * w;            // F right-alignment (w <= 32)
+  // F of the window at base b is read as the 64 big-endian bits starting at
+  // base b - (32 - w): its low 2w bits are F, the bits above are older bases
+  // that the mask (bits < 2w) removes, so no per-window shift is needed.
+  const uint32_t dshift = 2 * (32 - w);          // 0..62 bits
+  const bool dword = dshift >= 32;
+  const uint32_t dbits = dshift & 31;
   const uint64_t wmask_bits = (w >= 64) ? ~0ull : ((1ull << w) - 1);
   const uint64_t region_bits = (kWPT - 1 + w >= 64) ? ~0ull : ((1ull << (kWPT - 1 + w)) - 1);
+  if (tid < kBeOff) s_be[tid] = 0;
 
   // segment cursors (wave-uniform) for the current tile and the prefetch
   uint32_t seg_lo = 0, seg_hi = p.n_seg;
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
         le |= le8 << (8 * k);
         inv |= inv4 << (4 * k);
       }
-      s_be[i] = rev_pairs(le);
+      s_be[kBeOff + i] = rev_pairs(le);
       s_lc[i] = ~le;
       s_inv[i] = inv;
     }
@@ -273,27 +282,39 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
     }
 
     // 4) 16 windows per lane: starts 16*tid + j
-    const uint32_t be0 = s_be[tid], be1 = s_be[tid + 1], be2 = s_be[tid + 2];
+    uint32_t be[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) be[k] = s_be[kBeOff + tid - 2 + k];  // words tid-2 .. tid+2
+    uint32_t bs[3];  // BE words shifted back by (32 - w) bases
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t hi = dword ? be[k] : be[k + 1];
+      const uint32_t lo = dword ? be[k + 1] : be[k + 2];
+      bs[k] = funnel(hi, lo, dbits);
+    }
     const uint32_t lc0 = s_lc[tid], lc1 = s_lc[tid + 1], lc2 = s_lc[tid + 2];
     const uint64_t inv64 = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) |
                            ((uint64_t)s_inv[tid + 2] << 32) | ((uint64_t)s_inv[tid + 3] << 48);
     const bool lane_clean = (inv64 & region_bits) == 0;
-    const bool wave_clean = __all(lane_clean);
-
+    auto windows = [&](auto checked) {
 #pragma unroll
-    for (int j = 0; j < kWPT; ++j) {
-      uint32_t fh = j ? funnel(be0, be1, 32 - 2 * j) : be0;
-      uint32_t fl = j ? funnel(be1, be2, 32 - 2 * j) : be1;
-      uint64_t F = ((((uint64_t)fh) << 32) | fl) >> fshift;
-      uint32_t rl = j ? funnel(lc1, lc0, 2 * j) : lc0;
-      uint32_t rh = j ? funnel(lc2, lc1, 2 * j) : lc1;
-      uint64_t R = (((uint64_t)rh) << 32) | rl;
-      uint64_t fm = F & p.mask_lo, rm = R & p.mask_lo;
-      uint64_t c = fm < rm ? fm : rm;
-      bool valid = wave_clean || (((inv64 >> j) & wmask_bits) == 0);
-      win_count += valid ? 1u : 0u;
-      select_window<MODE, FLAVOUR>(p, q, g.seg, thresh, valid, c);
-    }
+      for (int j = 0; j < kWPT; ++j) {
+        const uint32_t fh = j ? funnel(bs[0], bs[1], 32 - 2 * j) : bs[0];
+        const uint32_t fl = j ? funnel(bs[1], bs[2], 32 - 2 * j) : bs[1];
+        const uint64_t F = (((uint64_t)fh) << 32) | fl;
+        const uint32_t rl = j ? funnel(lc1, lc0, 2 * j) : lc0;
+        const uint32_t rh = j ? funnel(lc2, lc1, 2 * j) : lc1;
+        const uint64_t R = (((uint64_t)rh) << 32) | rl;
+        const uint64_t fm = F & p.mask_lo, rm = R & p.mask_lo;
+        const uint64_t c = fm < rm ? fm : rm;
+        bool valid = true;
+        if constexpr (decltype(checked)::value) valid = ((inv64 >> j) & wmask_bits) == 0;
+        win_count += valid ? 1u : 0u;
+        select_window<MODE, FLAVOUR>(p, q, g.seg, thresh, valid, c);
+      }
+    };
+    if (__all(lane_clean)) windows(std::false_type{});
+    else windows(std::true_type{});
 
     // 5) flush the queue once it is half full
     __syncthreads();

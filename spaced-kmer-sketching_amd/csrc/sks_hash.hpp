@@ -22,12 +22,30 @@ constexpr uint64_t kMixMul = 0x0e9846af9b1a615dULL;   // boost hash_mix<64> mult
 constexpr uint64_t kMurmurMul = 0xc6a4a7935bd1e995ULL;
 constexpr uint64_t kMurmurAdd = 0xe6546b64ULL;
 
+// x * M (mod 2^64) for a compile-time constant M.  On gfx950 every 32-bit
+// integer multiply issues at the rate of any other VOP3 op, so the cost is the
+// instruction count: this lowering uses 1 v_mul_lo_u32 + 2 v_mad_u64_u32
+// (the compiler's default is 2 v_mul_lo_u32 + 1 v_mad_u64_u32 + 1 v_add3_u32);
+// measured 15% faster in tools/microbench/isa_rates.hip.
+template <uint64_t M>
+SKS_HD uint64_t mul_const(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // written so that hipcc emits v_mul_lo_u32 + 2 x v_mad_u64_u32 (the low
+  // word of hi*mlo + lo*mhi is formed by the first mad's 32-bit add)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t cross = hi * (uint32_t)M + lo * (uint32_t)(M >> 32);
+  return (uint64_t)lo * (uint32_t)M + ((uint64_t)cross << 32);
+#else
+  return x * M;
+#endif
+}
+
 // Flavour B (Boost >= 1.81): boost::hash_detail::hash_mix_impl<64>::fn
 SKS_HD uint64_t hash_mix(uint64_t x) {
   x ^= x >> 32;
-  x *= kMixMul;
+  x = mul_const<kMixMul>(x);
   x ^= x >> 32;
-  x *= kMixMul;
+  x = mul_const<kMixMul>(x);
   x ^= x >> 28;
   return x;
 }
@@ -35,11 +53,11 @@ SKS_HD uint64_t combine_mix(uint64_t seed, uint64_t v) { return hash_mix(seed + 
 
 // Flavour A (Boost 1.71-1.80): boost::hash_detail::hash_combine_impl (64-bit)
 SKS_HD uint64_t combine_legacy(uint64_t h, uint64_t k) {
-  k *= kMurmurMul;
+  k = mul_const<kMurmurMul>(k);
   k ^= k >> 47;
-  k *= kMurmurMul;
+  k = mul_const<kMurmurMul>(k);
   h ^= k;
-  h *= kMurmurMul;
+  h = mul_const<kMurmurMul>(h);
   h += kMurmurAdd;
   return h;
 }
@@ -92,8 +110,15 @@ inline DivTest make_div_test(uint64_t c) {
   return t;
 }
 
+// x * m (mod 2^64) for a wave-uniform runtime m (same lowering as mul_const).
+SKS_HD uint64_t mul_uniform(uint64_t x, uint64_t m) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t cross = hi * (uint32_t)m + lo * (uint32_t)(m >> 32);
+  return (uint64_t)lo * (uint32_t)m + ((uint64_t)cross << 32);
+}
+
 SKS_HD bool div_test(uint64_t x, uint64_t low_mask, uint32_t shift, uint64_t dinv, uint64_t dlim) {
-  return ((x & low_mask) == 0) & (((x >> shift) * dinv) <= dlim);
+  return ((x & low_mask) == 0) & (mul_uniform(x >> shift, dinv) <= dlim);
 }
 
 // splitmix64 output p of a stream seeded with `seed` (synthetic genomes).
