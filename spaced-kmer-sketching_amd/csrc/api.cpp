@@ -494,7 +494,10 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
                sks::fmh_const(mask[0], mask[1], window, policy->nonce, policy->flavour), {}};
   if (policy->kind == SKS_FRAC_MOD) S.dt = sks::make_div_test(policy->param);
   const bool bottom = policy->kind == SKS_BOTTOM_S;
-  const double alpha = 2.0;
+  // bottom-s candidate margin: the first threshold keeps ~alpha*s windows, at
+  // least 10 standard deviations above s for s >= 100 (a shortfall re-scans
+  // that genome with a larger threshold).
+  const double alpha = 1.0 + 10.0 / std::sqrt((double)policy->param) + 1.0 / (double)policy->param;
 
   sks_timings tm{};
   SKS_HIP(hipEventRecord(c->ev_begin, st));
@@ -563,10 +566,9 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
     p.mask_lo = S.mask_lo;
     p.mask_hi = S.mask_hi;
     p.kconst = S.kconst;
-    p.low_mask = S.dt.low_mask;
-    p.shift = S.dt.shift;
+    p.rot = S.dt.rot;
     p.dinv = S.dt.dinv;
-    p.dlim = S.dt.dlim;
+    p.dlim = S.dt.lim;
     p.seg_thresh = arena.ptr(o_thr);
     p.out_key = reinterpret_cast<uint64_t*>(c->rec[0].ptr);
     p.out_val = reinterpret_cast<uint64_t*>(c->rec[1].ptr);

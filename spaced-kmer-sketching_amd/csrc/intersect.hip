@@ -238,21 +238,24 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
       ii[q] = 0;
       jj[q] = 0;
     }
+    // branch-free steps: every lane issues all 32 reads each iteration
+    // (indices clamped), so the reads of the 16 merges overlap
+    const uint32_t na1 = na ? na - 1 : 0;
     for (;;) {
-      bool any = false;
+      uint32_t any = 0;
 #pragma unroll
       for (int q = 0; q < kDiagPerWave; ++q) {
         const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
-        const bool act = ii[q] < na && jj[q] < nb[q];
-        if (act) {
-          const uint64_t x = A[ii[q] * kSlots], y = lds[kTile + c + jj[q] * kSlots];
-          cnt[q] += (x == y);
-          ii[q] += (x <= y);
-          jj[q] += (y <= x);
-        }
+        const uint32_t nb1 = nb[q] ? nb[q] - 1 : 0;
+        const uint64_t x = A[min(ii[q], na1) * kSlots];
+        const uint64_t y = lds[kTile + c + min(jj[q], nb1) * kSlots];
+        const uint32_t act = (ii[q] < na) & (jj[q] < nb[q]);
+        cnt[q] += act & (uint32_t)(x == y);
+        ii[q] += act & (uint32_t)(x <= y);
+        jj[q] += act & (uint32_t)(y <= x);
         any |= act;
       }
-      if (!any) break;
+      if (!__any(any)) break;
     }
     __syncthreads();
   }

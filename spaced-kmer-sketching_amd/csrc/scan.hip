@@ -182,7 +182,7 @@ __device__ __forceinline__ void select_window(const ScanParams& p, Queue<MODE>& 
   }
   uint64_t f = h ^ p.kconst;
   bool keep;
-  if constexpr (MODE == kModeFrac) keep = div_test(f, p.low_mask, p.shift, p.dinv, p.dlim);
+  if constexpr (MODE == kModeFrac) keep = div_test(f, p.rot, p.dinv, p.dlim);
   else keep = f <= thresh;
   if (valid && keep) {
     if constexpr (MODE == kModeFrac) emit<MODE>(p, q, seg, c, 0);
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
         h = hash_bitset128<1>(cl, ch);
       }
       uint64_t f = h ^ p.kconst;
-      bool keep = (MODE == kModeFrac) ? div_test(f, p.low_mask, p.shift, p.dinv, p.dlim)
+      bool keep = (MODE == kModeFrac) ? div_test(f, p.rot, p.dinv, p.dlim)
                                       : (f <= thresh);
       if (valid && keep) {
         uint32_t slot = atomicAdd(&q_n, 1u);

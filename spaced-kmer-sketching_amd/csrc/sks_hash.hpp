@@ -86,14 +86,13 @@ SKS_HD uint64_t fmh_const(uint64_t mask_lo, uint64_t mask_hi, int w, int64_t non
          (uint64_t)(int64_t)(int32_t)nonce;
 }
 
-// Exact divisibility test for x % c == 0 without a 64-bit division:
-// c = 2^shift * d (d odd); x % c == 0  <=>  low `shift` bits of x are zero and
-// (x >> shift) * d^-1 (mod 2^64) <= floor((2^64 - 1) / d)   (Granlund-Montgomery).
+// Exact divisibility test for x % c == 0 without a 64-bit division
+// (Granlund-Montgomery; Hacker's Delight 10-17): with c = 2^s * d, d odd,
+//   x % c == 0  <=>  rotr64(x * d^-1 mod 2^64, s) <= floor((2^64 - 1) / c).
 struct DivTest {
-  uint64_t low_mask;
-  uint32_t shift;
+  uint32_t rot;
   uint64_t dinv;
-  uint64_t dlim;
+  uint64_t lim;
 };
 
 inline DivTest make_div_test(uint64_t c) {
@@ -103,10 +102,9 @@ inline DivTest make_div_test(uint64_t c) {
   uint64_t d = c >> s;
   uint64_t inv = d;  // Newton iteration: inverse of odd d modulo 2^64
   for (int i = 0; i < 6; ++i) inv *= 2 - d * inv;
-  t.shift = s;
-  t.low_mask = s >= 64 ? ~0ULL : ((1ULL << s) - 1);
+  t.rot = s;
   t.dinv = inv;
-  t.dlim = ~0ULL / d;
+  t.lim = ~0ull / c;
   return t;
 }
 
@@ -117,8 +115,23 @@ SKS_HD uint64_t mul_uniform(uint64_t x, uint64_t m) {
   return (uint64_t)lo * (uint32_t)m + ((uint64_t)cross << 32);
 }
 
-SKS_HD bool div_test(uint64_t x, uint64_t low_mask, uint32_t shift, uint64_t dinv, uint64_t dlim) {
-  return ((x & low_mask) == 0) & (mul_uniform(x >> shift, dinv) <= dlim);
+SKS_HD uint64_t rotr64(uint64_t x, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (s & 32) {  // wave-uniform
+    uint32_t t = lo;
+    lo = hi;
+    hi = t;
+  }
+  const uint32_t sh = s & 31;
+  return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, sh) << 32) | __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+  return s ? (x >> s) | (x << (64 - s)) : x;
+#endif
+}
+
+SKS_HD bool div_test(uint64_t x, uint32_t rot, uint64_t dinv, uint64_t lim) {
+  return rotr64(mul_uniform(x, dinv), rot) <= lim;
 }
 
 // splitmix64 output p of a stream seeded with `seed` (synthetic genomes).

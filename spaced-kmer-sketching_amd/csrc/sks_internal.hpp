@@ -24,8 +24,7 @@ struct ScanParams {
   uint64_t mask_lo, mask_hi;
   uint64_t kconst;              // H(mask) ^ w ^ nonce
   // FracMinHash divisibility test (sks_hash.hpp DivTest)
-  uint64_t low_mask;
-  uint32_t shift;
+  uint32_t rot;
   uint64_t dinv, dlim;
   // bottom-s pre-filter: keep fmh <= seg_thresh[seg]
   const uint64_t* seg_thresh;
