@@ -126,7 +126,8 @@ __global__ __launch_bounds__(kB) void k_all(const uint64_t* __restrict__ data,
 // leave with one atomicAdd per pair.
 constexpr int kTile = 64;
 constexpr int kSlots = 2 * kTile;
-constexpr int kMaxPart = 150;  // LDS: 150 * 128 * 8 = 153,600 B
+constexpr int kMaxPart = 150;   // LDS: 150 * 128 * 8 = 153,600 B (one workgroup per CU)
+constexpr int kGoodPart = 60;   // <= 60 keeps LDS <= 61.4 KB: two workgroups per CU
 constexpr int kDiagPerWave = kTile / kWavesPerBlock;  // 16
 
 struct TileArgs {
@@ -134,7 +135,7 @@ struct TileArgs {
   const uint64_t* starts;
   const uint32_t* sizes;
   const uint32_t* pos;  // [n][B + 1] bucket boundaries (element index within sketch)
-  uint32_t n, B, buckets_per_group, n_groups;
+  uint32_t n, B, P, buckets_per_group, n_groups;
   uint32_t row_begin, row_end;  // rows mode: rows [row_begin, row_end) x all n columns
   uint32_t n_col_blocks, n_row_blocks;
   int sym;                      // 1: upper-triangle tiles, write both (i, j) and (j, i)
@@ -187,7 +188,8 @@ __device__ __forceinline__ void sym_tile(uint64_t t, uint32_t nb, uint32_t& I, u
 }
 
 __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
-  __shared__ uint64_t lds[kMaxPart * kSlots];
+  // lds[pos * kSlots + slot], pos < a.P (dynamic: sized to the largest part)
+  extern __shared__ uint64_t lds[];
   __shared__ uint32_t s_len[kSlots];
   const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
   const uint32_t grp = blockIdx.x % a.n_groups;
@@ -223,39 +225,59 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
       len = spos[b + 1] - beg;
     }
     if (par == 0) s_len[slot] = len;
+    // 8 independent loads in flight per thread
     const uint64_t* src = a.data + sstart + beg;
-    for (uint32_t j = par; j < len; j += 2) lds[j * kSlots + slot] = src[j];
+    for (uint32_t j0 = par; j0 < len; j0 += 16) {
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t j = j0 + 2 * u;
+        v[u] = j < len ? src[j] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t j = j0 + 2 * u;
+        if (j < len) lds[j * kSlots + slot] = v[u];
+      }
+    }
     __syncthreads();
-    // 16 independent merges per lane, advanced together so that 32 LDS reads
-    // are in flight per step (one wave per SIMD at this LDS footprint).
+    // Lane = row `lane`; 16 columns (lane + 16*wave + q) mod 64.  The 16
+    // merges advance together, branch-free: reads use clamped indices, and a
+    // merge whose A or B side is exhausted can no longer count (its clamped
+    // element was already consumed), so lanes keep stepping until all finish.
     const uint32_t na = s_len[lane];
+    const uint32_t na1 = na ? na - 1 : 0;
     const uint64_t* A = lds + lane;
-    uint32_t ii[kDiagPerWave], jj[kDiagPerWave], nb[kDiagPerWave];
+    uint32_t ii[kDiagPerWave], jj[kDiagPerWave], nb1[kDiagPerWave];
+    const uint64_t* Bq[kDiagPerWave];
+    uint32_t live = 0;
 #pragma unroll
     for (int q = 0; q < kDiagPerWave; ++q) {
       const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
-      nb[q] = s_len[kTile + c];
-      ii[q] = 0;
-      jj[q] = 0;
+      const uint32_t nb = s_len[kTile + c];
+      nb1[q] = nb ? nb - 1 : 0;
+      ii[q] = na ? 0 : 1;  // an empty side starts exhausted
+      jj[q] = nb ? 0 : 1;
+      Bq[q] = lds + kTile + c;
+      live |= (na != 0) & (nb != 0);
     }
-    // branch-free steps: every lane issues all 32 reads each iteration
-    // (indices clamped), so the reads of the 16 merges overlap
-    const uint32_t na1 = na ? na - 1 : 0;
-    for (;;) {
-      uint32_t any = 0;
+    while (__any(live)) {
+#pragma unroll 1
+      for (int rep = 0; rep < 4; ++rep) {
 #pragma unroll
-      for (int q = 0; q < kDiagPerWave; ++q) {
-        const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
-        const uint32_t nb1 = nb[q] ? nb[q] - 1 : 0;
-        const uint64_t x = A[min(ii[q], na1) * kSlots];
-        const uint64_t y = lds[kTile + c + min(jj[q], nb1) * kSlots];
-        const uint32_t act = (ii[q] < na) & (jj[q] < nb[q]);
-        cnt[q] += act & (uint32_t)(x == y);
-        ii[q] += act & (uint32_t)(x <= y);
-        jj[q] += act & (uint32_t)(y <= x);
-        any |= act;
+        for (int q = 0; q < kDiagPerWave; ++q) {
+          const uint64_t x = A[min(ii[q], na1) * kSlots];
+          const uint64_t y = Bq[q][min(jj[q], nb1[q]) * kSlots];
+          const bool in = (ii[q] <= na1) & (jj[q] <= nb1[q]);
+          const bool lt = x < y, eq = x == y;
+          cnt[q] += (in & eq) ? 1u : 0u;
+          ii[q] += (lt | eq) ? 1u : 0u;
+          jj[q] += lt ? 0u : 1u;
+        }
       }
-      if (!__any(any)) break;
+      live = 0;
+#pragma unroll
+      for (int q = 0; q < kDiagPerWave; ++q) live |= (ii[q] <= na1) & (jj[q] <= nb1[q]) & (na != 0);
     }
     __syncthreads();
   }
@@ -329,7 +351,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   const uint32_t max_size = h_sizes[ref];
   if (max_size == 0) { *used_tiles = true; return hipSuccess; }
   uint32_t B = 1;
-  while ((uint64_t)B * 64 < max_size) B <<= 1;
+  while ((uint64_t)B * 32 < max_size) B <<= 1;  // mean part <= 32 elements
   std::vector<uint32_t> h_pos;
   uint32_t P = 0;
   for (;;) {
@@ -350,8 +372,11 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     for (uint32_t i = 0; i < n; ++i)
       for (uint32_t b = 0; b < B; ++b)
         P = std::max(P, h_pos[(uint64_t)i * (B + 1) + b + 1] - h_pos[(uint64_t)i * (B + 1) + b]);
-    if (P <= (uint32_t)kMaxPart) break;
-    if (B >= (1u << 16)) return hipSuccess;  // pathological skew: caller falls back
+    if (P <= (uint32_t)kGoodPart) break;
+    if (B >= (1u << 16) || (uint64_t)B * 8 > max_size) {
+      if (P <= (uint32_t)kMaxPart) break;
+      return hipSuccess;  // pathological skew: caller falls back to the global kernel
+    }
     B <<= 1;
   }
   TileArgs a{};
@@ -361,6 +386,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   a.pos = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(work.ptr) + B + 1);
   a.n = n;
   a.B = B;
+  a.P = P;
   a.sym = sym ? 1 : 0;
   a.n_col_blocks = (n + kTile - 1) / kTile;
   a.row_begin = row_begin;
@@ -378,7 +404,12 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   a.tile_begin = tile_begin;
   a.out = out;
   a.ld = n;
-  hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), 0, s, a);
+  const size_t lds_bytes = (size_t)std::max<uint32_t>(P, 1) * kSlots * sizeof(uint64_t);
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)(kMaxPart * kSlots * sizeof(uint64_t)));
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), lds_bytes, s, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   *used_tiles = true;
   return hipSuccess;
