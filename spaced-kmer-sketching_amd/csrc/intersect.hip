@@ -129,6 +129,7 @@ constexpr int kSlots = 2 * kTile;
 constexpr int kMaxPart = 150;   // LDS: 150 * 128 * 8 = 153,600 B (one workgroup per CU)
 constexpr int kGoodPart = 60;   // <= 60 keeps LDS <= 61.4 KB: two workgroups per CU
 constexpr int kDiagPerWave = kTile / kWavesPerBlock;  // 16
+constexpr int kRowBytes = kSlots * 8;                  // one LDS position across all slots
 
 struct TileArgs {
   const uint64_t* data;
@@ -189,8 +190,10 @@ __device__ __forceinline__ void sym_tile(uint64_t t, uint32_t nb, uint32_t& I, u
 
 __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
   // lds[pos * kSlots + slot], pos < a.P (dynamic: sized to the largest part)
+  // (the only LDS object, so its base is LDS address 0 and element offsets
+  // need no base add); part lengths follow the P x 128 element block
   extern __shared__ uint64_t lds[];
-  __shared__ uint32_t s_len[kSlots];
+  uint32_t* s_len = reinterpret_cast<uint32_t*>(lds + (size_t)a.P * kSlots);
   const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
   const uint32_t grp = blockIdx.x % a.n_groups;
   uint32_t I, J;
@@ -242,42 +245,61 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
     }
     __syncthreads();
     // Lane = row `lane`; 16 columns (lane + 16*wave + q) mod 64.  The 16
-    // merges advance together, branch-free: reads use clamped indices, and a
-    // merge whose A or B side is exhausted can no longer count (its clamped
-    // element was already consumed), so lanes keep stepping until all finish.
+    // merges advance together with no per-step branches: indices are LDS byte
+    // offsets clamped to the last element, every step reads both sides, and
+    // i += (x <= y), j += (y <= x), m += (x == y).  Once one side is exhausted
+    // its clamped element was already consumed, so it can match again only
+    // when BOTH sides sit on equal last elements; each such step advances both
+    // offsets, and those extra counts are subtracted after the bucket.
     const uint32_t na = s_len[lane];
-    const uint32_t na1 = na ? na - 1 : 0;
-    const uint64_t* A = lds + lane;
-    uint32_t ii[kDiagPerWave], jj[kDiagPerWave], nb1[kDiagPerWave];
-    const uint64_t* Bq[kDiagPerWave];
-    uint32_t live = 0;
+    // raw LDS byte addresses: dynamic LDS begins after the static allocation
+    const uint32_t lds0 = __builtin_amdgcn_groupstaticsize();
+    const uint32_t a_base = lds0 + lane * 8u;
+    const uint32_t a_last = a_base + (na ? na - 1 : 0) * kRowBytes;
+    uint32_t io[kDiagPerWave], jo[kDiagPerWave], b_last[kDiagPerWave];
 #pragma unroll
     for (int q = 0; q < kDiagPerWave; ++q) {
       const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
       const uint32_t nb = s_len[kTile + c];
-      nb1[q] = nb ? nb - 1 : 0;
-      ii[q] = na ? 0 : 1;  // an empty side starts exhausted
-      jj[q] = nb ? 0 : 1;
-      Bq[q] = lds + kTile + c;
-      live |= (na != 0) & (nb != 0);
+      const uint32_t b_base = lds0 + c * 8u;  // column slots start kTile * 8 bytes in
+      io[q] = a_base;
+      jo[q] = b_base;
+      b_last[q] = b_base + (nb ? nb - 1 : 0) * kRowBytes;
     }
-    while (__any(live)) {
+    typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+    // Matches are not counted per step: every step advances i, j or both, so
+    // over T steps  matches = (i advances + j advances) - T.
+    uint32_t steps = 0;
+    for (;;) {
+      uint32_t live = 0;
+#pragma unroll
+      for (int q = 0; q < kDiagPerWave; ++q) live |= (io[q] <= a_last) & (jo[q] <= b_last[q]);
+      if (!__any(live)) break;
 #pragma unroll 1
       for (int rep = 0; rep < 4; ++rep) {
+        uint64_t xs[kDiagPerWave], ys[kDiagPerWave];
 #pragma unroll
         for (int q = 0; q < kDiagPerWave; ++q) {
-          const uint64_t x = A[min(ii[q], na1) * kSlots];
-          const uint64_t y = Bq[q][min(jj[q], nb1[q]) * kSlots];
-          const bool in = (ii[q] <= na1) & (jj[q] <= nb1[q]);
-          const bool lt = x < y, eq = x == y;
-          cnt[q] += (in & eq) ? 1u : 0u;
-          ii[q] += (lt | eq) ? 1u : 0u;
-          jj[q] += lt ? 0u : 1u;
+          xs[q] = *reinterpret_cast<lds_u64*>((size_t)min(io[q], a_last));
+          ys[q] = *reinterpret_cast<lds_u64*>((size_t)(min(jo[q], b_last[q]) + kTile * 8));
+        }
+#pragma unroll
+        for (int q = 0; q < kDiagPerWave; ++q) {
+          io[q] += xs[q] > ys[q] ? 0u : (uint32_t)kRowBytes;
+          jo[q] += xs[q] < ys[q] ? 0u : (uint32_t)kRowBytes;
         }
       }
-      live = 0;
+      steps += 4;
+    }
 #pragma unroll
-      for (int q = 0; q < kDiagPerWave; ++q) live |= (ii[q] <= na1) & (jj[q] <= nb1[q]) & (na != 0);
+    for (int q = 0; q < kDiagPerWave; ++q) {
+      const uint32_t c = (lane + wave * kDiagPerWave + q) & (kTile - 1);
+      const uint32_t nb = s_len[kTile + c];
+      const int32_t ia = (int32_t)((io[q] - a_base) / kRowBytes);
+      const int32_t jb = (int32_t)((jo[q] - lds0 - c * 8u) / kRowBytes);
+      // steps taken with both sides past their ends (equal last elements)
+      const int32_t spurious = max(0, min(ia - (int32_t)na, jb - (int32_t)nb));
+      if (na && nb) cnt[q] += (uint32_t)(ia + jb - (int32_t)steps - spurious);
     }
     __syncthreads();
   }
@@ -404,10 +426,11 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   a.tile_begin = tile_begin;
   a.out = out;
   a.ld = n;
-  const size_t lds_bytes = (size_t)std::max<uint32_t>(P, 1) * kSlots * sizeof(uint64_t);
+  const size_t lds_bytes = (size_t)std::max<uint32_t>(P, 1) * kSlots * sizeof(uint64_t) +
+                           kSlots * sizeof(uint32_t);
   static const hipError_t attr = hipFuncSetAttribute(
       reinterpret_cast<const void*>(k_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)(kMaxPart * kSlots * sizeof(uint64_t)));
+      (int)(kMaxPart * kSlots * sizeof(uint64_t) + kSlots * sizeof(uint32_t)));
   if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), lds_bytes, s, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
