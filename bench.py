@@ -52,16 +52,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup(n_gpus):
+def dist_setup(n_gpus, backend):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob: SKS_BENCH_DEVICE=0 puts every rank on GPU 0 (use with gloo)
+    if os.environ.get("SKS_BENCH_DEVICE") is not None:
+        local = int(os.environ["SKS_BENCH_DEVICE"])
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
-        torch.cuda.set_device(0)
+        torch.cuda.set_device(local)
     return world, rank, local
 
 
@@ -71,22 +77,26 @@ def barrier(world):
         dist.barrier()
 
 
+def _reduce_scalar(x, op):
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
 def max_over_ranks(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _reduce_scalar(x, dist.ReduceOp.MAX)
 
 
 def sum_over_ranks(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce_scalar(x, dist.ReduceOp.SUM)
 
 
 # ---- config 3 ---------------------------------------------------------------------
@@ -154,10 +164,9 @@ def c4_genome_seeds(g):
 
 
 def run_pairs(ctx, world, rank, mask, steps, warmup):
-    import torch.distributed as dist
-    per = (C4_GENOMES + world - 1) // world
-    g0, g1 = rank * per, min(C4_GENOMES, (rank + 1) * per)
-    n_local = max(0, g1 - g0)
+    import sks_dist
+    per, g0, g1 = sks_dist.genome_shard(C4_GENOMES, world, rank)
+    n_local = g1 - g0
     seg = [0]
     for _ in range(n_local):
         seg.append(seg[-1] + C4_LEN + 1)
@@ -170,12 +179,13 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
     stride = C4_S
     local = torch.full((per, stride), -1, dtype=torch.int64, device="cuda")
     local_sz = torch.zeros(per, dtype=torch.int32, device="cuda")
-    full = torch.empty((per * world, stride), dtype=torch.int64, device="cuda")
-    full_sz = torch.empty(per * world, dtype=torch.int32, device="cuda")
     starts = torch.arange(per * world, dtype=torch.int64, device="cuda") * stride
     mat = torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32, device="cuda")
-    n_tiles = sksffi.intersect_sym_tiles(C4_GENOMES)
-    t_lo, t_hi = rank * n_tiles // world, (rank + 1) * n_tiles // world
+
+    def count_sym(src, src_sz, n, t0, t1, out):
+        ctx.intersect_sym(src.data_ptr(), starts.data_ptr(), src_sz.data_ptr(), 1, n, t0, t1,
+                          out.data_ptr())
+
     t_sketch = t_pairs = 0.0
     timed = 0
     for it in range(warmup + steps):
@@ -188,18 +198,8 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
             ss.export(local.data_ptr(), stride, local_sz.data_ptr())
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        if world > 1:
-            dist.all_gather_into_tensor(full, local)
-            dist.all_gather_into_tensor(full_sz, local_sz)
-            src, src_sz = full, full_sz
-        else:
-            src, src_sz = local, local_sz
-        # symmetric upper-triangle tiles [t_lo, t_hi) of the N x N matrix; the
-        # per-rank partial matrices are summed over RCCL
-        ctx.intersect_sym(src.data_ptr(), starts.data_ptr(), src_sz.data_ptr(), 1, C4_GENOMES,
-                          t_lo, t_hi, mat.data_ptr())
-        if world > 1:
-            dist.all_reduce(mat)
+        # all-gather sketches, symmetric tiles of this rank, all-reduce counts
+        sks_dist.all_vs_all(local, local_sz, C4_GENOMES, world, rank, count_sym, out=mat)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ts, tp = max_over_ranks(t1 - t0, world), max_over_ranks(t2 - t1, world)
@@ -211,17 +211,16 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
     # containment + ANI for every ordered pair (host, double, from exact counts;
     # kmer-sketching.cpp:195-200 with the first set of the pair as denominator)
     counts = mat.cpu().numpy()
-    sizes = src_sz.cpu().numpy()[:C4_GENOMES]
-    size_first = np.repeat(sizes.astype(np.int32), C4_GENOMES)
+    sizes = np.diag(counts).astype(np.int32)  # |S_i ∩ S_i| = |S_i|
+    size_first = np.repeat(sizes, C4_GENOMES)
     kmer_ones = bin(mask).count("1") // 2
     _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, kmer_ones)
     k_ms = ctx.last_intersect_ms()
     t_sketch /= max(timed, 1)
     t_pairs /= max(timed, 1)
-    # sanity on rank 0: diagonal = sizes, siblings of the same ancestor overlap
     if rank == 0:
-        assert all(counts[i, i] == sizes[i] for i in range(C4_GENOMES))
         assert (counts == counts.T).all() and counts[0, 1] > 0
+        assert (sizes[:n_local] == local_sz.cpu().numpy()[:n_local]).all()
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s", "scaling": "strong",
@@ -245,10 +244,11 @@ def main():
     ap.add_argument("--cpu-sample-mb", type=int, default=60)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pairs", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"))
     args = ap.parse_args()
 
-    world, rank, local = dist_setup(args.gpus)
+    world, rank, local = dist_setup(args.gpus, args.dist_backend)
     ctx = sksffi.Context(local)
     mask = sksffi.mask_generate(W, K, MASK_SEED)
 

@@ -1,0 +1,88 @@
+"""Multi-GPU orchestration for all-vs-all ANI (one process per GPU).
+
+The reference parallelises with cilk_for over files (kmer_set.cpp:124) and over
+pairs (kmer_set.cpp:179) inside one process.  Here:
+  * genomes are sharded across ranks (each rank sketches its own; no collective),
+  * the padded per-rank sketches are all-gathered (RCCL over xGMI for "nccl"),
+  * the upper-triangle 64x64 tiles of the N x N pair matrix are split evenly
+    across ranks (sks_intersect_sym writes each count to both halves), and
+  * the per-rank partial matrices are summed with one all-reduce.
+The functions take the count kernel as a callable so the same orchestration is
+exercised on CPU with gloo in tests/test_dist_cpu.py.
+"""
+import torch
+import torch.distributed as dist
+
+TILE = 64
+
+
+def genome_shard(n_genomes, world, rank):
+    per = (n_genomes + world - 1) // world
+    g0 = min(n_genomes, rank * per)
+    return per, g0, min(n_genomes, g0 + per)
+
+
+def sym_tiles(n):
+    nb = (n + TILE - 1) // TILE
+    return nb * (nb + 1) // 2
+
+
+def tile_shard(n_tiles, world, rank):
+    return rank * n_tiles // world, (rank + 1) * n_tiles // world
+
+
+def sym_tile_coords(t, n):
+    """(I, J) of upper-triangle tile t (row-major, I <= J) — intersect.hip sym_tile."""
+    nb = (n + TILE - 1) // TILE
+    i = 0
+    while t >= nb - i:
+        t -= nb - i
+        i += 1
+    return i, i + t
+
+
+def gather_sketches(local, local_sizes, world):
+    """local: [per, stride] int64 padded sketches; local_sizes: [per] int32."""
+    if world == 1:
+        return local, local_sizes
+    per, stride = local.shape
+    if dist.get_backend() == "nccl":
+        full = torch.empty((per * world, stride), dtype=local.dtype, device=local.device)
+        full_sz = torch.empty(per * world, dtype=local_sizes.dtype, device=local.device)
+        dist.all_gather_into_tensor(full, local)
+        dist.all_gather_into_tensor(full_sz, local_sizes)
+        return full, full_sz
+    # gloo (CPU tests, single-GPU rehearsal): stage through host memory
+    lc, lsc = local.cpu(), local_sizes.cpu()
+    parts = [torch.empty_like(lc) for _ in range(world)]
+    szs = [torch.empty_like(lsc) for _ in range(world)]
+    dist.all_gather(parts, lc)
+    dist.all_gather(szs, lsc)
+    return torch.cat(parts).to(local.device), torch.cat(szs).to(local.device)
+
+
+def sum_matrix(out):
+    if dist.get_backend() == "nccl" or out.device.type == "cpu":
+        dist.all_reduce(out)
+        return out
+    host = out.cpu()
+    dist.all_reduce(host)
+    out.copy_(host)
+    return out
+
+
+def all_vs_all(local, local_sizes, n_genomes, world, rank, count_sym, out=None):
+    """Returns the full n x n int32 intersection matrix on every rank.
+
+    count_sym(sketches, sizes, n, tile_begin, tile_end, out) must zero `out`
+    and write the counts of upper-triangle tiles [tile_begin, tile_end) to
+    both (i, j) and (j, i) — the contract of sks_intersect_sym.
+    """
+    src, src_sz = gather_sketches(local, local_sizes, world)
+    t0, t1 = tile_shard(sym_tiles(n_genomes), world, rank)
+    if out is None:
+        out = torch.empty((n_genomes, n_genomes), dtype=torch.int32, device=local.device)
+    count_sym(src, src_sz, n_genomes, t0, t1, out)
+    if world > 1:
+        sum_matrix(out)
+    return out

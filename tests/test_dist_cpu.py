@@ -1,0 +1,104 @@
+"""CPU (gloo, world_size 2 and 3): the multi-GPU all-vs-all orchestration of
+spaced-kmer-sketching_amd/sks_dist.py — genome sharding, the all-gather of
+padded sketches, the symmetric tile split and the all-reduce — assembles
+exactly the single-process matrix.  The count kernel is replaced by the
+oracle's merge count over the same tile contract (sks_intersect_sym)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import pyoracle as O
+import sks_dist
+import synth
+
+N_GENOMES = 70   # two tile blocks, ragged
+STRIDE = 400
+
+
+def _sketches():
+    m = O.mask(21, 21, 0)
+    out = []
+    for g in range(N_GENOMES):
+        seq = synth.bases(6000, seed=40 + g % 4, mut_seed=300 + g, mut_rate=0.002 * (g % 9))
+        sk, _ = O.sketch(O.cut_runs(seq.tobytes()), 21, m, "bottom", 300 - (g % 5) * 40)
+        out.append(sk[:, 0].astype(np.int64))
+    return out
+
+
+def _oracle_count_sym(src, src_sz, n, t0, t1, out):
+    out.zero_()
+    sk = [src[i, : int(src_sz[i])].numpy().astype(np.uint64) for i in range(n)]
+    for t in range(t0, t1):
+        I, J = sks_dist.sym_tile_coords(t, n)
+        for i in range(I * 64, min(n, I * 64 + 64)):
+            for j in range(J * 64, min(n, J * 64 + 64)):
+                c = O.intersect(np.stack([sk[i], 0 * sk[i]], 1), np.stack([sk[j], 0 * sk[j]], 1))
+                out[i, j] = c
+                out[j, i] = c
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sk = _sketches()
+    per, g0, g1 = sks_dist.genome_shard(N_GENOMES, world, rank)
+    local = torch.full((per, STRIDE), -1, dtype=torch.int64)
+    local_sz = torch.zeros(per, dtype=torch.int32)
+    for i, g in enumerate(range(g0, g1)):
+        local[i, : len(sk[g])] = torch.from_numpy(sk[g])
+        local_sz[i] = len(sk[g])
+    mat = sks_dist.all_vs_all(local, local_sz, N_GENOMES, world, rank, _oracle_count_sym)
+    q.put((rank, mat.numpy()))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_vs_all_gloo_matches_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sk = _sketches()
+    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(N_GENOMES)]
+                     for i in range(N_GENOMES)])
+    for r in range(world):
+        assert np.array_equal(results[r], want)
+
+
+def test_shard_arithmetic():
+    for n in (1, 63, 64, 65, 1000):
+        T = sks_dist.sym_tiles(n)
+        seen = []
+        for world in (1, 2, 3, 8):
+            cov = []
+            for r in range(world):
+                a, b = sks_dist.tile_shard(T, world, r)
+                cov += list(range(a, b))
+            assert cov == list(range(T))
+            covg = []
+            for r in range(world):
+                _, g0, g1 = sks_dist.genome_shard(n, world, r)
+                covg += list(range(g0, g1))
+            assert covg == list(range(n))
+        nb = (n + 63) // 64
+        for t in range(T):
+            seen.append(sks_dist.sym_tile_coords(t, n))
+        assert seen == [(i, j) for i in range(nb) for j in range(i, nb)]
