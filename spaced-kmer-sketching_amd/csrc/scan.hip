@@ -168,10 +168,9 @@ __device__ __forceinline__ void add_windows(const ScanParams& p, uint32_t seg, u
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(&p.seg_windows[seg], (unsigned long long)v);
 }
 
-// Hash + selection predicate + emit for one canonical k-mer (w <= 32).
-template <int MODE, int FLAVOUR>
-__device__ __forceinline__ void select_window(const ScanParams& p, Queue<MODE>& q, uint32_t seg,
-                                              uint64_t thresh, bool valid, uint64_t c) {
+// frac_min_hash of a canonical k-mer (w <= 32, so the high block is 0).
+template <int FLAVOUR>
+__device__ __forceinline__ uint64_t fmh_narrow(const ScanParams& p, uint64_t c) {
   uint64_t h;
   if constexpr (FLAVOUR == 0) {
     h = hash_mix(c + kGolden32);                // combine(0, lo)
@@ -180,20 +179,23 @@ __device__ __forceinline__ void select_window(const ScanParams& p, Queue<MODE>& 
   } else {
     h = hash_bitset128<1>(c, 0);
   }
-  uint64_t f = h ^ p.kconst;
-  bool keep;
-  if constexpr (MODE == kModeFrac) keep = div_test(f, p.rot, p.dinv, p.dlim);
-  else keep = f <= thresh;
-  if (valid && keep) {
-    if constexpr (MODE == kModeFrac) emit<MODE>(p, q, seg, c, 0);
-    else emit<MODE>(p, q, seg, f, c);
-  }
+  return h ^ p.kconst;
+}
+
+template <int MODE>
+__device__ __forceinline__ bool keep_fmh(const ScanParams& p, uint64_t f, uint64_t thresh) {
+  if constexpr (MODE == kModeFrac) return div_test(f, p.rot, p.dinv, p.dlim);
+  else return f <= thresh;
 }
 
 constexpr int kBeOff = 2;  // s_be[kBeOff + i] = word i; two zero words in front
 
+#ifndef SKS_SCAN_MIN_WAVES
+#define SKS_SCAN_MIN_WAVES 1
+#endif
+
 template <int MODE, int FLAVOUR>
-__global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
+__global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanParams p) {
   __shared__ uint32_t s_raw[kLoadVecs * 4];
   __shared__ uint32_t s_be[kWords + 2 + kBeOff];
   __shared__ uint32_t s_lc[kWords + 2];
@@ -296,25 +298,44 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanParams p) {
     const uint64_t inv64 = (uint64_t)s_inv[tid] | ((uint64_t)s_inv[tid + 1] << 16) |
                            ((uint64_t)s_inv[tid + 2] << 32) | ((uint64_t)s_inv[tid + 3] << 48);
     const bool lane_clean = (inv64 & region_bits) == 0;
+    // canonical masked k-mer of window j (runtime j allowed)
+    auto canon = [&](uint32_t j) -> uint64_t {
+      const uint32_t fh = j ? funnel(bs[0], bs[1], 32 - 2 * j) : bs[0];
+      const uint32_t fl = j ? funnel(bs[1], bs[2], 32 - 2 * j) : bs[1];
+      const uint64_t F = (((uint64_t)fh) << 32) | fl;
+      const uint32_t rl = j ? funnel(lc1, lc0, 2 * j) : lc0;
+      const uint32_t rh = j ? funnel(lc2, lc1, 2 * j) : lc1;
+      const uint64_t R = (((uint64_t)rh) << 32) | rl;
+      const uint64_t fm = F & p.mask_lo, rm = R & p.mask_lo;
+      return fm < rm ? fm : rm;
+    };
+    // Hot loop: no branches — one keep bit per window, so the compiler can
+    // interleave the 16 independent hash chains.  Survivors (~1/c) are
+    // re-derived and emitted afterwards.
+    uint32_t keepmask = 0;
     auto windows = [&](auto checked) {
 #pragma unroll
       for (int j = 0; j < kWPT; ++j) {
-        const uint32_t fh = j ? funnel(bs[0], bs[1], 32 - 2 * j) : bs[0];
-        const uint32_t fl = j ? funnel(bs[1], bs[2], 32 - 2 * j) : bs[1];
-        const uint64_t F = (((uint64_t)fh) << 32) | fl;
-        const uint32_t rl = j ? funnel(lc1, lc0, 2 * j) : lc0;
-        const uint32_t rh = j ? funnel(lc2, lc1, 2 * j) : lc1;
-        const uint64_t R = (((uint64_t)rh) << 32) | rl;
-        const uint64_t fm = F & p.mask_lo, rm = R & p.mask_lo;
-        const uint64_t c = fm < rm ? fm : rm;
-        bool valid = true;
-        if constexpr (decltype(checked)::value) valid = ((inv64 >> j) & wmask_bits) == 0;
-        win_count += valid ? 1u : 0u;
-        select_window<MODE, FLAVOUR>(p, q, g.seg, thresh, valid, c);
+        const uint64_t f = fmh_narrow<FLAVOUR>(p, canon(j));
+        bool k = keep_fmh<MODE>(p, f, thresh);
+        if constexpr (decltype(checked)::value) {
+          const bool valid = ((inv64 >> j) & wmask_bits) == 0;
+          win_count += valid ? 1u : 0u;
+          k = k && valid;
+        }
+        keepmask |= (k ? 1u : 0u) << j;
       }
+      if constexpr (!decltype(checked)::value) win_count += kWPT;
     };
     if (__all(lane_clean)) windows(std::false_type{});
     else windows(std::true_type{});
+    while (keepmask) {
+      const uint32_t j = __builtin_ctz(keepmask);
+      keepmask &= keepmask - 1;
+      const uint64_t c = canon(j);
+      if constexpr (MODE == kModeFrac) emit<MODE>(p, q, g.seg, c, 0);
+      else emit<MODE>(p, q, g.seg, fmh_narrow<FLAVOUR>(p, c), c);
+    }
 
     // 5) flush the queue once it is half full
     __syncthreads();

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libsks.so")
+LIB_PATH = os.environ.get("SKS_LIB") or os.path.join(PKG_DIR, "lib", "libsks.so")
 
 SKS_FRAC_MOD = 0
 SKS_BOTTOM_S = 1
