@@ -566,7 +566,8 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
     p.mask_lo = S.mask_lo;
     p.mask_hi = S.mask_hi;
     p.kconst = S.kconst;
-    p.rot = S.dt.rot;
+    p.low_mask = S.dt.low_mask;
+    p.high_mask = S.dt.rot > 32 ? (uint32_t)((1ull << (S.dt.rot - 32)) - 1) : 0u;
     p.dinv = S.dt.dinv;
     p.dlim = S.dt.lim;
     p.seg_thresh = arena.ptr(o_thr);

@@ -184,7 +184,7 @@ __device__ __forceinline__ uint64_t fmh_narrow(const ScanParams& p, uint64_t c) 
 
 template <int MODE>
 __device__ __forceinline__ bool keep_fmh(const ScanParams& p, uint64_t f, uint64_t thresh) {
-  if constexpr (MODE == kModeFrac) return div_test(f, p.rot, p.dinv, p.dlim);
+  if constexpr (MODE == kModeFrac) return div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim);
   else return f <= thresh;
 }
 
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
         h = hash_bitset128<1>(cl, ch);
       }
       uint64_t f = h ^ p.kconst;
-      bool keep = (MODE == kModeFrac) ? div_test(f, p.rot, p.dinv, p.dlim)
+      bool keep = (MODE == kModeFrac) ? div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim)
                                       : (f <= thresh);
       if (valid && keep) {
         uint32_t slot = atomicAdd(&q_n, 1u);

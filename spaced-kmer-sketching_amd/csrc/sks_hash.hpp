@@ -87,12 +87,14 @@ SKS_HD uint64_t fmh_const(uint64_t mask_lo, uint64_t mask_hi, int w, int64_t non
 }
 
 // Exact divisibility test for x % c == 0 without a 64-bit division
-// (Granlund-Montgomery; Hacker's Delight 10-17): with c = 2^s * d, d odd,
-//   x % c == 0  <=>  rotr64(x * d^-1 mod 2^64, s) <= floor((2^64 - 1) / c).
+// (Granlund-Montgomery): with c = 2^s * d, d odd,
+//   x % c == 0  <=>  (x mod 2^s == 0)  and  (x * d^-1 mod 2^64 <= floor((2^64 - 1) / d))
+// (d | x  <=>  x * d^-1 = x / d <= (2^64 - 1) / d;  2^s | x is independent).
 struct DivTest {
-  uint32_t rot;
+  uint32_t low_mask;  // low s bits (s <= 63; bits above 31 checked via dlim below)
   uint64_t dinv;
   uint64_t lim;
+  uint32_t rot;       // s
 };
 
 inline DivTest make_div_test(uint64_t c) {
@@ -104,7 +106,8 @@ inline DivTest make_div_test(uint64_t c) {
   for (int i = 0; i < 6; ++i) inv *= 2 - d * inv;
   t.rot = s;
   t.dinv = inv;
-  t.lim = ~0ull / c;
+  t.lim = ~0ull / d;
+  t.low_mask = s >= 32 ? 0xFFFFFFFFu : ((1u << s) - 1);
   return t;
 }
 
@@ -115,23 +118,12 @@ SKS_HD uint64_t mul_uniform(uint64_t x, uint64_t m) {
   return (uint64_t)lo * (uint32_t)m + ((uint64_t)cross << 32);
 }
 
-SKS_HD uint64_t rotr64(uint64_t x, uint32_t s) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  if (s & 32) {  // wave-uniform
-    uint32_t t = lo;
-    lo = hi;
-    hi = t;
-  }
-  const uint32_t sh = s & 31;
-  return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, sh) << 32) | __builtin_amdgcn_alignbit(hi, lo, sh);
-#else
-  return s ? (x >> s) | (x << (64 - s)) : x;
-#endif
-}
-
-SKS_HD bool div_test(uint64_t x, uint32_t rot, uint64_t dinv, uint64_t lim) {
-  return rotr64(mul_uniform(x, dinv), rot) <= lim;
+// s >= 32 needs the high word too: rare (c a multiple of 2^32) and handled by
+// the caller passing high_mask.
+SKS_HD bool div_test(uint64_t x, uint32_t low_mask, uint32_t high_mask, uint64_t dinv,
+                     uint64_t lim) {
+  return ((((uint32_t)x & low_mask) | ((uint32_t)(x >> 32) & high_mask)) == 0) &
+         (mul_uniform(x, dinv) <= lim);
 }
 
 // splitmix64 output p of a stream seeded with `seed` (synthetic genomes).

@@ -24,8 +24,8 @@ struct ScanParams {
   uint64_t mask_lo, mask_hi;
   uint64_t kconst;              // H(mask) ^ w ^ nonce
   // FracMinHash divisibility test (sks_hash.hpp DivTest)
-  uint32_t rot;
-  uint64_t dinv, dlim;
+  uint32_t low_mask, high_mask;  // x mod 2^s == 0 test (words)
+  uint64_t dinv, dlim;           // odd part: x * d^-1 <= (2^64 - 1) / d
   // bottom-s pre-filter: keep fmh <= seg_thresh[seg]
   const uint64_t* seg_thresh;
   // output records: frac narrow key=C; frac wide key=lo val=hi;
