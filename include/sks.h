@@ -173,6 +173,21 @@ int sks_intersect_sym(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_st
                       const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t tile_begin,
                       uint64_t tile_end, int32_t* d_out);
 
+/* ---- FASTA ingress (device) — fasta_processing.cpp:79-133 on the GPU ------------------
+ * d_raw: the n_raw bytes of one FASTA file in device memory (the host only reads
+ * the file).  Writes to d_stream exactly the bytes sks_fasta_stream() holds for
+ * the same file (records in order, each followed by one '\n'), and, when
+ * d_rec_end is non-NULL, the stream position of record i's '\n' to d_rec_end[i].
+ * *stream_bytes / *n_records always receive the sizes; d_stream == NULL is a
+ * size query.  Capacity too small -> SKS_E_LENGTH, nothing written.  Output is
+ * at most n_raw + 1 bytes.  Returns after the sizes are known; the copy kernels
+ * are queued on the context stream. */
+int sks_fasta_parse_device(sks_ctx* ctx, const uint8_t* d_raw, uint64_t n_raw, uint8_t* d_stream,
+                           uint64_t stream_cap, uint64_t* d_rec_end, uint64_t rec_cap,
+                           uint64_t* stream_bytes, uint64_t* n_records);
+/* Device time (ms) of the last sks_fasta_parse_device call (waits for it). */
+int sks_ctx_last_ingress_ms(sks_ctx* ctx, float* ms);
+
 /* ---- diagnostics / tuning ------------------------------------------------------------- */
 /* Device time (ms) between the first and last launch of the last
  * sks_intersect_* call on this context (waits for it to finish). */

@@ -21,6 +21,7 @@
 #include "sks.h"
 #include "sks_api_internal.hpp"
 #include "sks_hash.hpp"
+#include "facade_internal.hpp"
 
 namespace sks {
 namespace {
@@ -30,6 +31,8 @@ int g_device = 0;
 sks_ctx* g_ctx = nullptr;
 bool g_exit_on_io = true;
 int g_flavour = SKS_HASH_BOOST_MIX;
+
+}  // namespace
 
 [[noreturn]] void raise(int rc) {
   throw std::runtime_error(std::string("libsks: ") + sks_last_error() + " (status " +
@@ -50,19 +53,14 @@ sks_ctx* ctx() {
   return g_ctx;
 }
 
-// Device buffer owned by the facade for the duration of one call.
-struct DevMem {
-  void* p = nullptr;
-  explicit DevMem(size_t bytes) {
-    check_hip(hipSetDevice(g_device), "hipSetDevice");
-    check_hip(hipMalloc(&p, bytes ? bytes : 1), "hipMalloc");
-  }
-  ~DevMem() {
-    if (p) (void)hipFree(p);
-  }
-  template <class T>
-  T* as() const { return reinterpret_cast<T*>(p); }
-};
+DevMem::DevMem(size_t bytes) {
+  check_hip(hipSetDevice(g_device), "hipSetDevice");
+  check_hip(hipMalloc(&p, bytes ? bytes : 1), "hipMalloc");
+}
+
+DevMem::~DevMem() {
+  if (p) (void)hipFree(p);
+}
 
 sks_fasta* open_fasta(const char* path) {
   sks_fasta* f = nullptr;
@@ -82,27 +80,20 @@ struct FastaHandle {
   ~FastaHandle() { sks_fasta_close(f); }
 };
 
-// Upload byte streams as consecutive segments and sketch them in one build.
-std::vector<kmer_set> sketch_streams(const std::vector<std::vector<uint8_t>>& streams,
-                                     const kmer_bitset& mask, int w, const sketch_policy& pol) {
-  std::vector<uint64_t> off(1, 0);
-  for (auto& s : streams) off.push_back(off.back() + s.size());
-  std::vector<uint8_t> all;
-  all.reserve(off.back());
-  for (auto& s : streams) all.insert(all.end(), s.begin(), s.end());
-  DevMem d(all.size());
-  check_hip(hipMemcpy(d.p, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy H2D");
+// Sketch a device buffer of consecutive segments (off[i], off[i+1]) in one build.
+std::vector<kmer_set> sketch_device(const uint8_t* d_seq, const std::vector<uint64_t>& off,
+                                    const kmer_bitset& mask, int w, const sketch_policy& pol) {
+  const size_t n_seg = off.size() - 1;
   sks_policy p{pol.kind, pol.flavour, pol.param, pol.nonce};
   uint64_t m[2] = {mask.lo(), mask.hi()};
   sks_sketch_set* set = nullptr;
-  check(sks_sketch_build(ctx(), d.as<uint8_t>(), all.size(), off.data(), (uint32_t)streams.size(), w,
-                         m, &p, &set));
+  check(sks_sketch_build(ctx(), d_seq, off.back(), off.data(), (uint32_t)n_seg, w, m, &p, &set));
   const int ew = sks_sketch_set_elem_words(set);
-  std::vector<uint32_t> sizes(streams.size());
+  std::vector<uint32_t> sizes(n_seg);
   sks_sketch_set_sizes(set, sizes.data());
-  std::vector<kmer_set> out(streams.size());
+  std::vector<kmer_set> out(n_seg);
   std::vector<uint64_t> buf;
-  for (size_t i = 0; i < streams.size(); ++i) {
+  for (size_t i = 0; i < n_seg; ++i) {
     buf.resize((size_t)sizes[i] * ew);
     int rc = sks_sketch_set_copy(set, (uint32_t)i, buf.data());
     if (rc != SKS_OK) {
@@ -121,10 +112,86 @@ std::vector<kmer_set> sketch_streams(const std::vector<std::vector<uint8_t>>& st
   return out;
 }
 
-std::vector<uint8_t> stream_of(sks_fasta* f) {
-  const uint8_t* p = sks_fasta_stream(f);
-  return std::vector<uint8_t>(p, p + sks_fasta_stream_bytes(f));
+// Upload record streams (already parsed) as consecutive segments and sketch them.
+std::vector<kmer_set> sketch_streams(const std::vector<std::vector<uint8_t>>& streams,
+                                     const kmer_bitset& mask, int w, const sketch_policy& pol) {
+  std::vector<uint64_t> off(1, 0);
+  for (auto& s : streams) off.push_back(off.back() + s.size());
+  std::vector<uint8_t> all;
+  all.reserve(off.back());
+  for (auto& s : streams) all.insert(all.end(), s.begin(), s.end());
+  DevMem d(all.size());
+  check_hip(hipMemcpy(d.p, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy H2D");
+  return sketch_device(d.as<uint8_t>(), off, mask, w, pol);
 }
+
+// Raw FASTA files: the host only reads bytes; strings_from_fasta runs on the
+// device (sks_fasta_parse_device) straight into the segment layout.
+std::vector<kmer_set> sketch_raw_files(const std::vector<std::vector<uint8_t>>& raws,
+                                       const kmer_bitset& mask, int w, const sketch_policy& pol) {
+  std::vector<uint64_t> in_off(1, 0);
+  for (auto& r : raws) in_off.push_back(in_off.back() + r.size());
+  DevMem d_raw(in_off.back());
+  for (size_t i = 0; i < raws.size(); ++i)
+    if (!raws[i].empty())
+      check_hip(hipMemcpy(d_raw.as<uint8_t>() + in_off[i], raws[i].data(), raws[i].size(),
+                          hipMemcpyHostToDevice), "hipMemcpy H2D");
+  DevMem d_stream(in_off.back() + raws.size());  // a stream is at most raw + 1 bytes
+  std::vector<uint64_t> off(1, 0);
+  for (size_t i = 0; i < raws.size(); ++i) {
+    uint64_t nb = 0, nr = 0;
+    check(sks_fasta_parse_device(ctx(), d_raw.as<uint8_t>() + in_off[i], raws[i].size(),
+                                 d_stream.as<uint8_t>() + off.back(), raws[i].size() + 1, nullptr, 0,
+                                 &nb, &nr));
+    off.push_back(off.back() + nb);
+  }
+  return sketch_device(d_stream.as<uint8_t>(), off, mask, w, pol);
+}
+
+// Whole-file read; false if the file cannot be opened or read.
+bool read_raw(const char* path, std::vector<uint8_t>& buf) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  buf.clear();
+  uint8_t tmp[1 << 16];
+  size_t got;
+  while ((got = fread(tmp, 1, sizeof tmp, f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+  bool ok = !ferror(f);
+  fclose(f);
+  return ok;
+}
+
+// The reference's missing-file behaviour (fasta_processing.cpp:86-90).
+void report_unreadable(const char* path) {
+  FastaHandle f(path);  // exits (or throws) like the reference
+}
+
+
+std::vector<std::vector<uint8_t>> read_files(int num_files, char* filenames[]) {
+  const int n = num_files > 0 ? num_files : 0;
+  std::vector<std::vector<uint8_t>> raws(n);
+  // open serially first so that the reference's exit(1) / error order holds
+  for (int i = 0; i < n; ++i) {
+    FILE* fp = fopen(filenames[i], "rb");
+    if (!fp) report_unreadable(filenames[i]);
+    else fclose(fp);
+  }
+  std::vector<int> bad(n, 0);
+  const int workers = std::max(1, std::min<int>(n, (int)std::thread::hardware_concurrency()));
+  std::vector<std::thread> ts;
+  std::atomic<int> next{0};
+  for (int t = 0; t < workers; ++t)
+    ts.emplace_back([&]() {
+      for (int i; (i = next.fetch_add(1)) < n;)
+        if (!read_raw(filenames[i], raws[i])) bad[i] = 1;
+    });
+  for (auto& t : ts) t.join();
+  for (int i = 0; i < n; ++i)
+    if (bad[i]) report_unreadable(filenames[i]);
+  return raws;
+}
+
+namespace {
 
 // Pair counts on the GPU for sets sharing a mask; pairs with different masks
 // have no common k-mer (identity includes the mask, kmer.hpp:82-85).
@@ -292,12 +359,10 @@ kmer_set kmer_set_from_fasta_file(const char fasta_filename[], const kmer_bitset
 std::vector<kmer_set> kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
                                                  const kmer_bitset& mask, const int window_length,
                                                  const sketch_policy& policy) {
-  std::vector<std::vector<uint8_t>> streams(num_files > 0 ? num_files : 0);
-  for (int i = 0; i < num_files; ++i) {
-    sks::FastaHandle f(fasta_filenames[i]);
-    streams[i] = sks::stream_of(f.f);
-  }
-  return sks::sketch_streams(streams, mask, window_length, policy);
+  std::vector<std::vector<uint8_t>> raws(num_files > 0 ? num_files : 0);
+  for (int i = 0; i < num_files; ++i)
+    if (!sks::read_raw(fasta_filenames[i], raws[i])) sks::report_unreadable(fasta_filenames[i]);
+  return sks::sketch_raw_files(raws, mask, window_length, policy);
 }
 
 std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files,
@@ -305,37 +370,8 @@ std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files,
                                                           const kmer_bitset& mask,
                                                           const int window_length,
                                                           const sketch_policy& policy) {
-  const int n = num_files > 0 ? num_files : 0;
-  std::vector<std::vector<uint8_t>> streams(n);
-  std::vector<int> bad(n, 0);
-  // open serially first so that the reference's exit(1) / error order holds
-  for (int i = 0; i < n; ++i) {
-    FILE* fp = fopen(fasta_filenames[i], "rb");
-    if (!fp) {
-      sks::FastaHandle f(fasta_filenames[i]);  // reports like the reference
-    } else {
-      fclose(fp);
-    }
-  }
-  const int workers = std::max(1, std::min<int>(n, (int)std::thread::hardware_concurrency()));
-  std::vector<std::thread> ts;
-  std::atomic<int> next{0};
-  for (int t = 0; t < workers; ++t)
-    ts.emplace_back([&]() {
-      for (int i; (i = next.fetch_add(1)) < n;) {
-        sks_fasta* f = nullptr;
-        if (sks_fasta_open(fasta_filenames[i], &f) != SKS_OK) {
-          bad[i] = 1;
-          continue;
-        }
-        streams[i] = sks::stream_of(f);
-        sks_fasta_close(f);
-      }
-    });
-  for (auto& t : ts) t.join();
-  for (int i = 0; i < n; ++i)
-    if (bad[i]) sks::FastaHandle f(fasta_filenames[i]);
-  return sks::sketch_streams(streams, mask, window_length, policy);
+  return sks::sketch_raw_files(sks::read_files(num_files, fasta_filenames), mask, window_length,
+                               policy);
 }
 
 kmer_set nucleotide_string_list_to_kmer_set(const std::vector<std::vector<uint8_t>>& nucleotide_strings,

@@ -43,6 +43,8 @@ struct sks_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_s0 = nullptr, ev_s1 = nullptr;
+  hipEvent_t ev_i0 = nullptr, ev_i1 = nullptr;  // device FASTA ingress
+  sks::Scratch ingress;             // per-line arrays of the device FASTA parser
   sks::Scratch tmp;                 // rocPRIM temporary storage
   sks::Scratch rec[3];              // scan records (key, val, hi)
   sks::Scratch buf[10];             // dense working columns
@@ -227,7 +229,8 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
   c->device = device;
   c->stream = reinterpret_cast<hipStream_t>(stream);
   if (hipEventCreate(&c->ev_begin) != hipSuccess || hipEventCreate(&c->ev_end) != hipSuccess ||
-      hipEventCreate(&c->ev_s0) != hipSuccess || hipEventCreate(&c->ev_s1) != hipSuccess) {
+      hipEventCreate(&c->ev_s0) != hipSuccess || hipEventCreate(&c->ev_s1) != hipSuccess ||
+      hipEventCreate(&c->ev_i0) != hipSuccess || hipEventCreate(&c->ev_i1) != hipSuccess) {
     delete c;
     return sks::fail(SKS_E_HIP, "sks_ctx_create: hipEventCreate failed");
   }
@@ -246,10 +249,13 @@ int sks_ctx_destroy(sks_ctx* c) {
   c->pos.release();
   c->meta.release();
   c->iwork.release();
+  c->ingress.release();
   (void)hipEventDestroy(c->ev_begin);
   (void)hipEventDestroy(c->ev_end);
   (void)hipEventDestroy(c->ev_s0);
   (void)hipEventDestroy(c->ev_s1);
+  if (c->ev_i0) (void)hipEventDestroy(c->ev_i0);
+  if (c->ev_i1) (void)hipEventDestroy(c->ev_i1);
   delete c;
   return SKS_OK;
 }
@@ -836,6 +842,34 @@ int sks_ctx_last_intersect_ms(sks_ctx* c, float* ms) {
   DeviceGuard g(c->device);
   SKS_HIP(hipEventSynchronize(c->ev_end));
   SKS_HIP(hipEventElapsedTime(ms, c->ev_begin, c->ev_end));
+  return SKS_OK;
+}
+
+// ---- device FASTA ingress (ingress.hip) -----------------------------------------------------
+
+int sks_fasta_parse_device(sks_ctx* c, const uint8_t* d_raw, uint64_t n_raw, uint8_t* d_stream,
+                           uint64_t stream_cap, uint64_t* d_rec_end, uint64_t rec_cap,
+                           uint64_t* stream_bytes, uint64_t* n_records) {
+  if (!c || !stream_bytes || !n_records || (n_raw && !d_raw))
+    return sks::fail(SKS_E_ARG, "sks_fasta_parse_device: null argument");
+  DeviceGuard g(c->device);
+  bool too_small = false;
+  SKS_HIP(hipEventRecord(c->ev_i0, c->stream));
+  SKS_HIP(sks::fasta_parse_device(d_raw, n_raw, d_stream, stream_cap, d_rec_end, rec_cap, c->ingress,
+                                  c->tmp, c->stream, stream_bytes, n_records, &too_small));
+  SKS_HIP(hipEventRecord(c->ev_i1, c->stream));
+  if (too_small)
+    return sks::fail(SKS_E_LENGTH, "sks_fasta_parse_device: stream_cap or rec_cap too small for " +
+                                       std::to_string(*stream_bytes) + " bytes / " +
+                                       std::to_string(*n_records) + " records");
+  return SKS_OK;
+}
+
+int sks_ctx_last_ingress_ms(sks_ctx* c, float* ms) {
+  if (!c || !ms) return sks::fail(SKS_E_ARG, "null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventSynchronize(c->ev_i1));
+  SKS_HIP(hipEventElapsedTime(ms, c->ev_i0, c->ev_i1));
   return SKS_OK;
 }
 

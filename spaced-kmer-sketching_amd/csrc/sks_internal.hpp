@@ -103,6 +103,16 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
                                   Scratch& work, hipStream_t s, bool* used_tiles);
 uint64_t intersect_sym_tiles(uint32_t n);
 
+// ---- device FASTA ingress (ingress.hip) -------------------------------------------------
+// strings_from_fasta on the device: writes the host parser's record stream
+// (fasta.cpp) to `out` and each record's '\n' position to rec_end (optional).
+// out == nullptr: size query only.  *too_small: a capacity was short (nothing
+// written).  Synchronises `s` twice (sizes are read back).
+hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint64_t out_cap,
+                              uint64_t* rec_end, uint64_t rec_cap, Scratch& work, Scratch& tmp,
+                              hipStream_t s, uint64_t* out_bytes, uint64_t* n_records,
+                              bool* too_small);
+
 // ---- misc kernels (post.hip) -------------------------------------------------------------
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,
                         uint64_t mut_thresh, uint64_t pos_offset, hipStream_t s);

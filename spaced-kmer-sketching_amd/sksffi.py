@@ -47,6 +47,8 @@ EXPORTED = [
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
     "sks_synth_bases", "sks_intersect_sym", "sks_intersect_sym_tiles",
+    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_fasta_parse_device",
+    "sks_ctx_last_ingress_ms",
 ]
 
 _lib = None
@@ -89,6 +91,9 @@ def lib():
     L.sks_ctx_last_timings.argtypes = [vp, C.POINTER(Timings)]
     L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.sks_fasta_parse_device.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64,
+                                         u64p, u64p]
     L.sks_sketch_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
                                    C.POINTER(Policy), C.POINTER(vp)]
     L.sks_sketch_set_free.argtypes = [vp]
@@ -244,6 +249,21 @@ class Context:
         ms = C.c_float()
         check(lib().sks_ctx_last_intersect_ms(self.h, C.byref(ms)))
         return float(ms.value)
+
+    def last_ingress_ms(self):
+        ms = C.c_float()
+        check(lib().sks_ctx_last_ingress_ms(self.h, C.byref(ms)))
+        return float(ms.value)
+
+    def fasta_parse_device(self, d_raw_ptr, n_raw, d_stream_ptr=None, stream_cap=0,
+                           d_rec_end_ptr=None, rec_cap=0):
+        """Device strings_from_fasta; returns (stream_bytes, n_records)."""
+        nb, nr = C.c_uint64(), C.c_uint64()
+        check(lib().sks_fasta_parse_device(self.h, C.c_void_p(d_raw_ptr), n_raw,
+                                           C.c_void_p(d_stream_ptr), stream_cap,
+                                           C.c_void_p(d_rec_end_ptr), rec_cap, C.byref(nb),
+                                           C.byref(nr)))
+        return int(nb.value), int(nr.value)
 
     def close(self):
         if self.h:

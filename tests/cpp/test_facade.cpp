@@ -15,6 +15,7 @@
 #include "fasta_processing.hpp"
 #include "generators.hpp"
 #include "kmer.hpp"
+#include "sweep.hpp"
 
 static void hexset(const kmer_set& ks) {
   std::printf("[");
@@ -110,11 +111,31 @@ static int errors() {
   return ok == 6 ? 0 : 2;
 }
 
+// test_facade csv <out> <append 0|1> <w> <mask_lo hex> <mask_hi hex> <n> names1[n] names2[n] values[n]
+static int csv(int argc, char** argv) {
+  const std::string out = argv[2];
+  const bool append = std::atoi(argv[3]) != 0;
+  const int w = std::atoi(argv[4]);
+  const kmer_bitset mask(std::strtoull(argv[5], nullptr, 16), std::strtoull(argv[6], nullptr, 16));
+  const int n = std::atoi(argv[7]);
+  if (argc != 8 + 3 * n) return 64;
+  std::vector<std::string> a, b;
+  std::vector<double> v;
+  for (int i = 0; i < n; ++i) {
+    a.emplace_back(argv[8 + i]);
+    b.emplace_back(argv[8 + n + i]);
+    v.push_back(std::strtod(argv[8 + 2 * n + i], nullptr));
+  }
+  write_to_csv(a, b, v, w, mask, out, append);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 64;
   std::string mode = argv[1];
   if (mode == "sketch" && argc >= 8) return sketch(argc, argv);
   if (mode == "errors") return errors();
+  if (mode == "csv" && argc >= 8) return csv(argc, argv);
   if (mode == "missing" && argc == 3) {
     char* f[1] = {argv[2]};
     kmer_bitset mask = generate_random_spaced_seed_mask(21, 21, 0);
