@@ -18,16 +18,14 @@
 //   next H / E / Ssp event after it is not Ssp (EOF counts as a push)
 //                             -> the same scan over the reversed event list
 //
-// Passes (n = file bytes, L = lines):
-//   1. count '\n'                                   (reduce, reads n bytes)
-//   2. positions of '\n'                            (select, reads n bytes)
-//   3. mark lines that contain ' '                  (reads n bytes)
-//   4. per-line class / setter / event              (per line)
-//   5. two last-non-zero scans                      (per line, u8)
-//   6. per-line output length + push flag, scans    (per line)
-//   7. copy kept bytes, 4 KiB input spans per group (reads n, writes <= n)
-//   8. '\n' separators and record ends              (per line)
-// Everything except pass 7 touches O(L) words; pass 7 is a streaming copy.
+// Passes (n = file bytes, L = lines; byte passes work on aligned 4 KiB spans):
+//   1. newlines per span + exclusive scan           (reads n bytes)
+//   2. newline positions, lines holding a ' '       (reads n bytes, writes 8 B/line)
+//   3. per-line class / setter / event              (per line)
+//   4. two last-non-zero scans                      (per line, u8)
+//   5. per-line output length + push flag, scans    (per line)
+//   6. copy kept bytes                              (reads n, writes <= n)
+//   7. '\n' separators and record ends              (per line)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,31 +39,77 @@ namespace sks {
 namespace {
 
 constexpr int kB = 256;
-constexpr int kSpan = 4096;               // input bytes per copy work-group
+constexpr int kSpan = kB * 16;            // input bytes per work-group (16 per thread)
 constexpr int kSpanLines = kSpan + 1;     // lines a span can touch
 
 // line class bits
 constexpr uint8_t kH = 1, kE = 2, kSsp = 4, kNamed = 8;
 
-struct IsNewline {
-  __device__ bool operator()(uint8_t b) const { return b == '\n'; }
-};
-struct NewlineCount {
-  __device__ uint64_t operator()(uint8_t b) const { return b == '\n'; }
-};
 struct LastNonZero {
   __host__ __device__ uint8_t operator()(uint8_t a, uint8_t b) const { return b ? b : a; }
 };
 
-// number of newline positions < i  (= index of the line holding byte i)
-__device__ __forceinline__ uint64_t line_of(const uint64_t* nl, uint64_t n_nl, uint64_t i) {
-  uint64_t lo = 0, hi = n_nl;
-  while (lo < hi) {
-    uint64_t mid = (lo + hi) >> 1;
-    if (nl[mid] < i) lo = mid + 1;
-    else hi = mid;
+// High bit of every zero byte of t, exactly (no borrow between bytes).
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t t) {
+  const uint32_t y = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(y | t | 0x7F7F7F7Fu);
+}
+
+// 16-bit mask of the bytes of q equal to the byte replicated in c4.
+__device__ __forceinline__ uint32_t byte_eq_mask(const uint4& q, uint32_t c4) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t z = zero_bytes(w[i] ^ c4);
+    m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * i);
   }
-  return lo;
+  return m;
+}
+
+// Spans are aligned in absolute address terms: virtual offset v = i + align,
+// span s = [s * kSpan, (s + 1) * kSpan), thread t holds v0 = s * kSpan + 16 t,
+// so every load is one aligned uint4 (an aligned 16-byte block holding a
+// valid byte never crosses a page).  Bytes outside [0, n) are masked off.
+struct SpanThread {
+  uint64_t v0;
+  uint32_t valid;  // 16-bit mask of bytes inside [0, n)
+  uint4 q;
+};
+
+__device__ __forceinline__ SpanThread span_load(const uint8_t* raw, uint64_t n, uint32_t align) {
+  SpanThread t;
+  t.v0 = (uint64_t)blockIdx.x * kSpan + threadIdx.x * 16u;
+  const uint64_t end = n + align;
+  uint32_t valid = 0xFFFFu;
+  if (t.v0 < align) valid = align - t.v0 >= 16 ? 0u : (valid << (align - t.v0)) & 0xFFFFu;
+  if (t.v0 + 16 > end) valid &= t.v0 >= end ? 0u : (0xFFFFu >> (t.v0 + 16 - end));
+  t.valid = valid;
+  t.q = valid ? *reinterpret_cast<const uint4*>(raw - align + t.v0) : make_uint4(0, 0, 0, 0);
+  return t;
+}
+
+// Exclusive prefix sum over the work-group (s_tmp: one word per wave).
+__device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t* s_tmp,
+                                                        uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_tmp[wave] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kB / 64; ++w) {
+    const uint32_t t = s_tmp[w];
+    base += w < wave ? t : 0u;
+    tot += t;
+  }
+  *total = tot;
+  return base + x - v;
 }
 
 __device__ __forceinline__ uint64_t line_start(const uint64_t* nl, uint64_t l) {
@@ -76,18 +120,43 @@ __device__ __forceinline__ uint64_t line_end(const uint64_t* nl, uint64_t n_nl, 
   return l < n_nl ? nl[l] : n;
 }
 
-// Pass 3: a ' ' byte marks its line (benign same-value races).
-__global__ __launch_bounds__(kB) void k_spaces(const uint8_t* raw, uint64_t n, const uint64_t* nl,
-                                               uint64_t n_nl, uint8_t* has_space) {
-  const uint64_t stride = (uint64_t)gridDim.x * kB * 16;
-  for (uint64_t b = ((uint64_t)blockIdx.x * kB + threadIdx.x) * 16; b < n; b += stride) {
-    const uint64_t e = b + 16 < n ? b + 16 : n;
-    for (uint64_t i = b; i < e; ++i)
-      if (raw[i] == ' ') has_space[line_of(nl, n_nl, i)] = 1;
+// Pass 1: newlines per span.
+__global__ __launch_bounds__(kB) void k_span_count(const uint8_t* raw, uint64_t n, uint32_t align,
+                                                   uint32_t* span_nl) {
+  __shared__ uint32_t s_tmp[kB / 64];
+  const SpanThread t = span_load(raw, n, align);
+  uint32_t total;
+  (void)block_exclusive_sum(__popc(byte_eq_mask(t.q, 0x0A0A0A0Au) & t.valid), s_tmp, &total);
+  if (threadIdx.x == 0) span_nl[blockIdx.x] = total;
+}
+
+// Pass 2: newline positions (in order) and the lines holding a ' '.  The line
+// of a byte is the number of newlines before it, known from the span offset
+// and the block scan.
+__global__ __launch_bounds__(kB) void k_span_lines(const uint8_t* raw, uint64_t n, uint32_t align,
+                                                   const uint64_t* span_off, uint64_t* nl,
+                                                   uint8_t* has_space) {
+  __shared__ uint32_t s_tmp[kB / 64];
+  const SpanThread t = span_load(raw, n, align);
+  uint32_t nlm = byte_eq_mask(t.q, 0x0A0A0A0Au) & t.valid;
+  uint32_t spm = byte_eq_mask(t.q, 0x20202020u) & t.valid;
+  uint32_t total;
+  const uint64_t base = span_off[blockIdx.x] + block_exclusive_sum(__popc(nlm), s_tmp, &total);
+  const uint64_t i0 = t.v0 - align;  // input index of byte 0 (when valid)
+  while (spm) {
+    const int b = __ffs(spm) - 1;
+    spm &= spm - 1;
+    has_space[base + __popc(nlm & ((1u << b) - 1))] = 1;
+  }
+  uint64_t r = base;
+  while (nlm) {
+    const int b = __ffs(nlm) - 1;
+    nlm &= nlm - 1;
+    nl[r++] = i0 + b;
   }
 }
 
-// Pass 4
+// Pass 3
 __global__ __launch_bounds__(kB) void k_classify(const uint8_t* raw, uint64_t n, const uint64_t* nl,
                                                  uint64_t n_nl, uint64_t L, const uint8_t* has_space,
                                                  uint8_t* cls, uint8_t* setter, uint8_t* ev_rev) {
@@ -104,7 +173,7 @@ __global__ __launch_bounds__(kB) void k_classify(const uint8_t* raw, uint64_t n,
   ev_rev[L - 1 - l] = (c & (kH | kE)) ? 1 : ((c & kSsp) ? 2 : 0);
 }
 
-// Pass 6: out_len = bytes line l contributes to the stream.
+// Pass 5: out_len = bytes line l contributes to the stream.
 __global__ __launch_bounds__(kB) void k_out_len(const uint64_t* nl, uint64_t n_nl, uint64_t n,
                                                 uint64_t L, const uint8_t* cls,
                                                 const uint8_t* have_after, const uint8_t* nxt_rev,
@@ -142,57 +211,49 @@ __global__ void k_summary(uint64_t L, const uint64_t* out_off, const uint64_t* o
   s->n_records = (uint64_t)push_rank[L - 1] + push_cnt[L - 1] + eof;
 }
 
-// Pass 7: work-group per 4 KiB span of the input (spans are aligned in
-// absolute address terms so every 16-byte load is aligned); the lines the span
-// touches are staged in LDS, each thread moves 16 input bytes.
+// Pass 6: copy kept bytes.  The span is staged in LDS, each byte gets its
+// span-local line from the block scan of newline counts, and bytes are then
+// written lane-contiguously (64 consecutive output bytes per wave store).
 __global__ __launch_bounds__(kB) void k_copy(const uint8_t* raw, uint64_t n, uint32_t align,
-                                             const uint64_t* nl, uint64_t n_nl,
-                                             const uint8_t* kept, const uint64_t* out_off,
-                                             uint8_t* out) {
-  __shared__ int32_t s_start[kSpanLines];
+                                             const uint64_t* span_off, const uint64_t* nl,
+                                             uint64_t L, const uint8_t* kept,
+                                             const uint64_t* out_off, uint8_t* out) {
+  __shared__ uint4 s_bytes[kB];
+  __shared__ uint16_t s_lid[kSpan];
   __shared__ uint64_t s_dst[kSpanLines];
-  __shared__ uint64_t s_l[2];
-  const uint64_t vbeg = (uint64_t)blockIdx.x * kSpan;
-  const uint64_t ibeg = vbeg > align ? vbeg - align : 0;
-  const uint64_t iend = std::min<uint64_t>(n, vbeg + kSpan - align);
-  if (threadIdx.x < 2) s_l[threadIdx.x] = line_of(nl, n_nl, threadIdx.x ? iend - 1 : ibeg);
-  __syncthreads();
-  const uint64_t l0 = s_l[0];
-  const int m = (int)(s_l[1] - l0 + 1);
-  for (int j = threadIdx.x; j < m; j += kB) {
-    const uint64_t l = l0 + j;
-    const uint64_t st = line_start(nl, l);
-    s_start[j] = st <= ibeg ? 0 : (int32_t)(st - ibeg);
-    s_dst[j] = kept[l] ? out_off[l] - st : ~0ull;
-  }
-  __syncthreads();
-  const uint64_t v0 = vbeg + (uint64_t)threadIdx.x * 16;  // virtual offset of this thread's block
-  if (v0 + 16 <= align || v0 >= n + align) return;
-  const uint4 q = *reinterpret_cast<const uint4*>(raw - align + v0);
-  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-  const uint64_t i0 = v0 > align ? v0 - align : 0;  // first valid byte
-  const int32_t r0 = (int32_t)(i0 - ibeg);
-  int lo = 0, hi = m - 1;  // last j with s_start[j] <= r0
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (s_start[mid] <= r0) lo = mid;
-    else hi = mid - 1;
-  }
-  int j = lo;
+  __shared__ uint32_t s_tmp[kB / 64];
+  const SpanThread t = span_load(raw, n, align);
+  s_bytes[threadIdx.x] = t.q;
+  const uint32_t nlm = byte_eq_mask(t.q, 0x0A0A0A0Au) & t.valid;
+  uint32_t total;
+  uint32_t line = block_exclusive_sum(__popc(nlm), s_tmp, &total);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const uint64_t v = v0 + k;
+    s_lid[threadIdx.x * 16 + k] = (uint16_t)line;
+    line += (nlm >> k) & 1u;
+  }
+  const uint64_t l0 = span_off[blockIdx.x];  // line of the span's first byte
+  for (uint32_t j = threadIdx.x; j <= total; j += kB) {
+    const uint64_t l = l0 + j;
+    uint64_t d = ~0ull;
+    if (l < L && kept[l]) d = out_off[l] - line_start(nl, l);
+    s_dst[j] = d;
+  }
+  __syncthreads();
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_bytes);
+  const uint64_t vbeg = (uint64_t)blockIdx.x * kSpan;
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t b = k * kB + threadIdx.x;
+    const uint64_t v = vbeg + b;
     if (v < align || v >= n + align) continue;
-    const uint64_t i = v - align;
-    const int32_t r = (int32_t)(i - ibeg);
-    while (j + 1 < m && s_start[j + 1] <= r) ++j;
-    const uint8_t b = (uint8_t)(w[k >> 2] >> ((k & 3) * 8));
-    const uint64_t d = s_dst[j];
-    if (b != '\n' && d != ~0ull) out[d + i] = b;
+    const uint8_t ch = sb[b];
+    const uint64_t d = s_dst[s_lid[b]];
+    if (ch != '\n' && d != ~0ull) out[d + (v - align)] = ch;
   }
 }
 
-// Pass 8: separators and record ends.
+// Pass 7: separators and record ends.
 __global__ __launch_bounds__(kB) void k_push(uint64_t L, const uint8_t* cls, const uint8_t* have_after,
                                              const uint64_t* out_off, const uint32_t* push_rank,
                                              const Summary* sum, uint8_t* out, uint64_t* rec_end) {
@@ -223,30 +284,42 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   *out_bytes = *n_records = 0;
   if (n == 0) return hipSuccess;
   hipError_t e;
-#define SKS_CK(x)                     \
-  do {                                \
+#define SKS_CK(x)                          \
+  do {                                     \
     if ((e = (x)) != hipSuccess) return e; \
   } while (0)
 
-  // pass 1: count newlines (the count sizes every per-line array)
-  auto nl_count_it = rocprim::make_transform_iterator(raw, NewlineCount{});
-  SKS_CK(work.reserve(256));
-  uint64_t* d_cnt = reinterpret_cast<uint64_t*>(work.ptr);
+  const uint32_t align = (uint32_t)(reinterpret_cast<uintptr_t>(raw) & 15);
+  const uint64_t spans = (n + align + kSpan - 1) / kSpan;
+  if (spans >= (1ull << 31)) return hipErrorInvalidValue;
+
+  // pass 1: newlines per span and their exclusive scan (sizes every per-line array)
+  const size_t o_snl = 0;
+  const size_t o_soff = o_snl + align_up((spans + 1) * 4);
+  const size_t o_sum = o_soff + align_up((spans + 1) * 8);
+  const size_t o_lines = o_sum + align_up(sizeof(Summary));
+  SKS_CK(work.reserve(o_lines));
+  uint32_t* span_nl = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(work.ptr) + o_snl);
+  uint64_t* span_off = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(work.ptr) + o_soff);
+  SKS_CK(hipMemsetAsync(span_nl + spans, 0, 4, s));  // the scan's extra element: total
+  hipLaunchKernelGGL(k_span_count, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, span_nl);
   size_t need = 0;
-  SKS_CK(rocprim::reduce(nullptr, need, nl_count_it, d_cnt, uint64_t(0), n, rocprim::plus<uint64_t>(), s));
+  SKS_CK(rocprim::exclusive_scan(nullptr, need, span_nl, span_off, uint64_t(0), spans + 1,
+                                 rocprim::plus<uint64_t>(), s));
   SKS_CK(tmp.reserve(need));
-  SKS_CK(rocprim::reduce(tmp.ptr, need, nl_count_it, d_cnt, uint64_t(0), n, rocprim::plus<uint64_t>(), s));
+  SKS_CK(rocprim::exclusive_scan(tmp.ptr, need, span_nl, span_off, uint64_t(0), spans + 1,
+                                 rocprim::plus<uint64_t>(), s));
   uint64_t n_nl = 0;
   uint8_t last = 0;
-  SKS_CK(hipMemcpyAsync(&n_nl, d_cnt, sizeof n_nl, hipMemcpyDeviceToHost, s));
+  SKS_CK(hipMemcpyAsync(&n_nl, span_off + spans, sizeof n_nl, hipMemcpyDeviceToHost, s));
   SKS_CK(hipMemcpyAsync(&last, raw + n - 1, 1, hipMemcpyDeviceToHost, s));
   SKS_CK(hipStreamSynchronize(s));
   const uint64_t L = n_nl + (last != '\n');  // a trailing partial line is a line
+  if (L >= (1ull << 32)) return hipErrorInvalidValue;  // push ranks are u32
 
-  // per-line arrays, one allocation
-  size_t o = 0;
-  const size_t o_cnt = o;  o += align_up(sizeof(uint64_t));
-  const size_t o_sum = o;  o += align_up(sizeof(Summary));
+  // per-line arrays after the span arrays, one allocation (grown in place:
+  // Scratch::reserve reallocates, so take pointers afterwards)
+  size_t o = o_lines;
   const size_t o_nl = o;   o += align_up(n_nl * 8);
   const size_t o_sp = o;   o += align_up(L);
   const size_t o_cls = o;  o += align_up(L);
@@ -259,9 +332,17 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   const size_t o_off = o;  o += align_up(L * 8);
   const size_t o_pc = o;   o += align_up(L * 4);
   const size_t o_pr = o;   o += align_up(L * 4);
-  SKS_CK(work.reserve(o));
+  if (o > work.bytes) {
+    // keep the span offsets across the reallocation
+    Scratch grown;
+    SKS_CK(grown.reserve(o));
+    SKS_CK(hipMemcpyAsync(grown.ptr, work.ptr, o_lines, hipMemcpyDeviceToDevice, s));
+    SKS_CK(hipStreamSynchronize(s));
+    work.release();
+    work = grown;
+  }
   char* base = reinterpret_cast<char*>(work.ptr);
-  d_cnt = reinterpret_cast<uint64_t*>(base + o_cnt);
+  span_off = reinterpret_cast<uint64_t*>(base + o_soff);
   Summary* d_sum = reinterpret_cast<Summary*>(base + o_sum);
   uint64_t* nl = reinterpret_cast<uint64_t*>(base + o_nl);
   uint8_t* has_space = reinterpret_cast<uint8_t*>(base + o_sp);
@@ -276,29 +357,19 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   uint32_t* push_cnt = reinterpret_cast<uint32_t*>(base + o_pc);
   uint32_t* push_rank = reinterpret_cast<uint32_t*>(base + o_pr);
 
-  // pass 2: newline positions
-  if (n_nl) {
-    rocprim::counting_iterator<uint64_t> idx(0);
-    need = 0;
-    SKS_CK(rocprim::select(nullptr, need, idx, raw, nl, d_cnt, n, IsNewline{}, s));
-    SKS_CK(tmp.reserve(need));
-    SKS_CK(rocprim::select(tmp.ptr, need, idx, raw, nl, d_cnt, n, IsNewline{}, s));
-  }
-  // pass 3, 4
+  // pass 2, 3
   SKS_CK(hipMemsetAsync(has_space, 0, L, s));
-  {
-    const uint64_t blocks = std::min<uint64_t>((n + kB * 16 - 1) / (kB * 16), 1u << 20);
-    hipLaunchKernelGGL(k_spaces, dim3((unsigned)blocks), dim3(kB), 0, s, raw, n, nl, n_nl, has_space);
-  }
+  hipLaunchKernelGGL(k_span_lines, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, span_off,
+                     nl, has_space);
   hipLaunchKernelGGL(k_classify, dim3(grid_for(L)), dim3(kB), 0, s, raw, n, nl, n_nl, L, has_space,
                      cls, setter, ev_rev);
-  // pass 5
+  // pass 4
   need = 0;
   SKS_CK(rocprim::inclusive_scan(nullptr, need, setter, have_after, L, LastNonZero{}, s));
   SKS_CK(tmp.reserve(need));
   SKS_CK(rocprim::inclusive_scan(tmp.ptr, need, setter, have_after, L, LastNonZero{}, s));
   SKS_CK(rocprim::inclusive_scan(tmp.ptr, need, ev_rev, nxt_rev, L, LastNonZero{}, s));
-  // pass 6
+  // pass 5
   hipLaunchKernelGGL(k_out_len, dim3(grid_for(L)), dim3(kB), 0, s, nl, n_nl, n, L, cls, have_after,
                      nxt_rev, out_len, push_cnt, kept);
   need = 0;
@@ -324,11 +395,9 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
     *too_small = true;
     return hipSuccess;
   }
-  // pass 7, 8
-  const uint32_t align = (uint32_t)(reinterpret_cast<uintptr_t>(raw) & 15);
-  const uint64_t spans = (n + align + kSpan - 1) / kSpan;
-  hipLaunchKernelGGL(k_copy, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, nl, n_nl, kept,
-                     out_off, out);
+  // pass 6, 7
+  hipLaunchKernelGGL(k_copy, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, span_off, nl, L,
+                     kept, out_off, out);
   hipLaunchKernelGGL(k_push, dim3(grid_for(L)), dim3(kB), 0, s, L, cls, have_after, out_off,
                      push_rank, d_sum, out, rec_end);
   return hipGetLastError();
