@@ -24,8 +24,8 @@
 //   3. per-line class / setter / event              (per line)
 //   4. two last-non-zero scans                      (per line, u8)
 //   5. per-line output length + push flag, scans    (per line)
-//   6. copy kept bytes                              (reads n, writes <= n)
-//   7. '\n' separators and record ends              (per line)
+//   6. stream bytes per span, assembled in LDS      (reads n, writes <= n)
+//   7. record ends, EOF separator                   (per line)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -130,34 +130,48 @@ __global__ __launch_bounds__(kB) void k_span_count(const uint8_t* raw, uint64_t 
   if (threadIdx.x == 0) span_nl[blockIdx.x] = total;
 }
 
-// Pass 2: newline positions (in order) and the lines holding a ' '.  The line
-// of a byte is the number of newlines before it, known from the span offset
-// and the block scan.
+// Pass 2: newline positions (in order), the lines holding a ' ', and the
+// first byte of every line (fb[l]; '\n' for an empty line, 0 past EOF) so
+// that pass 3 reads per-line bytes sequentially.  The line of a byte is the
+// number of newlines before it: the span offset plus the block scan.
 __global__ __launch_bounds__(kB) void k_span_lines(const uint8_t* raw, uint64_t n, uint32_t align,
                                                    const uint64_t* span_off, uint64_t* nl,
-                                                   uint8_t* has_space) {
+                                                   uint8_t* has_space, uint8_t* fb) {
   __shared__ uint32_t s_tmp[kB / 64];
+  __shared__ uint4 s_bytes[kB + 1];
   const SpanThread t = span_load(raw, n, align);
+  s_bytes[threadIdx.x] = t.q;
+  if (threadIdx.x == 0) {
+    // the 16 bytes after the span (for the first byte of a line starting there)
+    const uint64_t v = (uint64_t)(blockIdx.x + 1) * kSpan;
+    s_bytes[kB] = v < n + align ? *reinterpret_cast<const uint4*>(raw - align + v)
+                                : make_uint4(0, 0, 0, 0);
+  }
   uint32_t nlm = byte_eq_mask(t.q, 0x0A0A0A0Au) & t.valid;
   uint32_t spm = byte_eq_mask(t.q, 0x20202020u) & t.valid;
   uint32_t total;
   const uint64_t base = span_off[blockIdx.x] + block_exclusive_sum(__popc(nlm), s_tmp, &total);
   const uint64_t i0 = t.v0 - align;  // input index of byte 0 (when valid)
+  if (blockIdx.x == 0 && threadIdx.x == 0) fb[0] = raw[0];
   while (spm) {
     const int b = __ffs(spm) - 1;
     spm &= spm - 1;
     has_space[base + __popc(nlm & ((1u << b) - 1))] = 1;
   }
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_bytes);
   uint64_t r = base;
   while (nlm) {
     const int b = __ffs(nlm) - 1;
     nlm &= nlm - 1;
-    nl[r++] = i0 + b;
+    const uint64_t p = i0 + b;
+    nl[r] = p;
+    fb[r + 1] = p + 1 < n ? sb[threadIdx.x * 16 + b + 1] : 0;
+    ++r;
   }
 }
 
 // Pass 3
-__global__ __launch_bounds__(kB) void k_classify(const uint8_t* raw, uint64_t n, const uint64_t* nl,
+__global__ __launch_bounds__(kB) void k_classify(const uint8_t* fb, uint64_t n, const uint64_t* nl,
                                                  uint64_t n_nl, uint64_t L, const uint8_t* has_space,
                                                  uint8_t* cls, uint8_t* setter, uint8_t* ev_rev) {
   const uint64_t l = (uint64_t)blockIdx.x * kB + threadIdx.x;
@@ -166,7 +180,7 @@ __global__ __launch_bounds__(kB) void k_classify(const uint8_t* raw, uint64_t n,
   const uint64_t len = en - st;
   uint8_t c;
   if (len == 0) c = kE;
-  else if (raw[st] == '>') c = kH | (len > 1 ? kNamed : 0);
+  else if (fb[l] == '>') c = kH | (len > 1 ? kNamed : 0);
   else c = has_space[l] ? kSsp : 0;
   cls[l] = c;
   setter[l] = (c & kH) ? ((c & kNamed) ? 2 : 1) : ((c & kSsp) ? 1 : 0);
@@ -189,7 +203,7 @@ __global__ __launch_bounds__(kB) void k_out_len(const uint64_t* nl, uint64_t n_n
   const uint64_t len = line_end(nl, n_nl, n, l) - line_start(nl, l);
   out_len[l] = keep ? len : (uint64_t)push;
   push_cnt[l] = push;
-  kept[l] = keep;
+  kept[l] = keep ? 1 : (push ? 2 : 0);
 }
 
 struct Summary {
@@ -211,62 +225,116 @@ __global__ void k_summary(uint64_t L, const uint64_t* out_off, const uint64_t* o
   s->n_records = (uint64_t)push_rank[L - 1] + push_cnt[L - 1] + eof;
 }
 
-// Pass 6: copy kept bytes.  The span is staged in LDS, each byte gets its
-// span-local line from the block scan of newline counts, and bytes are then
-// written lane-contiguously (64 consecutive output bytes per wave store).
-__global__ __launch_bounds__(kB) void k_copy(const uint8_t* raw, uint64_t n, uint32_t align,
-                                             const uint64_t* span_off, const uint64_t* nl,
-                                             uint64_t L, const uint8_t* kept,
-                                             const uint64_t* out_off, uint8_t* out) {
-  __shared__ uint4 s_bytes[kB];
-  __shared__ uint16_t s_lid[kSpan];
-  __shared__ uint64_t s_dst[kSpanLines];
-  __shared__ uint32_t s_tmp[kB / 64];
-  const SpanThread t = span_load(raw, n, align);
-  s_bytes[threadIdx.x] = t.q;
-  const uint32_t nlm = byte_eq_mask(t.q, 0x0A0A0A0Au) & t.valid;
-  uint32_t total;
-  uint32_t line = block_exclusive_sum(__popc(nlm), s_tmp, &total);
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    s_lid[threadIdx.x * 16 + k] = (uint16_t)line;
-    line += (nlm >> k) & 1u;
-  }
-  const uint64_t l0 = span_off[blockIdx.x];  // line of the span's first byte
-  for (uint32_t j = threadIdx.x; j <= total; j += kB) {
-    const uint64_t l = l0 + j;
-    uint64_t d = ~0ull;
-    if (l < L && kept[l]) d = out_off[l] - line_start(nl, l);
-    s_dst[j] = d;
-  }
-  __syncthreads();
-  const uint8_t* sb = reinterpret_cast<const uint8_t*>(s_bytes);
-  const uint64_t vbeg = (uint64_t)blockIdx.x * kSpan;
-#pragma unroll 4
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t b = k * kB + threadIdx.x;
-    const uint64_t v = vbeg + b;
-    if (v < align || v >= n + align) continue;
-    const uint8_t ch = sb[b];
-    const uint64_t d = s_dst[s_lid[b]];
-    if (ch != '\n' && d != ~0ull) out[d + (v - align)] = ch;
-  }
-}
-
-// Pass 7: separators and record ends.
-__global__ __launch_bounds__(kB) void k_push(uint64_t L, const uint8_t* cls, const uint8_t* have_after,
-                                             const uint64_t* out_off, const uint32_t* push_rank,
-                                             const Summary* sum, uint8_t* out, uint64_t* rec_end) {
+// Pass 6a (per line, after the scans): dst[l] maps line l's input bytes to
+// stream positions (kept line: stream = dst + i) or holds the separator's
+// stream position (push line).  Also record ends and the EOF separator.
+__global__ __launch_bounds__(kB) void k_line_dst(uint64_t L, const uint64_t* nl, const uint8_t* kept,
+                                                 const uint64_t* out_off, const uint32_t* push_rank,
+                                                 const Summary* sum, uint64_t* dst, uint8_t* out,
+                                                 uint64_t* rec_end) {
   const uint64_t l = (uint64_t)blockIdx.x * kB + threadIdx.x;
   if (l >= L) return;
-  const bool before = l ? have_after[l - 1] == 2 : false;
-  if ((cls[l] & (kH | kE)) && before) {
-    out[out_off[l]] = '\n';
-    if (rec_end) rec_end[push_rank[l]] = out_off[l];
-  }
+  const uint8_t ty = kept[l];
+  dst[l] = ty == 1 ? out_off[l] - line_start(nl, l) : out_off[l];
+  if (rec_end && ty == 2) rec_end[push_rank[l]] = out_off[l];
   if (l == L - 1 && sum->eof_push) {
     out[sum->total - 1] = '\n';
     if (rec_end) rec_end[sum->n_records - 1] = sum->total - 1;
+  }
+}
+
+// Pass 6b (per span): span_out[s] = stream bytes produced by the input before
+// span s (a push line's separator counts at its first byte);
+// span_out[spans] = the stream without the EOF separator.
+__global__ __launch_bounds__(kB) void k_span_out(uint64_t spans, uint64_t n, uint32_t align,
+                                                 const uint64_t* span_off, const uint64_t* nl,
+                                                 const uint8_t* kept, const uint64_t* out_off,
+                                                 const uint64_t* out_len, const Summary* sum,
+                                                 uint64_t* span_out) {
+  const uint64_t sp = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (sp > spans) return;
+  if (sp == spans) {
+    span_out[sp] = sum->total - sum->eof_push;
+    return;
+  }
+  const uint64_t v = sp * kSpan;
+  const uint64_t i = v > align ? v - align : 0;
+  const uint64_t l = span_off[sp];  // line of byte i
+  const uint64_t st = line_start(nl, l);
+  span_out[sp] = out_off[l] + (kept[l] == 1 ? i - st : (st < i ? out_len[l] : 0));
+}
+
+// Pass 6c: the stream bytes of one 4 KiB input span, [span_out[s],
+// span_out[s + 1]), are assembled in LDS — kept bytes by position, separators
+// whose stream position falls in the range — and written with aligned 16-byte
+// stores (byte stores only at the two ends).  All per-line inputs are
+// precomputed so a work-group waits on one round of loads.
+__global__ __launch_bounds__(kB) void k_copy(const uint8_t* raw, uint64_t n, uint32_t align,
+                                             const uint64_t* span_off, const uint64_t* span_out,
+                                             uint64_t L, const uint8_t* kept, const uint64_t* dst,
+                                             uint8_t* out) {
+  __shared__ int32_t s_rel[kSpanLines];
+  __shared__ uint32_t s_out[kSpan / 4 + 8];
+  __shared__ uint32_t s_tmp[kB / 64];
+  const SpanThread t = span_load(raw, n, align);
+  const uint64_t l0 = span_off[blockIdx.x];  // line of the span's first byte
+  const uint64_t o0 = span_out[blockIdx.x], o1 = span_out[blockIdx.x + 1];
+  const uint64_t vbeg = (uint64_t)blockIdx.x * kSpan;
+  const uint64_t ibeg = vbeg > align ? vbeg - align : 0;
+  const uint32_t nlm = byte_eq_mask(t.q, 0x0A0A0A0Au) & t.valid;
+  uint32_t total;
+  uint32_t j = block_exclusive_sum(__popc(nlm), s_tmp, &total);
+  uint8_t* so = reinterpret_cast<uint8_t*>(s_out);
+  for (uint32_t q = threadIdx.x; q <= total; q += kB) {
+    const uint64_t l = l0 + q;
+    int32_t rel = INT32_MIN;
+    if (l < L) {
+      const uint8_t ty = kept[l];
+      const uint64_t d = dst[l];
+      if (ty == 1) rel = (int32_t)(int64_t)(d + ibeg - o0);
+      else if (ty == 2 && d >= o0 && d < o1) so[d - o0] = '\n';
+    }
+    s_rel[q] = rel;
+  }
+  __syncthreads();
+  if (t.valid) {
+    const uint32_t w[4] = {t.q.x, t.q.y, t.q.z, t.q.w};
+    const int32_t r0 = (int32_t)(int64_t)(t.v0 - align - ibeg);  // byte 0 relative to ibeg
+    int32_t rel = s_rel[j];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (!((t.valid >> k) & 1u)) continue;
+      const uint8_t ch = (uint8_t)(w[k >> 2] >> ((k & 3) * 8));
+      if (ch == '\n') rel = s_rel[++j];
+      else if (rel != INT32_MIN) so[rel + r0 + k] = ch;
+    }
+  }
+  __syncthreads();
+  if (o1 <= o0) return;
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(out + o0);
+  const uintptr_t a1 = reinterpret_cast<uintptr_t>(out + o1);
+  const uintptr_t blk0 = a0 & ~uintptr_t(15);
+  const uint32_t n_blk = (uint32_t)((((a1 + 15) & ~uintptr_t(15)) - blk0) / 16);
+  for (uint32_t bi = threadIdx.x; bi < n_blk; bi += kB) {
+    const uintptr_t ba = blk0 + (uintptr_t)bi * 16;
+    const int64_t r = (int64_t)ba - (int64_t)a0;  // LDS offset of the block's first byte
+    if (ba >= a0 && ba + 16 <= a1) {
+      const uint32_t wi = (uint32_t)r >> 2, sh = (uint32_t)r & 3;
+      uint32_t x[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) x[k] = s_out[wi + k];
+      uint4 v;
+      v.x = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
+      v.y = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
+      v.z = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
+      v.w = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
+      *reinterpret_cast<uint4*>(ba) = v;
+    } else {
+      for (int k = 0; k < 16; ++k) {
+        const uintptr_t a = ba + k;
+        if (a >= a0 && a < a1) *reinterpret_cast<uint8_t*>(a) = so[r + k];
+      }
+    }
   }
 }
 
@@ -322,6 +390,7 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   size_t o = o_lines;
   const size_t o_nl = o;   o += align_up(n_nl * 8);
   const size_t o_sp = o;   o += align_up(L);
+  const size_t o_fb = o;   o += align_up(L + 1);
   const size_t o_cls = o;  o += align_up(L);
   const size_t o_set = o;  o += align_up(L);
   const size_t o_hav = o;  o += align_up(L);
@@ -332,6 +401,8 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   const size_t o_off = o;  o += align_up(L * 8);
   const size_t o_pc = o;   o += align_up(L * 4);
   const size_t o_pr = o;   o += align_up(L * 4);
+  const size_t o_dst = o;  o += align_up(L * 8);
+  const size_t o_spo = o;  o += align_up((spans + 1) * 8);
   if (o > work.bytes) {
     // keep the span offsets across the reallocation
     Scratch grown;
@@ -346,6 +417,7 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   Summary* d_sum = reinterpret_cast<Summary*>(base + o_sum);
   uint64_t* nl = reinterpret_cast<uint64_t*>(base + o_nl);
   uint8_t* has_space = reinterpret_cast<uint8_t*>(base + o_sp);
+  uint8_t* fb = reinterpret_cast<uint8_t*>(base + o_fb);
   uint8_t* cls = reinterpret_cast<uint8_t*>(base + o_cls);
   uint8_t* setter = reinterpret_cast<uint8_t*>(base + o_set);
   uint8_t* have_after = reinterpret_cast<uint8_t*>(base + o_hav);
@@ -356,12 +428,14 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   uint64_t* out_off = reinterpret_cast<uint64_t*>(base + o_off);
   uint32_t* push_cnt = reinterpret_cast<uint32_t*>(base + o_pc);
   uint32_t* push_rank = reinterpret_cast<uint32_t*>(base + o_pr);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(base + o_dst);
+  uint64_t* span_out = reinterpret_cast<uint64_t*>(base + o_spo);
 
   // pass 2, 3
   SKS_CK(hipMemsetAsync(has_space, 0, L, s));
   hipLaunchKernelGGL(k_span_lines, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, span_off,
-                     nl, has_space);
-  hipLaunchKernelGGL(k_classify, dim3(grid_for(L)), dim3(kB), 0, s, raw, n, nl, n_nl, L, has_space,
+                     nl, has_space, fb);
+  hipLaunchKernelGGL(k_classify, dim3(grid_for(L)), dim3(kB), 0, s, fb, n, nl, n_nl, L, has_space,
                      cls, setter, ev_rev);
   // pass 4
   need = 0;
@@ -395,11 +469,13 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
     *too_small = true;
     return hipSuccess;
   }
-  // pass 6, 7
-  hipLaunchKernelGGL(k_copy, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, span_off, nl, L,
-                     kept, out_off, out);
-  hipLaunchKernelGGL(k_push, dim3(grid_for(L)), dim3(kB), 0, s, L, cls, have_after, out_off,
-                     push_rank, d_sum, out, rec_end);
+  // pass 6: per-line stream mapping, per-span stream offsets, span copy
+  hipLaunchKernelGGL(k_line_dst, dim3(grid_for(L)), dim3(kB), 0, s, L, nl, kept, out_off, push_rank,
+                     d_sum, dst, out, rec_end);
+  hipLaunchKernelGGL(k_span_out, dim3(grid_for(spans + 1)), dim3(kB), 0, s, spans, n, align, span_off,
+                     nl, kept, out_off, out_len, d_sum, span_out);
+  hipLaunchKernelGGL(k_copy, dim3((unsigned)spans), dim3(kB), 0, s, raw, n, align, span_off, span_out,
+                     L, kept, dst, out);
   return hipGetLastError();
 #undef SKS_CK
 }
