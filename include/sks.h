@@ -148,6 +148,27 @@ int sks_sketch_set_copy(const sks_sketch_set* set, uint32_t i, uint64_t* out);
 int sks_sketch_set_export(const sks_sketch_set* set, uint64_t* d_dst, uint64_t stride,
                           uint32_t* d_sizes);
 
+/* ---- ordered k-mer lists: nucleotide_string_list_to_kmers (kmer_sliding.cpp:112-238) ---
+ * Every selected window of every segment, in stream order, duplicates kept —
+ * the reference's vector<kmer>.  Same inputs as sks_sketch_build; the policy
+ * must be SKS_FRAC_MOD (the per-k-mer predicate; param 1 keeps every window).
+ * Element i: window start byte positions[i] and bits[4i..4i+3] = kmer_bits
+ * (lo, hi), masked_bits (lo, hi) of the reference's `kmer` (kmer.hpp:75-86):
+ * kmer_bits is the chosen strand's window register — R (2w bits), or F, which
+ * in the reference keeps up to 64 bases of the run ending at the window. */
+typedef struct sks_kmer_list sks_kmer_list;
+int sks_kmer_list_build(sks_ctx* ctx, const uint8_t* d_seq, uint64_t n_bytes, const uint64_t* seg_off,
+                        uint32_t n_seg, int window, const uint64_t mask[2], const sks_policy* policy,
+                        sks_kmer_list** out);
+int sks_kmer_list_free(sks_kmer_list* list);
+uint64_t sks_kmer_list_total(const sks_kmer_list* list);
+/* counts[n_seg]: k-mers per segment (the list is segment 0's, then segment 1's, ...). */
+int sks_kmer_list_counts(const sks_kmer_list* list, uint64_t* counts);
+const uint64_t* sks_kmer_list_device_positions(const sks_kmer_list* list);
+const uint64_t* sks_kmer_list_device_bits(const sks_kmer_list* list);
+/* Host copies; either pointer may be NULL. */
+int sks_kmer_list_copy(const sks_kmer_list* list, uint64_t* positions, uint64_t* bits);
+
 /* ---- intersection: kmer_set.cpp:23-41, :143-184 ----------------------------------
  * Sketches in device memory: sketch i = d_data[d_starts[i]*elem_words ...],
  * d_sizes[i] elements, each sorted ascending and unique (as built above). */

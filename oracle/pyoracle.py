@@ -51,6 +51,8 @@ def lib():
         L.ora_frac_min_hash.restype = C.c_uint64
         L.ora_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, u64p,
                                   C.c_int64, C.c_int, C.POINTER(OraBuf)]
+        L.ora_kmer_list.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, u64p,
+                                    C.c_uint64, C.c_int64, C.c_int, C.POINTER(OraBuf)]
         L.ora_sketch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, u64p, C.c_int,
                                  C.c_uint64, C.c_int64, C.c_int, C.POINTER(OraBuf), u64p]
         L.ora_intersect.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
@@ -145,6 +147,23 @@ def windows(runs, w, m, nonce=1, flavour=0):
     finally:
         lib().ora_buf_free(C.byref(b))
     return a.reshape(-1, 10)
+
+
+def kmer_list(runs, w, m, c=200, nonce=1, flavour=0):
+    """nucleotide_string_list_to_kmers with fmh % c == 0: rows of
+    kmer_bits lo, hi, masked lo, hi, run, offset (uint64, shape (n, 6))."""
+    codes, lens = _runs_arrays(runs)
+    b = OraBuf()
+    rc = lib().ora_kmer_list(codes.ctypes.data, lens.ctypes.data, len(lens), w, _mask_arr(m), c,
+                             nonce, flavour, C.byref(b))
+    if rc:
+        raise ValueError("bad args")
+    try:
+        a = np.ctypeslib.as_array(C.cast(b.data, C.POINTER(C.c_uint64)), shape=(b.total,)).copy() \
+            if b.total else np.zeros(0, np.uint64)
+    finally:
+        lib().ora_buf_free(C.byref(b))
+    return a.reshape(-1, 6)
 
 
 def sketch(runs, w, m, kind="frac", param=200, nonce=1, flavour=0):

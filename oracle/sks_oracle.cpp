@@ -315,6 +315,39 @@ int ora_windows(const uint8_t* codes, const uint64_t* run_lens, uint64_t n_runs,
   return 0;
 }
 
+// nucleotide_string_list_to_kmers (kmer_sliding.cpp:112-238) with the
+// FracMinHash predicate fmh % c == 0: the selected windows in order, with
+// duplicates.  Each row is the reference's `kmer`: kmer_bits = the chosen
+// strand's raw window register (F keeps up to 64 bases of the run, never
+// cleared above bit 2w; R holds 2w bits), masked_bits = min(F & M, R & M)
+// with ties to R (:159-175).  Rows: kmer_bits lo, hi, masked lo, hi, run, offset.
+int ora_kmer_list(const uint8_t* codes, const uint64_t* run_lens, uint64_t n_runs, int w,
+                  const uint64_t* mask, uint64_t c, int64_t nonce, int flavour, ora_buf* out) {
+  if (w < 1 || w > 64 || c == 0) return 1;
+  u128 M = ((u128)mask[1] << 64) | mask[0];
+  std::vector<uint64_t> rows;
+  uint64_t off = 0;
+  for (uint64_t r = 0; r < n_runs; ++r) {
+    uint64_t i = 0;
+    slide(codes + off, run_lens[r], w, M, [&](u128 F, u128 R, u128 C) {
+      const u128 bits = ((F & M) < (R & M)) ? F : R;
+      if (frac_min_hash(C, M, w, nonce, flavour) % c == 0) {
+        uint64_t row[6] = {(uint64_t)bits, (uint64_t)(bits >> 64), (uint64_t)C,
+                           (uint64_t)(C >> 64), r, i};
+        rows.insert(rows.end(), row, row + 6);
+      }
+      ++i;
+    });
+    off += run_lens[r];
+  }
+  out->n = rows.size() / 6;
+  out->total = rows.size();
+  out->data = (uint8_t*)malloc(8 * (rows.size() ? rows.size() : 1));
+  out->lens = nullptr;
+  if (!rows.empty()) memcpy(out->data, rows.data(), 8 * rows.size());
+  return 0;
+}
+
 // Sketch of one genome given as runs.  kind 0 = FracMinHash (keep iff
 // fmh % param == 0; kmer-sketching.cpp:30-34 with c = param), kind 1 =
 // bottom-s (build-defined: the `param` distinct canonical k-mers with the

@@ -374,16 +374,59 @@ std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files,
                                policy);
 }
 
-kmer_set nucleotide_string_list_to_kmer_set(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
-                                            const kmer_bitset& mask, const int window_length,
-                                            const sketch_policy& policy) {
+namespace {
+// acgt_strings -> record stream; codes act through their low two bits like the
+// reference's update_kmer_window (kmer_sliding.cpp:26-47).
+std::vector<uint8_t> runs_stream(const std::vector<std::vector<uint8_t>>& nucleotide_strings) {
   static const char kAcgt[4] = {'A', 'C', 'G', 'T'};
   std::vector<uint8_t> s;
   for (const auto& run : nucleotide_strings) {
-    for (uint8_t b : run) s.push_back(b < 4 ? (uint8_t)kAcgt[b] : (uint8_t)'N');
+    for (uint8_t b : run) s.push_back((uint8_t)kAcgt[b & 3]);
     s.push_back('\n');
   }
-  return sks::sketch_streams({s}, mask, window_length, policy)[0];
+  return s;
+}
+}  // namespace
+
+kmer_set nucleotide_string_list_to_kmer_set(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                            const kmer_bitset& mask, const int window_length,
+                                            const sketch_policy& policy) {
+  return sks::sketch_streams({runs_stream(nucleotide_strings)}, mask, window_length, policy)[0];
+}
+
+void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& kmer_list,
+                                                  const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketch_policy& sketching_cond) {
+  if (sketching_cond.kind != SKS_FRAC_MOD)
+    throw std::invalid_argument("nucleotide_string_list_to_kmers: needs a per-k-mer (FracMinHash) condition");
+  const std::vector<uint8_t> s = runs_stream(nucleotide_strings);
+  if (s.empty()) return;
+  sks::DevMem d(s.size());
+  sks::check_hip(hipMemcpy(d.p, s.data(), s.size(), hipMemcpyHostToDevice), "hipMemcpy H2D");
+  sks_policy p{sketching_cond.kind, sketching_cond.flavour, sketching_cond.param, sketching_cond.nonce};
+  const uint64_t m[2] = {mask.lo(), mask.hi()};
+  const uint64_t seg[2] = {0, s.size()};
+  sks_kmer_list* kl = nullptr;
+  sks::check(sks_kmer_list_build(sks::ctx(), d.as<uint8_t>(), s.size(), seg, 1, window_length, m, &p, &kl));
+  const uint64_t n = sks_kmer_list_total(kl);
+  std::vector<uint64_t> bits(4 * n);
+  const int rc = sks_kmer_list_copy(kl, nullptr, bits.data());
+  sks_kmer_list_free(kl);
+  sks::check(rc);
+  kmer_list.reserve(kmer_list.size() + n);
+  for (uint64_t i = 0; i < n; ++i)
+    kmer_list.push_back(kmer{window_length, kmer_bitset(bits[4 * i], bits[4 * i + 1]), mask,
+                             kmer_bitset(bits[4 * i + 2], bits[4 * i + 3])});
+}
+
+std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketch_policy& sketching_cond) {
+  std::vector<kmer> out;
+  nucleotide_string_list_to_kmers_by_reference(out, nucleotide_strings, mask, window_length,
+                                               sketching_cond);
+  return out;
 }
 
 // ---- pairwise -------------------------------------------------------------------------------------------

@@ -206,14 +206,28 @@ kmer_set kmer_set_from_fasta_file(const char fasta_filename[], const kmer_bitset
 std::vector<kmer_set> kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
                                                  const kmer_bitset& mask, const int window_length,
                                                  const sketch_policy& policy);
-// Host file parsing runs on worker threads; sketching is one batched GPU launch.
+// Files are read on worker threads; parsing (sks_fasta_parse_device) and
+// sketching run on the GPU, all files in one batched build.
 std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files,
                                                           char* fasta_filenames[],
                                                           const kmer_bitset& mask,
                                                           const int window_length,
                                                           const sketch_policy& policy);
-// The set of k-mers the reference's nucleotide_string_list_to_kmers selects
-// from these runs (duplicates collapsed).
+// nucleotide_string_list_to_kmers[_by_reference] (kmer_sliding.cpp:199-238):
+// every selected window of every run, in order, duplicates kept, each with
+// the reference's kmer_bits / masked_bits.  The predicate must be a
+// per-k-mer FracMinHash condition (frac_mod_condition, or sketch_policy::frac;
+// c = 1 keeps every window); a bottom-s policy throws std::invalid_argument.
+// Codes are used as the reference uses them (low two bits, kmer_sliding.cpp:26-47).
+std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketch_policy& sketching_cond);
+void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& kmer_list,
+                                                  const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketch_policy& sketching_cond);
+// The set of k-mers nucleotide_string_list_to_kmers selects from these runs
+// (duplicates collapsed).
 kmer_set nucleotide_string_list_to_kmer_set(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
                                             const kmer_bitset& mask, const int window_length,
                                             const sketch_policy& policy);

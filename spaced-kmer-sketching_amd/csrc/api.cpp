@@ -56,6 +56,15 @@ struct sks_ctx {
   int grid_override = 0;
 };
 
+struct sks_kmer_list {
+  int device = 0;
+  uint32_t n = 0;
+  uint64_t total = 0;
+  uint64_t* d_pos = nullptr;   // [total] window start byte of each k-mer, stream order
+  uint64_t* d_bits = nullptr;  // [total][4] kmer_bits lo, hi, masked_bits lo, hi
+  std::vector<uint64_t> counts;
+};
+
 struct sks_sketch_set {
   int device = 0;
   int elem_words = 1;
@@ -463,6 +472,36 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   return SKS_OK;
 }
 
+// Argument checks shared by sks_sketch_build and sks_kmer_list_build.
+int validate_build(const char* fn, sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes,
+                   const uint64_t* seg_off, uint32_t n_seg, int window, const uint64_t mask[2],
+                   const sks_policy* policy) {
+  const std::string f(fn);
+  if (!c || !mask || !policy || (!seg_off && n_seg)) return sks::fail(SKS_E_ARG, f + ": null argument");
+  if (window < 1 || window > 64)
+    return sks::fail(SKS_E_ARG, f + ": window must be in [1, 64] (MAX_KMER_LENGTH)");
+  if (policy->kind != SKS_FRAC_MOD && policy->kind != SKS_BOTTOM_S)
+    return sks::fail(SKS_E_ARG, f + ": unknown policy kind");
+  if (policy->flavour != 0 && policy->flavour != 1)
+    return sks::fail(SKS_E_ARG, f + ": unknown hash flavour");
+  if (policy->param == 0) return sks::fail(SKS_E_ARG, f + ": policy param must be > 0");
+  {
+    const int bits = 2 * window;
+    uint64_t lo_allowed = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+    uint64_t hi_allowed = bits <= 64 ? 0 : (bits >= 128 ? ~0ull : ((1ull << (bits - 64)) - 1));
+    if ((mask[0] & ~lo_allowed) || (mask[1] & ~hi_allowed))
+      return sks::fail(SKS_E_UNSUPPORTED,
+                       f + ": mask has bits at or above 2*window (the reference's "
+                       "generate_random_spaced_seed_mask never produces such masks)");
+  }
+  if (n_bytes && !d_seq) return sks::fail(SKS_E_ARG, f + ": null sequence");
+  for (uint32_t g = 0; g < n_seg; ++g)
+    if (seg_off[g] > seg_off[g + 1] || seg_off[g + 1] > n_bytes)
+      return sks::fail(SKS_E_ARG, f + ": segment offsets must be non-decreasing and <= n_bytes");
+
+  return SKS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -470,29 +509,9 @@ extern "C" {
 int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const uint64_t* seg_off,
                      uint32_t n_seg, int window, const uint64_t mask[2], const sks_policy* policy,
                      sks_sketch_set** out) {
-  if (!c || !mask || !policy || !out || (!seg_off && n_seg))
-    return sks::fail(SKS_E_ARG, "sks_sketch_build: null argument");
+  if (!out) return sks::fail(SKS_E_ARG, "sks_sketch_build: null argument");
   *out = nullptr;
-  if (window < 1 || window > 64)
-    return sks::fail(SKS_E_ARG, "sks_sketch_build: window must be in [1, 64] (MAX_KMER_LENGTH)");
-  if (policy->kind != SKS_FRAC_MOD && policy->kind != SKS_BOTTOM_S)
-    return sks::fail(SKS_E_ARG, "sks_sketch_build: unknown policy kind");
-  if (policy->flavour != 0 && policy->flavour != 1)
-    return sks::fail(SKS_E_ARG, "sks_sketch_build: unknown hash flavour");
-  if (policy->param == 0) return sks::fail(SKS_E_ARG, "sks_sketch_build: policy param must be > 0");
-  {
-    const int bits = 2 * window;
-    uint64_t lo_allowed = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
-    uint64_t hi_allowed = bits <= 64 ? 0 : (bits >= 128 ? ~0ull : ((1ull << (bits - 64)) - 1));
-    if ((mask[0] & ~lo_allowed) || (mask[1] & ~hi_allowed))
-      return sks::fail(SKS_E_UNSUPPORTED,
-                       "sks_sketch_build: mask has bits at or above 2*window (the reference's "
-                       "generate_random_spaced_seed_mask never produces such masks)");
-  }
-  if (n_bytes && !d_seq) return sks::fail(SKS_E_ARG, "sks_sketch_build: null sequence");
-  for (uint32_t g = 0; g < n_seg; ++g)
-    if (seg_off[g] > seg_off[g + 1] || seg_off[g + 1] > n_bytes)
-      return sks::fail(SKS_E_ARG, "sks_sketch_build: segment offsets must be non-decreasing and <= n_bytes");
+  SKS_TRY(validate_build("sks_sketch_build", c, d_seq, n_bytes, seg_off, n_seg, window, mask, policy));
 
   DeviceGuard guard(c->device);
   hipStream_t st = c->stream;
@@ -767,6 +786,147 @@ int sks_sketch_set_export(const sks_sketch_set* set, uint64_t* d_dst, uint64_t s
   SKS_HIP(sks::launch_export(set->d_data, set->d_starts, set->d_sizes, set->n, set->elem_words,
                              d_dst, stride, d_sizes, nullptr));
   SKS_HIP(hipStreamSynchronize(nullptr));
+  return SKS_OK;
+}
+
+// ---- ordered k-mer lists (nucleotide_string_list_to_kmers) -----------------------------------
+
+int sks_kmer_list_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const uint64_t* seg_off,
+                        uint32_t n_seg, int window, const uint64_t mask[2], const sks_policy* policy,
+                        sks_kmer_list** out) {
+  if (!out) return sks::fail(SKS_E_ARG, "sks_kmer_list_build: null argument");
+  *out = nullptr;
+  SKS_TRY(validate_build("sks_kmer_list_build", c, d_seq, n_bytes, seg_off, n_seg, window, mask,
+                         policy));
+  if (policy->kind != SKS_FRAC_MOD)
+    return sks::fail(SKS_E_UNSUPPORTED,
+                     "sks_kmer_list_build: lists take a per-k-mer predicate (SKS_FRAC_MOD); "
+                     "bottom-s is a set selection");
+  DeviceGuard guard(c->device);
+  hipStream_t st = c->stream;
+  const bool wide = window > 32;
+  const sks::DivTest dt = sks::make_div_test(policy->param);
+  std::vector<uint64_t> beg(n_seg), end(n_seg), tp(n_seg + 1, 0), cap(n_seg), ooff(n_seg);
+  for (uint32_t g = 0; g < n_seg; ++g) {
+    beg[g] = seg_off[g];
+    end[g] = seg_off[g + 1];
+    tp[g + 1] = tp[g] + sks::scan_tiles_for(end[g] - beg[g]);
+    const double expect = (double)(end[g] - beg[g]) / (double)policy->param;
+    cap[g] = (uint64_t)std::min<double>(expect + 6.0 * std::sqrt(expect) + 4096.0,
+                                        (double)(end[g] - beg[g]) + 1.0);
+  }
+  std::vector<uint64_t> counts(n_seg, 0);
+  for (int pass = 0; pass < 2; ++pass) {  // pass 2 only if a capacity estimate overflowed
+    uint64_t total_cap = 0;
+    for (uint32_t g = 0; g < n_seg; ++g) {
+      ooff[g] = total_cap;
+      total_cap += cap[g];
+    }
+    SKS_HIP(c->rec[0].reserve(std::max<uint64_t>(total_cap, 1) * sizeof(uint64_t)));
+    MetaArena arena(c);
+    size_t o_beg = arena.add(beg), o_end = arena.add(end), o_tp = arena.add(tp),
+           o_cap = arena.add(cap), o_off = arena.add(ooff), o_cnt = arena.add_zero(n_seg),
+           o_win = arena.add_zero(n_seg);
+    SKS_TRY(arena.upload());
+    sks::ScanParams p{};
+    p.seq = d_seq;
+    p.seg_begin = arena.ptr(o_beg);
+    p.seg_end = arena.ptr(o_end);
+    p.tile_prefix = arena.ptr(o_tp);
+    p.n_seg = n_seg;
+    p.n_tiles = tp[n_seg];
+    p.w = window;
+    p.mask_lo = mask[0];
+    p.mask_hi = mask[1];
+    p.kconst = sks::fmh_const(mask[0], mask[1], window, policy->nonce, policy->flavour);
+    p.low_mask = dt.low_mask;
+    p.high_mask = dt.rot > 32 ? (uint32_t)((1ull << (dt.rot - 32)) - 1) : 0u;
+    p.dinv = dt.dinv;
+    p.dlim = dt.lim;
+    p.seg_thresh = arena.ptr(o_cap);  // unused in list mode
+    p.out_key = reinterpret_cast<uint64_t*>(c->rec[0].ptr);
+    p.seg_out_off = arena.ptr(o_off);
+    p.seg_out_cap = arena.ptr(o_cap);
+    p.seg_count = reinterpret_cast<unsigned long long*>(arena.ptr(o_cnt));
+    p.seg_windows = reinterpret_cast<unsigned long long*>(arena.ptr(o_win));
+    SKS_HIP(sks::launch_scan(p, sks::kModeList, policy->flavour, wide, c->device, st,
+                             c->grid_override));
+    SKS_HIP(hipMemcpyAsync(counts.data(), p.seg_count, n_seg * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, st));
+    SKS_HIP(hipStreamSynchronize(st));
+    bool overflow = false;
+    for (uint32_t g = 0; g < n_seg; ++g)
+      if (counts[g] > cap[g]) {
+        overflow = true;
+        cap[g] = counts[g];
+      }
+    if (!overflow) break;
+    if (pass == 1) return sks::fail(SKS_E_HIP, "sks_kmer_list_build: survivor count changed between passes");
+  }
+  // dense positions (segments in stream order), then one sort: stream order
+  std::vector<uint64_t> csr = prefix(counts);
+  const uint64_t T = csr[n_seg];
+  uint64_t max_len = 0;
+  for (uint64_t v : counts) max_len = std::max(max_len, v);
+  sks_kmer_list* kl = new (std::nothrow) sks_kmer_list();
+  if (!kl) return sks::fail(SKS_E_NOMEM, "sks_kmer_list_build: out of memory");
+  kl->device = c->device;
+  kl->n = n_seg;
+  kl->total = T;
+  kl->counts = counts;
+  int rc = alloc_u64(&kl->d_pos, T);
+  if (rc == SKS_OK) rc = alloc_u64(&kl->d_bits, 4 * T);
+  if (rc == SKS_OK) rc = reserve_cols(c, {0}, T + 1);
+  MetaArena arena(c);
+  size_t o_src = arena.add(ooff), o_csr = arena.add(csr), o_beg = arena.add(beg);
+  if (rc == SKS_OK) rc = arena.upload();
+  hipError_t e = hipSuccess;
+  if (rc == SKS_OK && T) {
+    e = sks::compact_regions(reinterpret_cast<uint64_t*>(c->rec[0].ptr), col(c, 0), arena.ptr(o_src),
+                             arena.ptr(o_csr), n_seg, max_len, st);
+    if (e == hipSuccess)
+      e = sks::seg_sort_keys(col(c, 0), kl->d_pos, T, {0, T}, nullptr, end_bit_of(n_bytes), c->tmp, st);
+    if (e == hipSuccess)
+      e = sks::launch_materialise(d_seq, arena.ptr(o_beg), n_seg, kl->d_pos, T, window, mask[0],
+                                  mask[1], kl->d_bits, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = sks::fail(SKS_E_HIP, std::string("sks_kmer_list_build: ") + hipGetErrorString(e));
+  }
+  if (rc != SKS_OK) {
+    sks_kmer_list_free(kl);
+    return rc;
+  }
+  *out = kl;
+  return SKS_OK;
+}
+
+int sks_kmer_list_free(sks_kmer_list* kl) {
+  if (!kl) return SKS_OK;
+  DeviceGuard g(kl->device);
+  if (kl->d_pos) (void)hipFree(kl->d_pos);
+  if (kl->d_bits) (void)hipFree(kl->d_bits);
+  delete kl;
+  return SKS_OK;
+}
+
+uint64_t sks_kmer_list_total(const sks_kmer_list* kl) { return kl ? kl->total : 0; }
+
+int sks_kmer_list_counts(const sks_kmer_list* kl, uint64_t* counts) {
+  if (!kl || (!counts && kl->n)) return sks::fail(SKS_E_ARG, "sks_kmer_list_counts: null argument");
+  std::copy(kl->counts.begin(), kl->counts.end(), counts);
+  return SKS_OK;
+}
+
+const uint64_t* sks_kmer_list_device_positions(const sks_kmer_list* kl) { return kl ? kl->d_pos : nullptr; }
+const uint64_t* sks_kmer_list_device_bits(const sks_kmer_list* kl) { return kl ? kl->d_bits : nullptr; }
+
+int sks_kmer_list_copy(const sks_kmer_list* kl, uint64_t* positions, uint64_t* bits) {
+  if (!kl) return sks::fail(SKS_E_ARG, "sks_kmer_list_copy: null list");
+  DeviceGuard g(kl->device);
+  if (positions && kl->total)
+    SKS_HIP(hipMemcpy(positions, kl->d_pos, kl->total * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (bits && kl->total)
+    SKS_HIP(hipMemcpy(bits, kl->d_bits, kl->total * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return SKS_OK;
 }
 

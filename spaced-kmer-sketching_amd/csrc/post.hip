@@ -189,6 +189,49 @@ __global__ void k_gather(const uint64_t* __restrict__ src, const uint64_t* __res
     out[i] = src[idx[i]];
 }
 
+// ACGT (either case) -> 0..3, anything else -> 4 (fasta_processing.cpp:35-69)
+__device__ __forceinline__ uint32_t base_code(uint8_t c) {
+  const uint32_t low = c | 0x20u;
+  const uint32_t code = ((low >> 1) ^ (low >> 2)) & 3u;
+  return ("acgt"[code] == (char)low) ? code : 4u;
+}
+
+__global__ void k_materialise(const uint8_t* __restrict__ seq, const uint64_t* __restrict__ seg_begin,
+                              uint32_t n_seg, const uint64_t* __restrict__ pos, uint64_t n, int w,
+                              uint64_t mask_lo, uint64_t mask_hi, uint64_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kB) {
+    const uint64_t p = pos[i];
+    uint32_t lo = 0, hi = n_seg;  // last segment with seg_begin <= p
+    while (lo + 1 < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (seg_begin[mid] <= p) lo = mid; else hi = mid;
+    }
+    const uint64_t sb = n_seg ? seg_begin[lo] : 0;
+    // run history before the window: at most 64 - w bases, stopping at a
+    // non-ACGT byte or the segment start (the reference starts each run
+    // with an empty window, kmer_sliding.cpp:129)
+    uint64_t h = 0;
+    while (h + w < 64 && p > sb + h && base_code(seq[p - h - 1]) < 4) ++h;
+    uint64_t fl = 0, fh = 0, rl = 0, rh = 0;
+    for (uint64_t b = p - h; b < p + w; ++b) {  // F <<= 2, F[0..1] = base
+      const uint64_t c = base_code(seq[b]) & 3u;
+      fh = (fh << 2) | (fl >> 62);
+      fl = (fl << 2) | c;
+    }
+    for (int k = 0; k < w; ++k) {  // R = sum comp(b_k) << 2k
+      const uint64_t c = (base_code(seq[p + k]) & 3u) ^ 3u;
+      if (k < 32) rl |= c << (2 * k);
+      else rh |= c << (2 * (k - 32));
+    }
+    const uint64_t fml = fl & mask_lo, fmh = fh & mask_hi, rml = rl & mask_lo, rmh = rh & mask_hi;
+    const bool f_lt = fmh < rmh || (fmh == rmh && fml < rml);  // kmer_sliding.cpp:165
+    out[4 * i + 0] = f_lt ? fl : rl;
+    out[4 * i + 1] = f_lt ? fh : rh;
+    out[4 * i + 2] = f_lt ? fml : rml;
+    out[4 * i + 3] = f_lt ? fmh : rmh;
+  }
+}
+
 inline unsigned grid_for(uint64_t n) {
   uint64_t g = (n + kB - 1) / kB;
   return (unsigned)std::min<uint64_t>(std::max<uint64_t>(g, 1), 65535);
@@ -274,6 +317,15 @@ hipError_t launch_export(const uint64_t* data, const uint64_t* starts, const uin
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_export, dim3(grid_for(stride * elem_words), n), dim3(kB), 0, s, data, starts,
                      sizes, elem_words, dst, stride, dst_sizes);
+  return hipGetLastError();
+}
+
+hipError_t launch_materialise(const uint8_t* seq, const uint64_t* seg_begin, uint32_t n_seg,
+                              const uint64_t* pos, uint64_t n, int w, uint64_t mask_lo,
+                              uint64_t mask_hi, uint64_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_materialise, dim3(grid_for(n)), dim3(kB), 0, s, seq, seg_begin, n_seg, pos, n,
+                     w, mask_lo, mask_hi, out);
   return hipGetLastError();
 }
 

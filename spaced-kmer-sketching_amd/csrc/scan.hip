@@ -7,7 +7,9 @@
 //   canonical C = min(F & M, R & M), ties -> R & M (same value)   (:159-175)
 //   fmh = H(C) ^ H(M) ^ w ^ nonce   (kmer.hpp:141-148, boost hash flavour)
 // and applies the selection policy (FracMinHash `fmh % c == 0`, or the
-// bottom-s pre-filter `fmh <= threshold`) in the same kernel.  Bytes that are
+// bottom-s pre-filter `fmh <= threshold`) in the same kernel.  List mode
+// (nucleotide_string_list_to_kmers) applies the FracMinHash test and emits the
+// window's start position instead of the k-mer (materialised later in order).  Bytes that are
 // not A/C/G/T (either case) split runs exactly like
 // fasta_processing.cpp:144-179; a window is valid iff all its w bytes are
 // ACGT and lie inside its segment, so k-mers never span runs or genomes.
@@ -184,7 +186,7 @@ __device__ __forceinline__ uint64_t fmh_narrow(const ScanParams& p, uint64_t c) 
 
 template <int MODE>
 __device__ __forceinline__ bool keep_fmh(const ScanParams& p, uint64_t f, uint64_t thresh) {
-  if constexpr (MODE == kModeFrac) return div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim);
+  if constexpr (MODE != kModeBottom) return div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim);
   else return f <= thresh;
 }
 
@@ -332,9 +334,13 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
     while (keepmask) {
       const uint32_t j = __builtin_ctz(keepmask);
       keepmask &= keepmask - 1;
-      const uint64_t c = canon(j);
-      if constexpr (MODE == kModeFrac) emit<MODE>(p, q, g.seg, c, 0);
-      else emit<MODE>(p, q, g.seg, fmh_narrow<FLAVOUR>(p, c), c);
+      if constexpr (MODE == kModeList) {
+        emit<MODE>(p, q, g.seg, g.win0 + (uint64_t)(kWPT * tid) + j, 0);  // window start byte
+      } else {
+        const uint64_t c = canon(j);
+        if constexpr (MODE == kModeFrac) emit<MODE>(p, q, g.seg, c, 0);
+        else emit<MODE>(p, q, g.seg, fmh_narrow<FLAVOUR>(p, c), c);
+      }
     }
 
     // 5) flush the queue once it is half full
@@ -393,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
       for (uint32_t i = tid; i < n; i += kBlock)
         if (base + i < c) {
           p.out_key[off + base + i] = q_a[i];
-          p.out_val[off + base + i] = q_b[i];
+          if (MODE != kModeList) p.out_val[off + base + i] = q_b[i];
           if (MODE == kModeBottom) p.out_hi[off + base + i] = q_c[i];
         }
     }
@@ -480,11 +486,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
         h = hash_bitset128<1>(cl, ch);
       }
       uint64_t f = h ^ p.kconst;
-      bool keep = (MODE == kModeFrac) ? div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim)
-                                      : (f <= thresh);
+      bool keep = (MODE != kModeBottom) ? div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim)
+                                        : (f <= thresh);
       if (valid && keep) {
         uint32_t slot = atomicAdd(&q_n, 1u);
-        uint64_t a = (MODE == kModeFrac) ? cl : f;
+        uint64_t a = (MODE == kModeList) ? g.win0 + (uint64_t)(kWPT * tid) + j
+                                         : (MODE == kModeFrac) ? cl : f;
         uint64_t b = (MODE == kModeFrac) ? ch : cl;
         if (slot < cap) {
           q_a[slot] = a; q_b[slot] = b; q_c[slot] = ch;
@@ -492,7 +499,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
           unsigned long long gi = atomicAdd(&p.seg_count[g.seg], 1ull);
           if (gi < p.seg_out_cap[g.seg]) {
             uint64_t o = p.seg_out_off[g.seg] + gi;
-            p.out_key[o] = a; p.out_val[o] = b;
+            p.out_key[o] = a;
+            if (MODE != kModeList) p.out_val[o] = b;
             if (MODE == kModeBottom) p.out_hi[o] = ch;
           }
         }
@@ -531,9 +539,11 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
   };
   if (!wide) {
     if (mode == kModeFrac) return flavour == 0 ? pick(scan_kernel<kModeFrac, 0>) : pick(scan_kernel<kModeFrac, 1>);
+    if (mode == kModeList) return flavour == 0 ? pick(scan_kernel<kModeList, 0>) : pick(scan_kernel<kModeList, 1>);
     return flavour == 0 ? pick(scan_kernel<kModeBottom, 0>) : pick(scan_kernel<kModeBottom, 1>);
   }
   if (mode == kModeFrac) return flavour == 0 ? pick(scan_kernel_wide<kModeFrac, 0>) : pick(scan_kernel_wide<kModeFrac, 1>);
+  if (mode == kModeList) return flavour == 0 ? pick(scan_kernel_wide<kModeList, 0>) : pick(scan_kernel_wide<kModeList, 1>);
   return flavour == 0 ? pick(scan_kernel_wide<kModeBottom, 0>) : pick(scan_kernel_wide<kModeBottom, 1>);
 }
 

@@ -10,6 +10,7 @@ namespace sks {
 
 constexpr int kModeFrac = 0;
 constexpr int kModeBottom = 1;
+constexpr int kModeList = 2;  // FracMinHash test, emits window start positions
 
 // Arguments of the fused scan kernel (scan.hip).  All per-segment arrays are
 // device arrays indexed by the launch-local segment index.
@@ -119,6 +120,14 @@ hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_se
 hipError_t launch_export(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                          uint32_t n, int elem_words, uint64_t* dst, uint64_t stride,
                          uint32_t* dst_sizes, hipStream_t s);
+// nucleotide_string_to_kmers' `kmer` for each selected window start pos[i]
+// (kmer_sliding.cpp:112-186): out[4i..4i+3] = kmer_bits (lo, hi), masked_bits
+// (lo, hi).  kmer_bits is the chosen strand's window register: R (2w bits), or
+// F holding up to 64 bases of the run ending at the window (the reference
+// never clears F's older bases).  seg_begin: [n_seg] sorted segment starts.
+hipError_t launch_materialise(const uint8_t* seq, const uint64_t* seg_begin, uint32_t n_seg,
+                              const uint64_t* pos, uint64_t n, int w, uint64_t mask_lo,
+                              uint64_t mask_hi, uint64_t* out, hipStream_t s);
 hipError_t launch_iota(uint64_t* out, uint64_t n, hipStream_t s);
 hipError_t launch_gather(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
                          hipStream_t s);

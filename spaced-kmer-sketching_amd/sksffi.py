@@ -48,7 +48,9 @@ EXPORTED = [
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
     "sks_synth_bases", "sks_intersect_sym", "sks_intersect_sym_tiles",
     "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_fasta_parse_device",
-    "sks_ctx_last_ingress_ms",
+    "sks_ctx_last_ingress_ms", "sks_kmer_list_build", "sks_kmer_list_free", "sks_kmer_list_total",
+    "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
+    "sks_kmer_list_copy",
 ]
 
 _lib = None
@@ -92,6 +94,16 @@ def lib():
     L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.sks_kmer_list_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
+                                      C.POINTER(Policy), C.POINTER(vp)]
+    L.sks_kmer_list_free.argtypes = [vp]
+    L.sks_kmer_list_total.argtypes = [vp]
+    L.sks_kmer_list_total.restype = C.c_uint64
+    L.sks_kmer_list_counts.argtypes = [vp, vp]
+    L.sks_kmer_list_copy.argtypes = [vp, vp, vp]
+    for f in ("sks_kmer_list_device_positions", "sks_kmer_list_device_bits"):
+        getattr(L, f).argtypes = [vp]
+        getattr(L, f).restype = vp
     L.sks_fasta_parse_device.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64,
                                          u64p, u64p]
     L.sks_sketch_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
@@ -285,6 +297,26 @@ class Context:
                                      len(seg) - 1, window, _mask_arr(mask), C.byref(pol),
                                      C.byref(h)))
         return SketchSet(h)
+
+    def kmer_list(self, d_seq_ptr, n_bytes, seg_off, window, mask, c=200, nonce=1, flavour=0):
+        """nucleotide_string_list_to_kmers on the device: returns (positions,
+        bits[n, 4] = kmer_bits lo, hi, masked lo, hi, counts per segment)."""
+        seg = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        pol = Policy(SKS_FRAC_MOD, flavour, c, nonce)
+        h = C.c_void_p()
+        check(lib().sks_kmer_list_build(self.h, C.c_void_p(d_seq_ptr), n_bytes, seg.ctypes.data,
+                                        len(seg) - 1, window, _mask_arr(mask), C.byref(pol),
+                                        C.byref(h)))
+        try:
+            n = int(lib().sks_kmer_list_total(h))
+            pos = np.zeros(max(n, 1), np.uint64)
+            bits = np.zeros(max(4 * n, 1), np.uint64)
+            counts = np.zeros(max(len(seg) - 1, 1), np.uint64)
+            check(lib().sks_kmer_list_copy(h, pos.ctypes.data, bits.ctypes.data))
+            check(lib().sks_kmer_list_counts(h, counts.ctypes.data))
+        finally:
+            lib().sks_kmer_list_free(h)
+        return pos[:n], bits[:4 * n].reshape(n, 4), counts[:len(seg) - 1]
 
     def intersect_pairs(self, data_ptr, starts_ptr, sizes_ptr, elem_words, a_ptr, b_ptr,
                         n_pairs, out_ptr):

@@ -130,12 +130,28 @@ static int csv(int argc, char** argv) {
   return 0;
 }
 
+// test_facade list <w> <k> <mask_seed> <c> <file>: nucleotide_string_list_to_kmers
+// on the file's runs; one line per kmer: kmer_bits masked_bits (hex)
+static int list(char** argv) {
+  const int w = std::atoi(argv[2]), k = std::atoi(argv[3]);
+  const kmer_bitset mask = generate_random_spaced_seed_mask(w, k, std::strtoull(argv[4], nullptr, 10));
+  const frac_mod_condition cond{frac_min_hash(1), std::strtoull(argv[5], nullptr, 10)};
+  auto runs = nucleotide_strings_from_fasta_file(argv[6]);
+  std::vector<kmer> ks = nucleotide_string_list_to_kmers(runs, mask, w, cond);
+  for (const kmer& x : ks)
+    std::printf("%llx%016llx %llx%016llx\n", (unsigned long long)x.kmer_bits.hi(),
+                (unsigned long long)x.kmer_bits.lo(), (unsigned long long)x.masked_bits.hi(),
+                (unsigned long long)x.masked_bits.lo());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 64;
   std::string mode = argv[1];
   if (mode == "sketch" && argc >= 8) return sketch(argc, argv);
   if (mode == "errors") return errors();
   if (mode == "csv" && argc >= 8) return csv(argc, argv);
+  if (mode == "list" && argc == 7) return list(argv);
   if (mode == "missing" && argc == 3) {
     char* f[1] = {argv[2]};
     kmer_bitset mask = generate_random_spaced_seed_mask(21, 21, 0);
