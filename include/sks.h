@@ -102,6 +102,8 @@ typedef struct sks_ctx sks_ctx;
 int sks_ctx_create(int device, void* stream, sks_ctx** out);
 int sks_ctx_destroy(sks_ctx* ctx);
 int sks_ctx_set_stream(sks_ctx* ctx, void* stream);
+/* The device index the context was created on (-1 for NULL). */
+int sks_ctx_device(const sks_ctx* ctx);
 int sks_ctx_synchronize(sks_ctx* ctx);
 
 /* Per-phase device times of the last sketch build / intersection on this
@@ -147,6 +149,32 @@ int sks_sketch_set_copy(const sks_sketch_set* set, uint32_t i, uint64_t* out);
  * (d_dst[i * stride * elem_words ...], d_sizes[i]) — the all-gather shape. */
 int sks_sketch_set_export(const sks_sketch_set* set, uint64_t* d_dst, uint64_t stride,
                           uint32_t* d_sizes);
+
+/* ---- persisted sketches (no reference equivalent) ------------------
+ * A sketch set remembers how it was made; sks_sketch_set_save writes it with
+ * that description to a self-checking file (format: csrc/persist.cpp) and
+ * sks_sketch_set_load brings it back onto the context's device, ready for
+ * sks_intersect_*.  A missing, truncated or corrupt file -> SKS_E_IO. */
+typedef struct sks_sketch_info {
+  int32_t window;
+  int32_t elem_words;
+  uint64_t mask[2];
+  sks_policy policy;
+  uint32_t n;
+  int32_t has_names;
+} sks_sketch_info;
+int sks_sketch_set_info(const sks_sketch_set* set, sks_sketch_info* info);
+/* names: n strings (e.g. the FASTA file names), or NULL to clear. */
+int sks_sketch_set_set_names(sks_sketch_set* set, const char* const* names);
+/* Name of sketch i, or NULL when the set has no names. */
+const char* sks_sketch_set_name(const sks_sketch_set* set, uint32_t i);
+int sks_sketch_set_save(const sks_sketch_set* set, const char* path);
+int sks_sketch_set_load(sks_ctx* ctx, const char* path, sks_sketch_set** out);
+/* One set holding the sketches of sets[0], sets[1], ... in order (e.g. shards
+ * sketched on different ranks or at different times).  All sets must share
+ * window, mask and policy. */
+int sks_sketch_set_concat(sks_ctx* ctx, const sks_sketch_set* const* sets, uint32_t n_sets,
+                          sks_sketch_set** out);
 
 /* ---- ordered k-mer lists: nucleotide_string_list_to_kmers (kmer_sliding.cpp:112-238) ---
  * Every selected window of every segment, in stream order, duplicates kept —

@@ -65,17 +65,6 @@ struct sks_kmer_list {
   std::vector<uint64_t> counts;
 };
 
-struct sks_sketch_set {
-  int device = 0;
-  int elem_words = 1;
-  uint32_t n = 0;
-  uint64_t* d_data = nullptr;    // elements (elem_words u64 each)
-  uint64_t* d_starts = nullptr;  // [n] element index of each sketch
-  uint32_t* d_sizes = nullptr;   // [n]
-  std::vector<uint32_t> sizes;
-  std::vector<uint64_t> starts;
-  std::vector<uint64_t> windows;
-};
 
 namespace {
 
@@ -268,6 +257,8 @@ int sks_ctx_destroy(sks_ctx* c) {
   delete c;
   return SKS_OK;
 }
+
+int sks_ctx_device(const sks_ctx* c) { return c ? c->device : -1; }
 
 int sks_ctx_set_stream(sks_ctx* c, void* stream) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_set_stream: null ctx");
@@ -661,6 +652,10 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
   set->sizes.resize(n_seg);
   set->starts.resize(n_seg);
   set->windows = windows_g;
+  set->window = window;
+  set->mask[0] = mask[0];
+  set->mask[1] = mask[1];
+  set->policy = *policy;
   uint64_t total = 0;
   for (uint32_t g = 0; g < n_seg; ++g) {
     set->starts[g] = total;

@@ -2,8 +2,27 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "sks.h"
+
+// A device-resident set of sketches (one per genome / segment).
+struct sks_sketch_set {
+  int device = 0;
+  int elem_words = 1;
+  uint32_t n = 0;
+  uint64_t* d_data = nullptr;    // elements (elem_words u64 each)
+  uint64_t* d_starts = nullptr;  // [n] element index of each sketch
+  uint32_t* d_sizes = nullptr;   // [n]
+  std::vector<uint32_t> sizes;
+  std::vector<uint64_t> starts;
+  std::vector<uint64_t> windows;
+  // how the sketches were made (persisted with them)
+  int window = 0;
+  uint64_t mask[2] = {0, 0};
+  sks_policy policy{};
+  std::vector<std::string> names;  // optional, from a sketch file or sks_sketch_set_set_name
+};
 
 namespace sks {
 
@@ -20,6 +39,22 @@ inline uint8_t nucleotide_code(uint8_t ch) {
     default: return 4;
   }
 }
+
+// ---- sketch files (persist.cpp) ----------------------------------------------------
+struct SketchFileMeta {
+  int window = 0;
+  int elem_words = 1;
+  uint64_t mask[2] = {0, 0};
+  sks_policy policy{};
+};
+// Writes / reads the format documented in persist.cpp.  `data` holds the
+// sketches back to back (sizes[i] * elem_words words each); names may be empty.
+int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::vector<uint32_t>& sizes,
+                      const std::vector<uint64_t>& windows, const uint64_t* data,
+                      const std::vector<std::string>& names);
+int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
+                     std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
+                     std::vector<std::string>& names);
 
 void parse_fasta_bytes(const uint8_t* data, uint64_t n, sks_fasta* out);
 

@@ -30,6 +30,11 @@ class Policy(C.Structure):
                 ("nonce", C.c_int64)]
 
 
+class SketchInfo(C.Structure):
+    _fields_ = [("window", C.c_int32), ("elem_words", C.c_int32), ("mask", C.c_uint64 * 2),
+                ("policy", Policy), ("n", C.c_uint32), ("has_names", C.c_int32)]
+
+
 class Timings(C.Structure):
     _fields_ = [("scan_ms", C.c_float), ("post_ms", C.c_float), ("total_ms", C.c_float),
                 ("windows", C.c_uint64), ("scan_launches", C.c_uint64),
@@ -50,7 +55,8 @@ EXPORTED = [
     "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_fasta_parse_device",
     "sks_ctx_last_ingress_ms", "sks_kmer_list_build", "sks_kmer_list_free", "sks_kmer_list_total",
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
-    "sks_kmer_list_copy",
+    "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
+    "sks_sketch_set_name", "sks_sketch_set_save", "sks_sketch_set_load", "sks_sketch_set_concat",
 ]
 
 _lib = None
@@ -94,6 +100,14 @@ def lib():
     L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.sks_ctx_device.argtypes = [vp]
+    L.sks_sketch_set_info.argtypes = [vp, C.POINTER(SketchInfo)]
+    L.sks_sketch_set_set_names.argtypes = [vp, vp]
+    L.sks_sketch_set_name.argtypes = [vp, C.c_uint32]
+    L.sks_sketch_set_name.restype = C.c_char_p
+    L.sks_sketch_set_save.argtypes = [vp, C.c_char_p]
+    L.sks_sketch_set_load.argtypes = [vp, C.c_char_p, C.POINTER(vp)]
+    L.sks_sketch_set_concat.argtypes = [vp, vp, C.c_uint32, C.POINTER(vp)]
     L.sks_kmer_list_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
                                       C.POINTER(Policy), C.POINTER(vp)]
     L.sks_kmer_list_free.argtypes = [vp]
@@ -318,6 +332,17 @@ class Context:
             lib().sks_kmer_list_free(h)
         return pos[:n], bits[:4 * n].reshape(n, 4), counts[:len(seg) - 1]
 
+    def load_sketches(self, path):
+        h = C.c_void_p()
+        check(lib().sks_sketch_set_load(self.h, str(path).encode(), C.byref(h)))
+        return SketchSet(h)
+
+    def concat(self, sets):
+        arr = (C.c_void_p * len(sets))(*[s.h for s in sets])
+        h = C.c_void_p()
+        check(lib().sks_sketch_set_concat(self.h, arr, len(sets), C.byref(h)))
+        return SketchSet(h)
+
     def intersect_pairs(self, data_ptr, starts_ptr, sizes_ptr, elem_words, a_ptr, b_ptr,
                         n_pairs, out_ptr):
         check(lib().sks_intersect_pairs(self.h, data_ptr, starts_ptr, sizes_ptr, elem_words,
@@ -354,6 +379,33 @@ class SketchSet:
             self.free()
         except Exception:
             pass
+
+    def info(self):
+        i = SketchInfo()
+        check(lib().sks_sketch_set_info(self.h, C.byref(i)))
+        return {"window": i.window, "elem_words": i.elem_words,
+                "mask": int(i.mask[0]) | int(i.mask[1]) << 64, "kind": i.policy.kind,
+                "flavour": i.policy.flavour, "param": i.policy.param, "nonce": i.policy.nonce,
+                "n": i.n, "has_names": bool(i.has_names)}
+
+    def set_names(self, names):
+        if names is None:
+            check(lib().sks_sketch_set_set_names(self.h, None))
+            return
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        check(lib().sks_sketch_set_set_names(self.h, arr))
+
+    def names(self):
+        out = []
+        for i in range(self.n):
+            v = lib().sks_sketch_set_name(self.h, i)
+            if v is None:
+                return None
+            out.append(v.decode())
+        return out
+
+    def save(self, path):
+        check(lib().sks_sketch_set_save(self.h, str(path).encode()))
 
     def sizes(self):
         out = np.zeros(max(self.n, 1), dtype=np.uint32)

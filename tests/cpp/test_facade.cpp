@@ -3,6 +3,7 @@
 //   test_facade sketch <w> <k> <mask_seed> <c|s> <frac|bottom> <file>...
 //   test_facade errors
 //   test_facade missing <file>
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -15,6 +16,7 @@
 #include "fasta_processing.hpp"
 #include "generators.hpp"
 #include "kmer.hpp"
+#include "sketch_io.hpp"
 #include "sweep.hpp"
 
 static void hexset(const kmer_set& ks) {
@@ -145,6 +147,57 @@ static int list(char** argv) {
   return 0;
 }
 
+// test_facade store <path> <window>: save three host sets, load them back;
+// prints the elements (hex lo hi per line, sets separated by "--").
+// test_facade load <path>: load and print the same way (errors -> exit 3).
+static void print_sets(const std::vector<kmer_set>& sets, const std::vector<std::string>& names) {
+  for (size_t i = 0; i < sets.size(); ++i) {
+    std::printf("-- %s %d\n", names.empty() ? "" : names[i].c_str(), sets[i].window_length);
+    for (const kmer_bitset& e : sets[i].elements)
+      std::printf("%llx %llx\n", (unsigned long long)e.lo(), (unsigned long long)e.hi());
+  }
+}
+
+static int store(char** argv) {
+  const int w = std::atoi(argv[3]);
+  const kmer_bitset mask = generate_random_spaced_seed_mask(w, w > 10 ? w - 5 : w, 0);
+  std::vector<kmer_set> sets(3);
+  uint64_t x = 88172645463325252ull;
+  for (int i = 0; i < 3; ++i) {
+    sets[i].window_length = w;
+    sets[i].mask = mask;
+    sets[i].has_mask = true;
+    std::vector<kmer_bitset> v;
+    for (int j = 0; j < 50 * i; ++j) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      v.push_back(kmer_bitset(x, 0) & mask);
+    }
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    sets[i].elements = v;
+  }
+  sks::save_kmer_sets(argv[2], sets, sketch_policy::frac(200, 1), {"a.fa", "dir/b.fa", "c"});
+  std::vector<std::string> names;
+  sketch_policy pol;
+  auto back = sks::load_kmer_sets(argv[2], &names, &pol);
+  bool same = back.size() == sets.size() && pol.param == 200 && pol.kind == SKS_FRAC_MOD;
+  for (size_t i = 0; same && i < sets.size(); ++i)
+    same = back[i].elements == sets[i].elements && back[i].mask == mask;
+  print_sets(back, names);
+  return same ? 0 : 2;
+}
+
+static int load(char** argv) {
+  try {
+    std::vector<std::string> names;
+    print_sets(sks::load_kmer_sets(argv[2], &names), names);
+  } catch (const std::runtime_error& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return 3;
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 64;
   std::string mode = argv[1];
@@ -152,6 +205,8 @@ int main(int argc, char** argv) {
   if (mode == "errors") return errors();
   if (mode == "csv" && argc >= 8) return csv(argc, argv);
   if (mode == "list" && argc == 7) return list(argv);
+  if (mode == "store" && argc == 4) return store(argv);
+  if (mode == "load" && argc == 3) return load(argv);
   if (mode == "missing" && argc == 3) {
     char* f[1] = {argv[2]};
     kmer_bitset mask = generate_random_spaced_seed_mask(21, 21, 0);

@@ -1,0 +1,177 @@
+"""Persisted sketches (no reference equivalent).
+
+The SKSKETCH format documented in spaced-kmer-sketching_amd/csrc/persist.cpp
+is read here by an independent Python parser, so the layout is pinned by the
+documentation rather than by the C++ code alone.  CPU tests drive the host
+facade (sks::save_kmer_sets / load_kmer_sets) through tests/cpp/test_facade;
+GPU tests round-trip device sets (sks_sketch_set_save / _load / _concat) and
+check that loaded sketches intersect exactly like freshly built ones."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FACADE = os.path.join(ROOT, "tests", "cpp", "build", "test_facade")
+
+
+def fnv1a64(b: bytes) -> int:
+    h = 0xcbf29ce484222325
+    for x in b:
+        h = ((h ^ x) * 0x100000001b3) & (2**64 - 1)
+    return h
+
+
+def parse_sksketch(data: bytes):
+    hdr = struct.unpack_from("<8sIIiiiiQqQQQQQQ", data, 0)
+    magic, ver, ew, w, kind, flav, _r0, param, nonce, mlo, mhi, n, total, nb, _r1 = hdr
+    assert magic == b"SKSKETCH" and ver == 1
+    o = 96
+    sizes = list(struct.unpack_from(f"<{n}I", data, o))
+    o += (n * 4 + 7) & ~7
+    windows = list(struct.unpack_from(f"<{n}Q", data, o))
+    o += 8 * n
+    words = np.frombuffer(data, dtype="<u8", count=total * ew, offset=o)
+    o += 8 * total * ew
+    names = data[o:o + nb].split(b"\0")[:-1] if nb else []
+    o += nb
+    (chk,) = struct.unpack_from("<Q", data, o)
+    assert o + 8 == len(data)
+    assert chk == fnv1a64(data[:o])
+    sk, e = [], 0
+    for s in sizes:
+        sk.append(words[e * ew:(e + s) * ew].reshape(s, ew))
+        e += s
+    return dict(window=w, elem_words=ew, kind=kind, flavour=flav, param=param, nonce=nonce,
+                mask=mlo | mhi << 64, sizes=sizes, windows=windows, sketches=sk,
+                names=[x.decode() for x in names])
+
+
+@pytest.fixture(scope="module")
+def facade_bin():
+    if not os.path.exists(FACADE):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+    return FACADE
+
+
+def _printed_sets(text):
+    sets = []
+    for line in text.splitlines():
+        if line.startswith("--"):
+            sets.append([])
+        else:
+            lo, hi = line.split()
+            sets[-1].append(int(lo, 16) | int(hi, 16) << 64)
+    return sets
+
+
+@pytest.mark.parametrize("w", [21, 40])
+def test_host_store_roundtrip_and_layout(facade_bin, tmp_path, w):
+    path = tmp_path / "s.sks"
+    r = subprocess.run([facade_bin, "store", str(path), str(w)], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    f = parse_sksketch(path.read_bytes())
+    assert f["window"] == w and f["elem_words"] == (2 if w > 32 else 1)
+    assert f["names"] == ["a.fa", "dir/b.fa", "c"]
+    assert (f["kind"], f["param"], f["nonce"]) == (0, 200, 1)
+    assert f["mask"] == O.mask(w, w - 5, 0)
+    printed = _printed_sets(r.stdout)
+    for sk, want in zip(f["sketches"], printed):
+        vals = [int(row[0]) | (int(row[1]) << 64 if f["elem_words"] == 2 else 0) for row in sk]
+        assert vals == want
+        assert vals == sorted(set(vals))
+
+
+def test_host_load_rejects_damage(facade_bin, tmp_path):
+    path = tmp_path / "s.sks"
+    subprocess.run([facade_bin, "store", str(path), "21"], check=True, capture_output=True, timeout=60)
+    good = path.read_bytes()
+    cases = {
+        "checksum": good[:200] + bytes([good[200] ^ 1]) + good[201:],
+        "length": good[:-9],
+        "not a sketch file": b"XX" + good[2:],
+        "unsupported version": good[:8] + b"\x07" + good[9:],
+    }
+    for msg, data in cases.items():
+        bad = tmp_path / "bad.sks"
+        bad.write_bytes(data)
+        r = subprocess.run([facade_bin, "load", str(bad)], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 3 and msg in r.stderr, (msg, r.stderr)
+    r = subprocess.run([facade_bin, "load", str(tmp_path / "missing.sks")], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 3 and "cannot open" in r.stderr
+
+
+# ---------------------------------------------------------------- GPU ------
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    import sksffi
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    c = sksffi.Context(0)
+    yield torch, c
+    c.close()
+
+
+def _build(torch, ctx, genomes, w, m, kind, param):
+    import sksffi
+    stream = b"".join(g + b"\n" for g in genomes)
+    offs = [0]
+    for g in genomes:
+        offs.append(offs[-1] + len(g) + 1)
+    d = torch.frombuffer(bytearray(stream), dtype=torch.uint8).to("cuda:0")
+    k = sksffi.SKS_FRAC_MOD if kind == "frac" else sksffi.SKS_BOTTOM_S
+    return ctx.sketch_build(d.data_ptr(), len(stream), offs, w, m, k, param)
+
+
+def _all_pairs(torch, ctx, ss):
+    n = ss.n
+    out = torch.zeros((n, n), dtype=torch.int32, device="cuda:0")
+    data, starts, sizes = ss.device_ptrs()
+    ctx.intersect_all(data, starts, sizes, ss.elem_words, n, 0, n, out.data_ptr())
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,k,kind,param", [(31, 21, "frac", 50), (31, 21, "bottom", 300),
+                                            (45, 30, "frac", 20)])
+def test_device_save_load_concat(gpu, tmp_path, w, k, kind, param):
+    torch, ctx = gpu
+    genomes = [synth.bases(20000, seed=5, mut_seed=40 + i, mut_rate=0.01 * i).tobytes()
+               for i in range(6)]
+    m = O.mask(w, k, 2)
+    ss = _build(torch, ctx, genomes, w, m, kind, param)
+    names = [f"g{i}.fa" for i in range(6)]
+    ss.set_names(names)
+    path = tmp_path / "s.sks"
+    ss.save(path)
+    f = parse_sksketch(path.read_bytes())
+    assert f["names"] == names and f["mask"] == m and f["window"] == w
+    assert f["param"] == param and f["kind"] == (0 if kind == "frac" else 1)
+    assert f["windows"] == [int(x) for x in ss.windows()]
+    back = ctx.load_sketches(path)
+    assert back.names() == names
+    assert back.info() == ss.info()
+    for i in range(6):
+        assert np.array_equal(back.sketch(i), ss.sketch(i))
+    assert np.array_equal(_all_pairs(torch, ctx, back), _all_pairs(torch, ctx, ss))
+    # shards built separately and concatenated == one build over all genomes
+    a = _build(torch, ctx, genomes[:2], w, m, kind, param)
+    b = _build(torch, ctx, genomes[2:], w, m, kind, param)
+    cat = ctx.concat([a, b])
+    assert cat.n == 6
+    for i in range(6):
+        assert np.array_equal(cat.sketch(i), ss.sketch(i))
+    assert np.array_equal(_all_pairs(torch, ctx, cat), _all_pairs(torch, ctx, ss))
+    other = _build(torch, ctx, genomes[:1], w, O.mask(w, k, 3), kind, param)
+    import sksffi
+    with pytest.raises(sksffi.SksError):
+        ctx.concat([a, other])
