@@ -46,6 +46,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 W, K, MASK_SEED = 31, 21, 0
 C3_CONTIGS, C3_CONTIG_LEN, C3_NRUN, C3_NRUN_LEN, C3_FRAC = 24, 125_000_000, 4, 10_000, 1000
 C4_GENOMES, C4_LEN, C4_ANCESTORS, C4_S = 1000, 5_000_000, 10, 10000
+C5_GENOMES, C5_SEEDS = 200, 8  # first 200 genomes of config 4, mask seeds 0..7
 
 
 def log(*a):
@@ -236,6 +237,73 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
     }
 
 
+# ---- config 5 ------------------------------------------------------------------------
+def run_seed_sweep(ctx, world, rank, steps, warmup):
+    """Config 5: 8 spaced seeds (w=31/k=21, mask seeds 0..7) over the first 200
+    genomes of config 4, bottom-s s=10000; per seed: sketch all genomes, count
+    all 200 x 200 ordered pairs (symmetric tiles), containment + ANI on the host
+    (bit-exact doubles, kmer-sketching.cpp:195-200); consensus = mean ANI over
+    the seeds.  Ranks shard seeds (sks_dist.seed_sweep); one all-reduce of the
+    ANI sums.  A step is the whole sweep, consensus included."""
+    import sks_dist
+    n = C5_GENOMES
+    seg = [0]
+    for _ in range(n):
+        seg.append(seg[-1] + C4_LEN + 1)
+    buf = torch.empty(seg[-1], dtype=torch.uint8, device="cuda")
+    for g in range(n):
+        anc_seed, mut_seed, rate = c4_genome_seeds(g)
+        ctx.synth_bases(buf.data_ptr() + seg[g], C4_LEN, anc_seed, mut_seed, rate)
+        buf[seg[g] + C4_LEN] = ord("\n")
+    torch.cuda.synchronize()
+    masks = [sksffi.mask_generate(W, K, s) for s in range(C5_SEEDS)]
+    ones = [bin(m).count("1") // 2 for m in masks]
+    padded = torch.full((n, C4_S), -1, dtype=torch.int64, device="cuda")
+    sizes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    starts = torch.arange(n, dtype=torch.int64, device="cuda") * C4_S
+    mat = torch.empty((n, n), dtype=torch.int32, device="cuda")
+    n_tiles = sksffi.intersect_sym_tiles(n)
+    dev = "cuda" if world > 1 and os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
+
+    def ani_for_seed(s):
+        ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, masks[s], sksffi.SKS_BOTTOM_S, C4_S)
+        ss.export(padded.data_ptr(), C4_S, sizes.data_ptr())
+        ctx.intersect_sym(padded.data_ptr(), starts.data_ptr(), sizes.data_ptr(), 1, n, 0,
+                          n_tiles, mat.data_ptr())
+        counts = mat.cpu().numpy()
+        del ss
+        size_first = np.repeat(np.diag(counts).astype(np.int32), n)
+        _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones[s])
+        return torch.from_numpy(ani.reshape(n, n))
+
+    total = 0.0
+    timed = 0
+    for it in range(warmup + steps):
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        cons, mine = sks_dist.seed_sweep(C5_SEEDS, world, rank, ani_for_seed, n, device=dev)
+        cons = cons.cpu()
+        dt = max_over_ranks(time.perf_counter() - t0, world)
+        if it >= warmup:
+            total += dt
+            timed += 1
+    t = total / max(timed, 1)
+    c = cons.numpy()
+    return {
+        "metric": "seed-sweep genome-pairs ANI/s", "value": C5_SEEDS * n * n / t,
+        "unit": "ordered (pair, seed) ANIs/s", "scaling": "strong", "ms_per_sweep": t * 1e3,
+        "sketch_kmers_per_s": C5_SEEDS * n * (C4_LEN - W + 1) / t,
+        "consensus_ani_mean": float(c.mean()),
+        "consensus_ani_offdiag_min": float((c + np.eye(n) * 2).min()),
+        "config": {"workload": "config5 seed sweep", "genomes": n, "genome_len": C4_LEN,
+                   "seeds": C5_SEEDS, "s": C4_S, "w": W, "k": K,
+                   "sharding": "seeds over ranks", "consensus": "mean ANI over seeds",
+                   "collective": ("all_reduce of ANI sums (RCCL)" if world > 1 and dev == "cuda"
+                                  else ("all_reduce (gloo)" if world > 1 else "none"))},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -244,6 +312,7 @@ def main():
     ap.add_argument("--cpu-sample-mb", type=int, default=60)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pairs", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"))
     args = ap.parse_args()
@@ -296,6 +365,10 @@ def main():
         pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 3)),
                           warmup=1)
 
+    sweep = None
+    if not args.no_sweep:
+        sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_c3(mask, args.cpu_sample_mb * 1_000_000)
@@ -317,6 +390,7 @@ def main():
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "pairs": pairs,
+            "seed_sweep": sweep,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -243,6 +243,16 @@ int sks_ctx_last_ingress_ms(sks_ctx* ctx, float* ms);
 int sks_ctx_last_intersect_ms(sks_ctx* ctx, float* ms);
 /* Fix the scan kernel's persistent grid size (0 = derive from occupancy). */
 int sks_ctx_set_scan_grid(sks_ctx* ctx, int grid);
+/* Kernel used by sks_intersect_all / sks_intersect_sym for u64 sketches.  All
+ * give identical counts; AUTO (default) = the LDS hash join when the bucket
+ * sizes allow it, else the LDS merge tiles, else one wavefront per pair. */
+enum {
+  SKS_INTERSECT_AUTO = 0,
+  SKS_INTERSECT_MERGE = 1,  /* 64x64 tiles of pairwise LDS merges */
+  SKS_INTERSECT_JOIN = 2,   /* 64x64 tiles, LDS hash join of the two blocks */
+  SKS_INTERSECT_GLOBAL = 3  /* one wavefront per pair, straight from HBM */
+};
+int sks_ctx_set_intersect_kernel(sks_ctx* ctx, int kind);
 
 /* ---- synthetic genomes (bench / test utility; no reference equivalent) ----------------- */
 /* Fills d_out[0..n) with ACGT bytes: base(p) = splitmix64(seed ^ (p * golden)) >> 62;

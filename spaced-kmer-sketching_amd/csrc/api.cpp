@@ -54,6 +54,7 @@ struct sks_ctx {
   std::vector<uint64_t> meta_host;  // staging for `meta`
   sks_timings last{};
   int grid_override = 0;
+  int intersect_algo = 0;  // sks::kIntersect*
 };
 
 struct sks_kmer_list {
@@ -283,6 +284,14 @@ int sks_ctx_last_timings(const sks_ctx* c, sks_timings* out) {
 int sks_ctx_set_scan_grid(sks_ctx* c, int grid) {
   if (!c) return sks::fail(SKS_E_ARG, "null ctx");
   c->grid_override = grid;
+  return SKS_OK;
+}
+
+int sks_ctx_set_intersect_kernel(sks_ctx* c, int kind) {
+  if (!c) return sks::fail(SKS_E_ARG, "null ctx");
+  if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_GLOBAL)
+    return sks::fail(SKS_E_ARG, "sks_ctx_set_intersect_kernel: unknown kernel");
+  c->intersect_algo = kind;
   return SKS_OK;
 }
 
@@ -953,9 +962,9 @@ int sks_intersect_all(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   DeviceGuard g(c->device);
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   bool done = false;
-  if (elem_words == 1)
+  if (elem_words == 1 && c->intersect_algo != sks::kIntersectGlobal)
     SKS_HIP(sks::launch_intersect_tiled(d_data, d_starts, d_sizes, n, false, row_begin, row_end, 0, 0,
-                                        d_out, c->iwork, c->stream, &done));
+                                        d_out, c->iwork, c->stream, &done, c->intersect_algo));
   if (!done)
     SKS_HIP(sks::launch_intersect_all_global(d_data, d_starts, d_sizes, elem_words, n, row_begin,
                                              row_end, d_out, c->stream));
@@ -976,9 +985,10 @@ int sks_intersect_sym(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   const uint64_t all = sks::intersect_sym_tiles(n);
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   bool done = false;
-  if (elem_words == 1)
+  if (elem_words == 1 && c->intersect_algo != sks::kIntersectGlobal)
     SKS_HIP(sks::launch_intersect_tiled(d_data, d_starts, d_sizes, n, true, 0, n, tile_begin,
-                                        tile_end, d_out, c->iwork, c->stream, &done));
+                                        tile_end, d_out, c->iwork, c->stream, &done,
+                                        c->intersect_algo));
   if (!done) {
     if (tile_begin != 0 || tile_end < all)
       return sks::fail(SKS_E_UNSUPPORTED,

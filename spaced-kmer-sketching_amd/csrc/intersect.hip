@@ -315,6 +315,164 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
   }
 }
 
+
+// ---- join all-pairs kernel (u64 sketches) ----------------------------------------------
+//
+// Same tiles and buckets as k_tiles, but instead of merging 64 x 64 pairs a
+// workgroup joins the two blocks: per bucket, the 64 column parts go into an
+// LDS hash table value -> 64-bit mask of the columns holding it, and every
+// row element probes it once; a hit with mask m adds 1 to cnt[row][c] for each
+// set bit c (ds_add in an LDS 64 x 65 matrix).  Work per tile is
+// (row elements + column elements) + Σ_pairs |S_i ∩ S_j| instead of
+// Σ_pairs (|S_i| + |S_j|) — 64x fewer steps for unrelated sketches and still
+// fewer when every pair is identical.  Lane l of every wave owns row l, so the
+// ds_adds of one instruction hit 64 different rows (stride 65: distinct banks
+// for equal columns).
+constexpr int kJSlots = 2048;               // hash slots (load <= 1/2, see host)
+constexpr int kJLog = 11;
+constexpr int kJMaxPart = 32;               // largest part a join launch accepts
+constexpr int kJMaxCol = kJSlots / 2;       // largest column-block bucket population
+constexpr int kJPer = kJMaxPart / kWavesPerBlock;  // elements per thread per part (8)
+constexpr int kCntLd = kTile + 1;
+constexpr uint64_t kEmpty = ~0ull;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t join_hash(uint64_t v) {
+  return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x9E3779B1u) >> (32 - kJLog);
+}
+
+__global__ __launch_bounds__(kB) void k_join(TileArgs a) {
+  __shared__ uint64_t s_key[kJSlots];
+  __shared__ uint64_t s_msk[kJSlots];
+  __shared__ uint64_t s_row[kJMaxPart * kTile];
+  __shared__ uint32_t s_cnt[kTile * kCntLd];
+  __shared__ uint32_t s_len[kTile];
+  __shared__ unsigned long long s_special;  // columns holding the value ~0 (== kEmpty)
+
+  const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
+  const uint32_t grp = blockIdx.x % a.n_groups;
+  uint32_t I, J;
+  if (a.sym) {
+    sym_tile(t, a.n_col_blocks, I, J);
+  } else {
+    I = (uint32_t)(t / a.n_col_blocks);
+    J = (uint32_t)(t % a.n_col_blocks);
+  }
+  const uint32_t row0 = (a.sym ? 0 : a.row_begin) + I * kTile;
+  const uint32_t row_lim = a.sym ? a.n : a.row_end;
+  const uint32_t col0 = J * kTile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  for (int i = tid; i < kJSlots; i += kB) {
+    s_key[i] = kEmpty;
+    s_msk[i] = 0;
+  }
+  for (int i = tid; i < kTile * kCntLd; i += kB) s_cnt[i] = 0;
+  if (tid == 0) s_special = 0;
+
+  // lane = sketch slot within the block (row `lane` and column `lane`)
+  const uint32_t rid = row0 + lane, cid = col0 + lane;
+  const bool rv = rid < row_lim, cv = cid < a.n;
+  const uint64_t rstart = rv ? a.starts[rid] : 0, cstart = cv ? a.starts[cid] : 0;
+  const uint32_t* rpos = a.pos + (uint64_t)(rv ? rid : 0) * (a.B + 1);
+  const uint32_t* cpos = a.pos + (uint64_t)(cv ? cid : 0) * (a.B + 1);
+  const unsigned long long cbit = 1ull << lane;
+
+  const uint32_t b0 = grp * a.buckets_per_group;
+  const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
+  __syncthreads();
+  for (uint32_t b = b0; b < b1; ++b) {
+    // 1) stage the row parts (lds[pos][row]) and insert the column parts
+    uint32_t rbeg = 0, rlen = 0, cbeg = 0, clen = 0;
+    if (rv) { rbeg = rpos[b]; rlen = rpos[b + 1] - rbeg; }
+    if (cv) { cbeg = cpos[b]; clen = cpos[b + 1] - cbeg; }
+    if (wave == 0) s_len[lane] = rlen;
+    uint64_t rvals[kJPer], cvals[kJPer];
+#pragma unroll
+    for (int u = 0; u < kJPer; ++u) {
+      const uint32_t e = wave + kWavesPerBlock * u;
+      rvals[u] = e < rlen ? a.data[rstart + rbeg + e] : 0;
+      cvals[u] = e < clen ? a.data[cstart + cbeg + e] : 0;
+    }
+    uint32_t made[kJPer];
+#pragma unroll
+    for (int u = 0; u < kJPer; ++u) {
+      const uint32_t e = wave + kWavesPerBlock * u;
+      made[u] = kNoSlot;
+      if (e < rlen) s_row[e * kTile + lane] = rvals[u];
+      if (e < clen) {
+        const uint64_t v = cvals[u];
+        if (v == kEmpty) {
+          atomicOr(&s_special, cbit);
+        } else {
+          uint32_t h = join_hash(v);
+          for (;;) {
+            const unsigned long long prev = atomicCAS(
+                reinterpret_cast<unsigned long long*>(&s_key[h]), (unsigned long long)kEmpty,
+                (unsigned long long)v);
+            if (prev == kEmpty || prev == v) {
+              if (prev == kEmpty) made[u] = h;
+              atomicOr(reinterpret_cast<unsigned long long*>(&s_msk[h]), cbit);
+              break;
+            }
+            h = (h + 1) & (kJSlots - 1);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // 2) probe: lane = row, this wave takes positions wave, wave + 4, ...
+    const uint32_t nrow = s_len[lane];
+    const unsigned long long special = s_special;
+#pragma unroll
+    for (int u = 0; u < kJPer; ++u) {
+      const uint32_t e = wave + kWavesPerBlock * u;
+      if (e < nrow) {
+        const uint64_t v = s_row[e * kTile + lane];
+        unsigned long long m = 0;
+        if (v == kEmpty) {
+          m = special;
+        } else {
+          uint32_t h = join_hash(v);
+          for (;;) {
+            const uint64_t k = s_key[h];
+            if (k == v) { m = s_msk[h]; break; }
+            if (k == kEmpty) break;
+            h = (h + 1) & (kJSlots - 1);
+          }
+        }
+        while (m) {
+          const uint32_t c = (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          atomicAdd(&s_cnt[lane * kCntLd + c], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    // 3) reset the slots this thread created (and the ~0 mask)
+#pragma unroll
+    for (int u = 0; u < kJPer; ++u) {
+      if (made[u] != kNoSlot) {
+        s_key[made[u]] = kEmpty;
+        s_msk[made[u]] = 0;
+      }
+    }
+    if (tid == 0) s_special = 0;
+    __syncthreads();
+  }
+  // counts -> global (one atomic per nonzero pair; both halves for sym off-diagonal)
+  for (int i = tid; i < kTile * kTile; i += kB) {
+    const uint32_t r = i >> 6, c = i & 63;
+    const uint32_t cnt = s_cnt[r * kCntLd + c];
+    if (!cnt) continue;
+    const uint32_t gr = row0 + r, gc = col0 + c;
+    if (gr >= row_lim || gc >= a.n) continue;
+    const uint64_t orow = a.sym ? gr : (gr - a.row_begin);
+    atomicAdd(&a.out[orow * a.ld + gc], (int32_t)cnt);
+    if (a.sym && I != J) atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
@@ -357,7 +515,7 @@ namespace sks {
 hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                                   uint32_t n, bool sym, uint32_t row_begin, uint32_t row_end,
                                   uint64_t tile_begin, uint64_t tile_end, int32_t* out,
-                                  Scratch& work, hipStream_t s, bool* used_tiles) {
+                                  Scratch& work, hipStream_t s, bool* used_tiles, int algo) {
   *used_tiles = false;
   hipError_t e;
   const uint64_t out_words = sym ? (uint64_t)n * n : (uint64_t)(row_end - row_begin) * n;
@@ -376,6 +534,8 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   while ((uint64_t)B * 32 < max_size) B <<= 1;  // mean part <= 32 elements
   std::vector<uint32_t> h_pos;
   uint32_t P = 0;
+  bool use_join = false;
+  const uint32_t n_cb = (n + kTile - 1) / kTile;
   for (;;) {
     size_t bytes = sizeof(uint64_t) * (B + 1) + sizeof(uint32_t) * (uint64_t)n * (B + 1) + 64;
     if ((e = work.reserve(bytes)) != hipSuccess) return e;
@@ -394,9 +554,25 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     for (uint32_t i = 0; i < n; ++i)
       for (uint32_t b = 0; b < B; ++b)
         P = std::max(P, h_pos[(uint64_t)i * (B + 1) + b + 1] - h_pos[(uint64_t)i * (B + 1) + b]);
-    if (P <= (uint32_t)kGoodPart) break;
-    if (B >= (1u << 16) || (uint64_t)B * 8 > max_size) {
-      if (P <= (uint32_t)kMaxPart) break;
+    if (algo != kIntersectMerge && P <= (uint32_t)kJMaxPart) {
+      // largest bucket population of one 64-sketch column block (hash-table load)
+      uint32_t colmax = 0;
+      std::vector<uint32_t> acc(B);
+      for (uint32_t cb = 0; cb < n_cb && colmax <= (uint32_t)kJMaxCol; ++cb) {
+        std::fill(acc.begin(), acc.end(), 0u);
+        for (uint32_t i = cb * kTile; i < std::min(n, cb * kTile + kTile); ++i) {
+          const uint32_t* q = &h_pos[(uint64_t)i * (B + 1)];
+          for (uint32_t b = 0; b < B; ++b) acc[b] += q[b + 1] - q[b];
+        }
+        for (uint32_t b = 0; b < B; ++b) colmax = std::max(colmax, acc[b]);
+      }
+      if (colmax <= (uint32_t)kJMaxCol) { use_join = true; break; }
+    }
+    if (algo == kIntersectMerge && P <= (uint32_t)kGoodPart) break;
+    const bool grow = B < (1u << 16) &&
+                      (uint64_t)B * (algo == kIntersectMerge ? 8 : 2) <= max_size;
+    if (!grow) {
+      if (P <= (uint32_t)kMaxPart) break;  // merge tiles
       return hipSuccess;  // pathological skew: caller falls back to the global kernel
     }
     B <<= 1;
@@ -426,6 +602,12 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   a.tile_begin = tile_begin;
   a.out = out;
   a.ld = n;
+  if (use_join) {
+    hipLaunchKernelGGL(k_join, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), 0, s, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    *used_tiles = true;
+    return hipSuccess;
+  }
   const size_t lds_bytes = (size_t)std::max<uint32_t>(P, 1) * kSlots * sizeof(uint64_t) +
                            kSlots * sizeof(uint32_t);
   static const hipError_t attr = hipFuncSetAttribute(

@@ -101,7 +101,12 @@ hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* sta
 hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                                   uint32_t n, bool sym, uint32_t row_begin, uint32_t row_end,
                                   uint64_t tile_begin, uint64_t tile_end, int32_t* out,
-                                  Scratch& work, hipStream_t s, bool* used_tiles);
+                                  Scratch& work, hipStream_t s, bool* used_tiles, int algo);
+// intersection kernel choice (sks_ctx_set_intersect_kernel)
+constexpr int kIntersectAuto = 0;    // join when the bucket sizes allow, else merge tiles
+constexpr int kIntersectMerge = 1;   // k_tiles (pairwise LDS merges)
+constexpr int kIntersectJoin = 2;    // k_join (LDS hash join), merge tiles if infeasible
+constexpr int kIntersectGlobal = 3;  // one wavefront per pair from global memory
 uint64_t intersect_sym_tiles(uint32_t n);
 
 // ---- device FASTA ingress (ingress.hip) -------------------------------------------------

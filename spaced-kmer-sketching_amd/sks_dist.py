@@ -86,3 +86,30 @@ def all_vs_all(local, local_sizes, n_genomes, world, rank, count_sym, out=None):
     if world > 1:
         sum_matrix(out)
     return out
+
+
+# ---- seed sweep (BASELINE config 5) ----------------------------------------------------
+# The reference sweeps (w, k) configurations serially, re-sketching every file
+# per configuration (kmer-sketching.cpp:214-239 around :151-212).  Config 5 runs
+# several spaced seeds over one genome collection; seeds are independent, so
+# ranks shard by seed (rank r takes seeds r, r + world, ...), each rank keeps
+# the whole collection resident, sketches it and computes its own all-vs-all
+# matrix per seed.  The only exchange is the consensus: one all-reduce (sum)
+# of the per-seed ANI matrices, divided by the number of seeds.
+
+def seed_shard(n_seeds, world, rank):
+    return list(range(rank, n_seeds, world))
+
+
+def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
+    """ani_for_seed(seed_index) -> [n_genomes, n_genomes] float64 tensor (row i =
+    first set of the pair, as kmer-sketching.cpp:195-200).  Returns (consensus,
+    local_seeds): the mean over all seeds of the ANI matrices, on every rank."""
+    acc = torch.zeros((n_genomes, n_genomes), dtype=torch.float64, device=device)
+    mine = seed_shard(n_seeds, world, rank)
+    for s in mine:
+        acc += ani_for_seed(s).to(device)
+    if world > 1:
+        sum_matrix(acc)
+    acc /= n_seeds
+    return acc, mine

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("SKS_LIB") or os.path.join(PKG_DIR, "lib", "libsks.so"
 
 SKS_FRAC_MOD = 0
 SKS_BOTTOM_S = 1
+INTERSECT_AUTO, INTERSECT_MERGE, INTERSECT_JOIN, INTERSECT_GLOBAL = 0, 1, 2, 3
 FLAVOUR_BOOST_MIX = 0
 FLAVOUR_BOOST_LEGACY = 1
 
@@ -52,7 +53,7 @@ EXPORTED = [
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
     "sks_synth_bases", "sks_intersect_sym", "sks_intersect_sym_tiles",
-    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_fasta_parse_device",
+    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_ctx_set_intersect_kernel", "sks_fasta_parse_device",
     "sks_ctx_last_ingress_ms", "sks_kmer_list_build", "sks_kmer_list_free", "sks_kmer_list_total",
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
@@ -98,6 +99,7 @@ def lib():
     L.sks_ctx_synchronize.argtypes = [vp]
     L.sks_ctx_last_timings.argtypes = [vp, C.POINTER(Timings)]
     L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
+    L.sks_ctx_set_intersect_kernel.argtypes = [vp, C.c_int]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_device.argtypes = [vp]
@@ -262,6 +264,11 @@ class Context:
 
     def set_scan_grid(self, grid):
         check(lib().sks_ctx_set_scan_grid(self.h, grid))
+
+    def set_intersect_kernel(self, kind):
+        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL (sks.h); all give identical counts."""
+        check(lib().sks_ctx_set_intersect_kernel(self.h, kind))
+        self._intersect_kernel = kind
 
     def synchronize(self):
         check(lib().sks_ctx_synchronize(self.h))

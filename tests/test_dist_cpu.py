@@ -102,3 +102,57 @@ def test_shard_arithmetic():
         for t in range(T):
             seen.append(sks_dist.sym_tile_coords(t, n))
         assert seen == [(i, j) for i in range(nb) for j in range(i, nb)]
+
+
+# ---- config 5: seed sweep sharded by seed, consensus by all-reduce ------------------
+SWEEP_GENOMES, SWEEP_SEEDS = 12, 5
+
+
+def _sweep_ani(seed_index):
+    """ANI matrix of one mask seed over the sweep collection, oracle-only."""
+    m = O.mask(31, 21, seed_index)
+    k = bin(m).count("1") // 2
+    sk = []
+    for g in range(SWEEP_GENOMES):
+        seq = synth.bases(4000, seed=70 + g % 2, mut_seed=500 + g, mut_rate=0.004 * (g % 6))
+        s, _ = O.sketch(O.cut_runs(seq.tobytes()), 31, m, "bottom", 150)
+        sk.append(s)
+    ani = np.zeros((SWEEP_GENOMES, SWEEP_GENOMES))
+    for i in range(SWEEP_GENOMES):
+        for j in range(SWEEP_GENOMES):
+            ani[i, j] = O.binomial_estimator(O.containment(O.intersect(sk[i], sk[j]), len(sk[i])), k)
+    return torch.from_numpy(ani)
+
+
+def _sweep_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cons, mine = sks_dist.seed_sweep(SWEEP_SEEDS, world, rank, _sweep_ani, SWEEP_GENOMES)
+    q.put((rank, cons.numpy(), mine))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_seed_sweep_gloo_matches_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sweep_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, cons, mine = q.get(timeout=240)
+        results[r] = (cons, mine)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    covered = sorted(s for r in results for s in results[r][1])
+    assert covered == list(range(SWEEP_SEEDS))
+    want = sum(_sweep_ani(s).numpy() for s in range(SWEEP_SEEDS)) / SWEEP_SEEDS
+    for r in range(world):
+        # summation order differs (all-reduce vs sequential): within 1e-12, the
+        # north-star ANI tolerance is 1e-9
+        assert np.allclose(results[r][0], want, rtol=0, atol=1e-12)
+    assert want[0, 0] == 1.0 and 0 < want[0, 2] < 1

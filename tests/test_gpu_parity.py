@@ -253,11 +253,25 @@ def test_argument_errors(torch_cuda, ctx):
         ctx.sketch_build(d.data_ptr(), 9, [0, 10], 4, m, sksffi.SKS_FRAC_MOD, 5)
 
 
-def test_many_sketches_tiled_and_symmetric(torch_cuda, ctx):
+KERNELS = [sksffi.INTERSECT_AUTO, sksffi.INTERSECT_MERGE, sksffi.INTERSECT_JOIN,
+           sksffi.INTERSECT_GLOBAL]
+
+
+@pytest.fixture
+def kernel_ctx(ctx, request):
+    ctx.set_intersect_kernel(request.param)
+    yield ctx
+    ctx.set_intersect_kernel(sksffi.INTERSECT_AUTO)
+
+
+@pytest.mark.parametrize("kernel_ctx", KERNELS, indirect=True)
+def test_many_sketches_tiled_and_symmetric(torch_cuda, kernel_ctx):
     """130 sketches (3 tile blocks, ragged last block) of varied sizes: the
     tiled all-pairs kernel, its row-block form, and the symmetric tile form
-    split across 3 'ranks' and summed, all equal the oracle's merge counts."""
+    split across 3 'ranks' and summed, all equal the oracle's merge counts —
+    for every intersection kernel (join, merge tiles, global)."""
     torch = torch_cuda
+    ctx = kernel_ctx
     n = 130
     genomes = []
     for i in range(n):
@@ -282,9 +296,74 @@ def test_many_sketches_tiled_and_symmetric(torch_cuda, ctx):
     T = sksffi.intersect_sym_tiles(n)
     assert T == 6
     acc = np.zeros((n, n), dtype=np.int64)
-    for (a, b) in [(0, 2), (2, 3), (3, T)]:
+    ranges = [(0, T)] if ctx_kernel(ctx) == sksffi.INTERSECT_GLOBAL else [(0, 2), (2, 3), (3, T)]
+    for (a, b) in ranges:
         part = torch.full((n * n,), 5, dtype=torch.int32, device="cuda:0")
         ctx.intersect_sym(data, starts, sizes, 1, n, a, b, part.data_ptr())
         torch.cuda.synchronize()
         acc += part.cpu().numpy().reshape(n, n)
     assert np.array_equal(acc, want)
+
+
+def ctx_kernel(ctx):
+    return getattr(ctx, "_intersect_kernel", sksffi.INTERSECT_AUTO)
+
+
+def _device_sketch_arrays(torch, sketches):
+    """Packs sorted unique u64 arrays as the CSR (data, starts, sizes) the
+    sks_intersect_* entry points take (any caller-owned device arrays)."""
+    sizes = np.array([len(x) for x in sketches], dtype=np.uint32)
+    starts = np.zeros(len(sketches), dtype=np.uint64)
+    starts[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    flat = np.concatenate([np.asarray(x, dtype=np.uint64) for x in sketches] + [np.zeros(1, np.uint64)])
+    d = torch.from_numpy(flat.view(np.int64)).to("cuda:0")
+    st = torch.from_numpy(starts.view(np.int64)).to("cuda:0")
+    sz = torch.from_numpy(sizes.view(np.int32)).to("cuda:0")
+    return d, st, sz
+
+
+@pytest.mark.parametrize("kernel_ctx", KERNELS, indirect=True)
+@pytest.mark.parametrize("shape", ["families", "identical", "extremes"])
+def test_intersect_kernels_adversarial_arrays(torch_cuda, kernel_ctx, shape):
+    """Caller-provided sorted unique u64 arrays that stress the kernels:
+    heavy sharing (every pair shares most values), all sketches identical
+    (the join's worst case: every probe hits all 64 columns), and the extreme
+    values 0 and 2^64-1 (the join table's empty key) plus runs of values that
+    differ only in their high words.  Counts equal numpy's intersect1d."""
+    torch = torch_cuda
+    ctx = kernel_ctx
+    rng = np.random.default_rng({"families": 1, "identical": 2, "extremes": 3}[shape])
+    n = 150
+    sk = []
+    if shape == "families":
+        base = [np.unique(rng.integers(0, 2**62, size=3000, dtype=np.uint64)) for _ in range(3)]
+        for i in range(n):
+            b = base[i % 3]
+            keep = b[rng.random(b.size) < 0.3 + 0.6 * ((i * 7) % 10) / 10]
+            extra = rng.integers(0, 2**62, size=int(rng.integers(0, 400)), dtype=np.uint64)
+            sk.append(np.unique(np.concatenate([keep, extra])))
+    elif shape == "identical":
+        one = np.unique(rng.integers(0, 2**64 - 1, size=2500, dtype=np.uint64))
+        sk = [one.copy() for _ in range(n)]
+    else:
+        hi = (np.arange(1, 40, dtype=np.uint64) << np.uint64(40))
+        core = np.unique(np.concatenate([
+            np.array([0, 1, 2**64 - 2, 2**64 - 1], dtype=np.uint64), hi,
+            rng.integers(0, 2**64 - 1, size=1500, dtype=np.uint64)]))
+        for i in range(n):
+            sel = core[rng.random(core.size) < 0.5]
+            if i % 4 == 0:
+                sel = np.union1d(sel, np.array([0, 2**64 - 1], dtype=np.uint64))
+            sk.append(sel if i % 37 else np.zeros(0, dtype=np.uint64))
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)]
+                     for i in range(n)])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    out = torch.full((n * n,), -3, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_all(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, n, out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(n, n), want)
+    T = sksffi.intersect_sym_tiles(n)
+    sym = torch.full((n * n,), 9, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_sym(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, T, sym.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(sym.cpu().numpy().reshape(n, n), want)

@@ -1,0 +1,53 @@
+"""A/B of the all-pairs intersection kernels on config 4 (1000 x 5 Mb, bottom-s
+10000) or config 5's 200 genomes: sketches once, then times sks_intersect_sym
+over all tiles per kernel (median of reps) and checks the matrices agree.
+    python tools/bench_pairs.py [n_genomes] [reps]"""
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spaced-kmer-sketching_amd"))
+sys.path.insert(0, ROOT)
+import sksffi  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    ctx = sksffi.Context(0)
+    L = bench.C4_LEN
+    seg = [0]
+    for _ in range(n):
+        seg.append(seg[-1] + L + 1)
+    buf = torch.empty(seg[-1], dtype=torch.uint8, device="cuda")
+    for g in range(n):
+        a, m, r = bench.c4_genome_seeds(g)
+        ctx.synth_bases(buf.data_ptr() + seg[g], L, a, m, r)
+        buf[seg[g] + L] = ord("\n")
+    mask = sksffi.mask_generate(31, 21, 0)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, 31, mask, sksffi.SKS_BOTTOM_S, 10000)
+    data, starts, sizes = ss.device_ptrs()
+    T = sksffi.intersect_sym_tiles(n)
+    ref = None
+    for name, k in (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN)):
+        ctx.set_intersect_kernel(k)
+        out = torch.empty((n, n), dtype=torch.int32, device="cuda")
+        ms = []
+        for _ in range(reps + 1):
+            ctx.intersect_sym(data, starts, sizes, 1, n, 0, T, out.data_ptr())
+            ms.append(ctx.last_intersect_ms())
+        got = out.cpu()
+        if ref is None:
+            ref = got
+        same = bool(torch.equal(ref, got))
+        print(f"{name:6s} n={n} median {statistics.median(ms[1:]):.3f} ms  min {min(ms[1:]):.3f}"
+              f"  equal_to_merge={same}  offdiag_sum={int(got.sum() - got.diag().sum())}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
