@@ -13,8 +13,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <cstdint>
 #include <vector>
+
+#include <rocprim/rocprim.hpp>
 
 #include "sks_internal.hpp"
 
@@ -145,13 +150,31 @@ struct TileArgs {
   uint64_t ld;
 };
 
-__global__ void k_bounds(const uint64_t* __restrict__ data, uint64_t ref_start, uint32_t ref_size,
-                         uint32_t B, uint64_t* __restrict__ bounds) {
+// Common bucket bounds: bounds[b] = mean over K sample sketches (spread over the
+// collection) of each one's b/B quantile.  A single sketch's quantiles are
+// noisy — its wide gaps become buckets that hold several times the mean part
+// of every unrelated sketch — and averaging K of them shrinks that noise by
+// sqrt(K).  Any non-decreasing bounds give exact counts; these only have to
+// balance the parts.  Each quantile sequence is non-decreasing and rounded
+// addition / division are monotonic, so the bounds are too.
+__global__ void k_bounds(const uint64_t* __restrict__ data, const uint64_t* __restrict__ starts,
+                         const uint32_t* __restrict__ sizes, uint32_t n, uint32_t K, uint32_t B,
+                         uint64_t* __restrict__ bounds) {
   uint32_t b = blockIdx.x * kB + threadIdx.x;
   if (b > B) return;
-  if (b == 0) bounds[0] = 0;
-  else if (b == B) bounds[B] = ~0ull;
-  else bounds[b] = data[ref_start + (uint64_t)b * ref_size / B];
+  if (b == 0) { bounds[0] = 0; return; }
+  if (b == B) { bounds[B] = ~0ull; return; }
+  double acc = 0.0;
+  uint32_t used = 0;
+  for (uint32_t k = 0; k < K; ++k) {
+    const uint32_t i = (uint32_t)((uint64_t)k * n / K);
+    const uint32_t sz = sizes[i];
+    if (!sz) continue;
+    acc += (double)data[starts[i] + (uint64_t)b * sz / B];
+    ++used;
+  }
+  const double m = used ? acc / (double)used : 0.0;
+  bounds[b] = m >= 18446744073709549568.0 ? ~0ull : (uint64_t)m;
 }
 
 __global__ void k_bucket_pos(const uint64_t* __restrict__ data, const uint64_t* __restrict__ starts,
@@ -175,6 +198,24 @@ __global__ void k_bucket_pos(const uint64_t* __restrict__ data, const uint64_t* 
     r = lo;
   }
   pos[(uint64_t)i * (B + 1) + b] = r;
+}
+
+// Largest part over all (sketch, bucket), and largest bucket population of one
+// 64-sketch block (the join's hash-table load).  One thread per (block, bucket).
+__global__ void k_part_stats(const uint32_t* __restrict__ pos, uint32_t n, uint32_t B, uint32_t n_cb,
+                             uint32_t* __restrict__ stats) {
+  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (idx >= (uint64_t)n_cb * B) return;
+  const uint32_t cb = (uint32_t)(idx / B), b = (uint32_t)(idx % B);
+  uint32_t mx = 0, sum = 0;
+  for (uint32_t i = cb * 64; i < min(n, cb * 64 + 64); ++i) {
+    const uint32_t* q = pos + (uint64_t)i * (B + 1) + b;
+    const uint32_t part = q[1] - q[0];
+    mx = max(mx, part);
+    sum += part;
+  }
+  atomicMax(&stats[0], mx);
+  atomicMax(&stats[1], sum);
 }
 
 __device__ __forceinline__ void sym_tile(uint64_t t, uint32_t nb, uint32_t& I, uint32_t& J) {
@@ -318,35 +359,145 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 
 // ---- join all-pairs kernel (u64 sketches) ----------------------------------------------
 //
-// Same tiles and buckets as k_tiles, but instead of merging 64 x 64 pairs a
-// workgroup joins the two blocks: per bucket, the 64 column parts go into an
-// LDS hash table value -> 64-bit mask of the columns holding it, and every
-// row element probes it once; a hit with mask m adds 1 to cnt[row][c] for each
-// set bit c (ds_add in an LDS 64 x 65 matrix).  Work per tile is
-// (row elements + column elements) + Σ_pairs |S_i ∩ S_j| instead of
-// Σ_pairs (|S_i| + |S_j|) — 64x fewer steps for unrelated sketches and still
-// fewer when every pair is identical.  Lane l of every wave owns row l, so the
-// ds_adds of one instruction hit 64 different rows (stride 65: distinct banks
-// for equal columns).
-constexpr int kJSlots = 2048;               // hash slots (load <= 1/2, see host)
+// Same 64 x 64 tiles as k_tiles, but a workgroup joins the two blocks instead
+// of merging 4096 pairs: the column block's elements go into an LDS hash table
+// value -> 64-bit mask of the columns holding it, every row element probes it
+// once, and a hit with mask m adds 1 to cnt[row][c] for each set bit c
+// (ds_add into an LDS 64 x 65 matrix).  Work per tile is
+// (row + column elements) + Σ_pairs |S_i ∩ S_j| instead of
+// Σ_pairs (|S_i| + |S_j|): 64x fewer steps for unrelated sketches and still
+// fewer when every pair is identical.
+//
+// Layout (built per call by k_hb_count / scan / k_hb_scatter): elements are
+// hash-bucketed — masked k-mers sit on a lattice (the mask's don't-care bits
+// are 0), so value-range buckets are lumpy, while a hash of the value gives
+// Poisson parts — and stored block-major: for each 64-sketch block, bucket by
+// bucket, sketch by sketch, with the sketch's slot in the block in a u8 id
+// array.  A run of buckets of one block is one contiguous range, so a
+// workgroup streams the column block in coalesced chunks of whole buckets
+// that fit the table (<= kJCap elements) and the row block's same buckets
+// with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
+constexpr int kJSlots = 2048;               // hash slots
 constexpr int kJLog = 11;
-constexpr int kJMaxPart = 32;               // largest part a join launch accepts
-constexpr int kJMaxCol = kJSlots / 2;       // largest column-block bucket population
-constexpr int kJPer = kJMaxPart / kWavesPerBlock;  // elements per thread per part (8)
+constexpr int kJCap = kJSlots / 2;          // column elements per chunk (load <= 1/2)
+constexpr int kJMade = kJCap / kB;          // column elements per thread per chunk (4)
+constexpr int kJWin = 256;                  // bucket offsets staged per window
 constexpr int kCntLd = kTile + 1;
 constexpr uint64_t kEmpty = ~0ull;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
+__device__ __forceinline__ uint32_t bucket_hash(uint64_t v, uint32_t log_b) {
+  return log_b ? (uint32_t)((v * 0x9E3779B97F4A7C15ull) >> (64 - log_b)) : 0u;
+}
 __device__ __forceinline__ uint32_t join_hash(uint64_t v) {
-  return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x9E3779B1u) >> (32 - kJLog);
+  return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x85EBCA77u) >> (32 - kJLog);
 }
 
-__global__ __launch_bounds__(kB) void k_join(TileArgs a) {
-  __shared__ uint64_t s_key[kJSlots];
-  __shared__ uint64_t s_msk[kJSlots];
-  __shared__ uint64_t s_row[kJMaxPart * kTile];
+// One workgroup per sketch i in [first, first + count): per-bucket element
+// counts into counts[(blk * B + b) * 64 + slot], blk/slot of i - base.
+__global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ data,
+                                                 const uint64_t* __restrict__ starts,
+                                                 const uint32_t* __restrict__ sizes,
+                                                 uint32_t first, uint32_t base, uint32_t B,
+                                                 uint32_t log_b, uint32_t* __restrict__ counts) {
+  extern __shared__ uint32_t h[];
+  const uint32_t i = first + blockIdx.x;
+  const uint32_t sz = sizes[i];
+  const uint64_t* src = data + starts[i];
+  for (uint32_t b = threadIdx.x; b < B; b += kB) h[b] = 0;
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < sz; e += kB) atomicAdd(&h[bucket_hash(src[e], log_b)], 1u);
+  __syncthreads();
+  const uint32_t blk = (i - base) >> 6, slot = (i - base) & 63;
+  uint32_t* dst = counts + (uint64_t)blk * B * 64 + slot;
+  for (uint32_t b = threadIdx.x; b < B; b += kB) dst[(uint64_t)b * 64] = h[b];
+}
+
+// Scatter each sketch's elements to its (blk, b, slot) ranges (order inside a
+// range is arbitrary: the join does not need it).
+__global__ __launch_bounds__(kB) void k_hb_scatter(const uint64_t* __restrict__ data,
+                                                   const uint64_t* __restrict__ starts,
+                                                   const uint32_t* __restrict__ sizes,
+                                                   uint32_t first, uint32_t base, uint32_t B,
+                                                   uint32_t log_b, const uint32_t* __restrict__ off,
+                                                   uint64_t* __restrict__ out,
+                                                   uint8_t* __restrict__ ids) {
+  extern __shared__ uint32_t cur[];
+  const uint32_t i = first + blockIdx.x;
+  const uint32_t sz = sizes[i];
+  const uint64_t* src = data + starts[i];
+  const uint32_t blk = (i - base) >> 6, slot = (i - base) & 63;
+  const uint32_t* o = off + (uint64_t)blk * B * 64 + slot;
+  for (uint32_t b = threadIdx.x; b < B; b += kB) cur[b] = o[(uint64_t)b * 64];
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < sz; e += kB) {
+    const uint64_t v = src[e];
+    const uint32_t d = atomicAdd(&cur[bucket_hash(v, log_b)], 1u);
+    out[d] = v;
+    ids[d] = (uint8_t)slot;
+  }
+}
+
+// Largest block-bucket population (one thread per (blk, b)).
+__global__ void k_hb_stats(const uint32_t* __restrict__ off, uint32_t n_blk, uint32_t B,
+                           uint32_t* __restrict__ stat) {
+  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (idx >= (uint64_t)n_blk * B) return;
+  const uint32_t d = off[(idx + 1) * 64] - off[idx * 64];
+  atomicMax(stat, d);
+}
+
+struct JoinArgs {
+  const uint64_t* r_data;
+  const uint8_t* r_ids;
+  const uint32_t* r_off;
+  uint32_t r_blk0;  // row block I of the tile = block r_blk0 + I of the row layout
+  const uint64_t* c_data;
+  const uint8_t* c_ids;
+  const uint32_t* c_off;
+  uint32_t B, n, n_col_blocks, n_groups, buckets_per_group;
+  int sym;
+  uint32_t row_begin, row_end;
+  uint64_t tile_begin;
+  int32_t* out;
+  uint64_t ld;
+  uint32_t cap;  // column elements per chunk (<= kJCap): table load <= cap / kJSlots
+  int dbg;  // timing experiments only (SKS_JOIN_DEBUG): 1 = no table work, 2 = inserts only
+};
+
+// Elements of one chunk held in registers: column elements k = cs + tid + 256u
+// (u < kJMade: a chunk holds <= kJCap) and the first kJRowPf * 256 row elements;
+// the rest of a (rare) larger row range is read in the probe loop.
+constexpr int kJRowPf = 6;
+struct JoinChunk {
+  uint64_t cv[kJMade];
+  uint32_t cid[kJMade];
+  uint64_t rv[kJRowPf];
+  uint32_t rid[kJRowPf];
+};
+
+__device__ __forceinline__ void join_fetch(const JoinArgs& a, uint32_t cs, uint32_t ce, uint32_t rs,
+                                           uint32_t re, int tid, JoinChunk& c) {
+#pragma unroll
+  for (int u = 0; u < kJMade; ++u) {
+    const uint32_t k = cs + tid + kB * u;
+    c.cv[u] = k < ce ? a.c_data[k] : 0;
+    c.cid[u] = k < ce ? a.c_ids[k] : 0xFFu;
+  }
+#pragma unroll
+  for (int u = 0; u < kJRowPf; ++u) {
+    const uint32_t k = rs + tid + kB * u;
+    c.rv[u] = k < re ? a.r_data[k] : 0;
+    c.rid[u] = k < re ? a.r_ids[k] : 0xFFu;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
+  // slot h = {key, mask of columns}: one ds_read_b128 per probe step
+  __shared__ ulonglong2 s_tab[kJSlots];
   __shared__ uint32_t s_cnt[kTile * kCntLd];
-  __shared__ uint32_t s_len[kTile];
+  __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
+  __shared__ uint16_t s_next[kJWin];       // greedy chunk end of a chunk starting at bucket b
   __shared__ unsigned long long s_special;  // columns holding the value ~0 (== kEmpty)
 
   const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
@@ -361,105 +512,157 @@ __global__ __launch_bounds__(kB) void k_join(TileArgs a) {
   const uint32_t row0 = (a.sym ? 0 : a.row_begin) + I * kTile;
   const uint32_t row_lim = a.sym ? a.n : a.row_end;
   const uint32_t col0 = J * kTile;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t* roff = a.r_off + (uint64_t)(a.r_blk0 + I) * a.B * 64;
+  const uint32_t* coff = a.c_off + (uint64_t)J * a.B * 64;
+  const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);  // slots < r_valid are rows
+  unsigned long long* tab = reinterpret_cast<unsigned long long*>(s_tab);  // [2h] key, [2h+1] mask
 
-  for (int i = tid; i < kJSlots; i += kB) {
-    s_key[i] = kEmpty;
-    s_msk[i] = 0;
-  }
+  for (int i = tid; i < kJSlots; i += kB) s_tab[i] = make_ulonglong2(kEmpty, 0ull);
   for (int i = tid; i < kTile * kCntLd; i += kB) s_cnt[i] = 0;
   if (tid == 0) s_special = 0;
 
-  // lane = sketch slot within the block (row `lane` and column `lane`)
-  const uint32_t rid = row0 + lane, cid = col0 + lane;
-  const bool rv = rid < row_lim, cv = cid < a.n;
-  const uint64_t rstart = rv ? a.starts[rid] : 0, cstart = cv ? a.starts[cid] : 0;
-  const uint32_t* rpos = a.pos + (uint64_t)(rv ? rid : 0) * (a.B + 1);
-  const uint32_t* cpos = a.pos + (uint64_t)(cv ? cid : 0) * (a.B + 1);
-  const unsigned long long cbit = 1ull << lane;
+  // a row element's bit loop starts at column `lane`: lanes holding the same
+  // row with similar masks then add to different counters
+  auto add_hits = [&](uint32_t r, unsigned long long m) {
+    m = (m >> lane) | (lane ? m << (64 - lane) : 0ull);
+    uint32_t* crow = &s_cnt[r * kCntLd];
+    while (m) {
+      const uint32_t c = ((uint32_t)__builtin_ctzll(m) + lane) & 63;
+      m &= m - 1;
+      atomicAdd(&crow[c], 1u);
+    }
+  };
 
   const uint32_t b0 = grp * a.buckets_per_group;
   const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
-  __syncthreads();
-  for (uint32_t b = b0; b < b1; ++b) {
-    // 1) stage the row parts (lds[pos][row]) and insert the column parts
-    uint32_t rbeg = 0, rlen = 0, cbeg = 0, clen = 0;
-    if (rv) { rbeg = rpos[b]; rlen = rpos[b + 1] - rbeg; }
-    if (cv) { cbeg = cpos[b]; clen = cpos[b + 1] - cbeg; }
-    if (wave == 0) s_len[lane] = rlen;
-    uint64_t rvals[kJPer], cvals[kJPer];
-#pragma unroll
-    for (int u = 0; u < kJPer; ++u) {
-      const uint32_t e = wave + kWavesPerBlock * u;
-      rvals[u] = e < rlen ? a.data[rstart + rbeg + e] : 0;
-      cvals[u] = e < clen ? a.data[cstart + cbeg + e] : 0;
+  for (uint32_t wb = b0; wb < b1; wb += kJWin) {
+    const uint32_t we = min(b1, wb + kJWin);
+    __syncthreads();  // previous window fully consumed
+    for (uint32_t i = tid; i <= we - wb; i += kB) {
+      s_roff[i] = roff[(uint64_t)(wb + i) * 64];
+      s_coff[i] = coff[(uint64_t)(wb + i) * 64];
     }
-    uint32_t made[kJPer];
+    __syncthreads();
+    // chunk = whole buckets [bs, be) whose column elements fit the table: the
+    // largest be with coff[be] - coff[bs] <= cap (at least bs + 1), found
+    // for every start bucket at once by binary search
+    for (uint32_t i = tid; i < we - wb; i += kB) {
+      const uint32_t cs = s_coff[i];
+      uint32_t lo = i + 1, hi = we - wb;  // answer in [lo, hi]
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_coff[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
+      }
+      s_next[i] = (uint16_t)lo;
+    }
+    __syncthreads();
+    auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
+    uint32_t bs = wb, be = chunk_end(wb);
+    JoinChunk cur;
+    join_fetch(a, s_coff[0], s_coff[be - wb], s_roff[0], s_roff[be - wb], tid, cur);
+    while (bs < we) {
+      const uint32_t cs = s_coff[bs - wb], ce = s_coff[be - wb];
+      const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
+      // prefetch the next chunk's elements while this one is joined
+      const uint32_t nbs = be;
+      const uint32_t nbe = nbs < we ? chunk_end(nbs) : nbs;
+      JoinChunk nxt;
+      if (nbs < we)
+        join_fetch(a, s_coff[nbs - wb], s_coff[nbe - wb], s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
+
+      // 1) insert the column elements: every first CAS in flight together,
+      //    then the collisions walk on
+      uint32_t hs[kJMade];
+      unsigned long long prev[kJMade];
 #pragma unroll
-    for (int u = 0; u < kJPer; ++u) {
-      const uint32_t e = wave + kWavesPerBlock * u;
-      made[u] = kNoSlot;
-      if (e < rlen) s_row[e * kTile + lane] = rvals[u];
-      if (e < clen) {
-        const uint64_t v = cvals[u];
-        if (v == kEmpty) {
-          atomicOr(&s_special, cbit);
-        } else {
-          uint32_t h = join_hash(v);
-          for (;;) {
-            const unsigned long long prev = atomicCAS(
-                reinterpret_cast<unsigned long long*>(&s_key[h]), (unsigned long long)kEmpty,
-                (unsigned long long)v);
-            if (prev == kEmpty || prev == v) {
-              if (prev == kEmpty) made[u] = h;
-              atomicOr(reinterpret_cast<unsigned long long*>(&s_msk[h]), cbit);
-              break;
-            }
-            h = (h + 1) & (kJSlots - 1);
+      for (int u = 0; u < kJMade; ++u) {
+        hs[u] = kNoSlot;
+        if (a.dbg != 1 && cs + tid + kB * u < ce) {
+          const uint64_t v = cur.cv[u];
+          if (v == kEmpty) {
+            atomicOr(&s_special, 1ull << cur.cid[u]);
+          } else {
+            hs[u] = join_hash(v);
+            prev[u] = atomicCAS(&tab[2 * hs[u]], (unsigned long long)kEmpty, (unsigned long long)v);
           }
         }
       }
-    }
-    __syncthreads();
-    // 2) probe: lane = row, this wave takes positions wave, wave + 4, ...
-    const uint32_t nrow = s_len[lane];
-    const unsigned long long special = s_special;
+      uint32_t made[kJMade];
 #pragma unroll
-    for (int u = 0; u < kJPer; ++u) {
-      const uint32_t e = wave + kWavesPerBlock * u;
-      if (e < nrow) {
-        const uint64_t v = s_row[e * kTile + lane];
+      for (int u = 0; u < kJMade; ++u) {
+        made[u] = kNoSlot;
+        if (hs[u] != kNoSlot) {
+          const uint64_t v = cur.cv[u];
+          uint32_t h = hs[u];
+          unsigned long long p = prev[u];
+          while (p != kEmpty && p != v) {
+            h = (h + 1) & (kJSlots - 1);
+            p = atomicCAS(&tab[2 * h], (unsigned long long)kEmpty, (unsigned long long)v);
+          }
+          if (p == kEmpty) made[u] = h;
+          atomicOr(&tab[2 * h + 1], 1ull << cur.cid[u]);
+        }
+      }
+      __syncthreads();
+      // 2) probe with the row elements: first slots read together
+      const unsigned long long special = s_special;
+      ulonglong2 sl[kJRowPf];
+#pragma unroll
+      for (int u = 0; u < kJRowPf; ++u) {
+        sl[u] = make_ulonglong2(kEmpty, 0ull);
+        if (cur.rid[u] < r_valid && cur.rv[u] != kEmpty) sl[u] = s_tab[join_hash(cur.rv[u])];
+      }
+#pragma unroll
+      for (int u = 0; u < kJRowPf; ++u) {
+        const uint32_t r = cur.rid[u];
+        if (r >= r_valid || a.dbg) continue;
+        const uint64_t v = cur.rv[u];
+        unsigned long long m;
+        if (v == kEmpty) {
+          m = special;
+        } else {
+          ulonglong2 x = sl[u];
+          uint32_t h = join_hash(v);
+          while (x.x != v && x.x != kEmpty) {
+            h = (h + 1) & (kJSlots - 1);
+            x = s_tab[h];
+          }
+          m = x.x == v ? x.y : 0ull;
+        }
+        if (m) add_hits(r, m);
+      }
+      for (uint32_t k = rs + tid + kB * kJRowPf; k < re; k += kB) {
+        const uint32_t r = a.r_ids[k];
+        if (r >= r_valid) continue;
+        const uint64_t v = a.r_data[k];
         unsigned long long m = 0;
         if (v == kEmpty) {
           m = special;
         } else {
           uint32_t h = join_hash(v);
-          for (;;) {
-            const uint64_t k = s_key[h];
-            if (k == v) { m = s_msk[h]; break; }
-            if (k == kEmpty) break;
+          ulonglong2 x = s_tab[h];
+          while (x.x != v && x.x != kEmpty) {
             h = (h + 1) & (kJSlots - 1);
+            x = s_tab[h];
           }
+          m = x.x == v ? x.y : 0ull;
         }
-        while (m) {
-          const uint32_t c = (uint32_t)__builtin_ctzll(m);
-          m &= m - 1;
-          atomicAdd(&s_cnt[lane * kCntLd + c], 1u);
-        }
+        if (m) add_hits(r, m);
       }
-    }
-    __syncthreads();
-    // 3) reset the slots this thread created (and the ~0 mask)
+      __syncthreads();
+      // 3) reset the slots this thread created (and the ~0 mask)
 #pragma unroll
-    for (int u = 0; u < kJPer; ++u) {
-      if (made[u] != kNoSlot) {
-        s_key[made[u]] = kEmpty;
-        s_msk[made[u]] = 0;
-      }
+      for (int u = 0; u < kJMade; ++u)
+        if (made[u] != kNoSlot) s_tab[made[u]] = make_ulonglong2(kEmpty, 0ull);
+      if (tid == 0) s_special = 0;
+      __syncthreads();
+      cur = nxt;
+      bs = nbs;
+      be = nbe;
     }
-    if (tid == 0) s_special = 0;
-    __syncthreads();
   }
+  __syncthreads();
   // counts -> global (one atomic per nonzero pair; both halves for sym off-diagonal)
   for (int i = tid; i < kTile * kTile; i += kB) {
     const uint32_t r = i >> 6, c = i & 63;
@@ -522,102 +725,209 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
   if (n == 0 || out_words == 0) { *used_tiles = true; return hipSuccess; }
   std::vector<uint32_t> h_sizes(n);
-  std::vector<uint64_t> h_starts(n);
   if ((e = hipMemcpyAsync(h_sizes.data(), sizes, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-  if ((e = hipMemcpyAsync(h_starts.data(), starts, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-  uint32_t ref = 0;
-  for (uint32_t i = 1; i < n; ++i) if (h_sizes[i] > h_sizes[ref]) ref = i;
-  const uint32_t max_size = h_sizes[ref];
+  const uint32_t max_size = *std::max_element(h_sizes.begin(), h_sizes.end());
   if (max_size == 0) { *used_tiles = true; return hipSuccess; }
-  uint32_t B = 1;
-  while ((uint64_t)B * 32 < max_size) B <<= 1;  // mean part <= 32 elements
-  std::vector<uint32_t> h_pos;
-  uint32_t P = 0;
-  bool use_join = false;
+
   const uint32_t n_cb = (n + kTile - 1) / kTile;
-  for (;;) {
-    size_t bytes = sizeof(uint64_t) * (B + 1) + sizeof(uint32_t) * (uint64_t)n * (B + 1) + 64;
-    if ((e = work.reserve(bytes)) != hipSuccess) return e;
-    uint64_t* bounds = reinterpret_cast<uint64_t*>(work.ptr);
-    uint32_t* pos = reinterpret_cast<uint32_t*>(bounds + B + 1);
-    hipLaunchKernelGGL(k_bounds, dim3((B + 1 + kB - 1) / kB), dim3(kB), 0, s, data, h_starts[ref],
-                       max_size, B, bounds);
-    uint64_t items = (uint64_t)n * (B + 1);
-    hipLaunchKernelGGL(k_bucket_pos, dim3((unsigned)((items + kB - 1) / kB)), dim3(kB), 0, s, data,
-                       starts, sizes, n, B, bounds, pos);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    h_pos.resize(items);
-    if ((e = hipMemcpyAsync(h_pos.data(), pos, items * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    P = 0;
-    for (uint32_t i = 0; i < n; ++i)
-      for (uint32_t b = 0; b < B; ++b)
-        P = std::max(P, h_pos[(uint64_t)i * (B + 1) + b + 1] - h_pos[(uint64_t)i * (B + 1) + b]);
-    if (algo != kIntersectMerge && P <= (uint32_t)kJMaxPart) {
-      // largest bucket population of one 64-sketch column block (hash-table load)
-      uint32_t colmax = 0;
-      std::vector<uint32_t> acc(B);
-      for (uint32_t cb = 0; cb < n_cb && colmax <= (uint32_t)kJMaxCol; ++cb) {
-        std::fill(acc.begin(), acc.end(), 0u);
-        for (uint32_t i = cb * kTile; i < std::min(n, cb * kTile + kTile); ++i) {
-          const uint32_t* q = &h_pos[(uint64_t)i * (B + 1)];
-          for (uint32_t b = 0; b < B; ++b) acc[b] += q[b + 1] - q[b];
-        }
-        for (uint32_t b = 0; b < B; ++b) colmax = std::max(colmax, acc[b]);
-      }
-      if (colmax <= (uint32_t)kJMaxCol) { use_join = true; break; }
-    }
-    if (algo == kIntersectMerge && P <= (uint32_t)kGoodPart) break;
-    const bool grow = B < (1u << 16) &&
-                      (uint64_t)B * (algo == kIntersectMerge ? 8 : 2) <= max_size;
-    if (!grow) {
-      if (P <= (uint32_t)kMaxPart) break;  // merge tiles
-      return hipSuccess;  // pathological skew: caller falls back to the global kernel
-    }
-    B <<= 1;
-  }
-  TileArgs a{};
-  a.data = data;
-  a.starts = starts;
-  a.sizes = sizes;
-  a.pos = reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(work.ptr) + B + 1);
-  a.n = n;
-  a.B = B;
-  a.P = P;
-  a.sym = sym ? 1 : 0;
-  a.n_col_blocks = (n + kTile - 1) / kTile;
-  a.row_begin = row_begin;
-  a.row_end = row_end;
-  a.n_row_blocks = sym ? a.n_col_blocks : (row_end - row_begin + kTile - 1) / kTile;
-  const uint64_t all_tiles = sym ? (uint64_t)a.n_col_blocks * (a.n_col_blocks + 1) / 2
-                                 : (uint64_t)a.n_row_blocks * a.n_col_blocks;
+  const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
+  const uint64_t all_tiles = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
   if (!sym) { tile_begin = 0; tile_end = all_tiles; }
   tile_end = std::min(tile_end, all_tiles);
   if (tile_begin >= tile_end) { *used_tiles = true; return hipSuccess; }
   const uint64_t tiles = tile_end - tile_begin;
-  uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (2048 + tiles - 1) / tiles));
-  a.buckets_per_group = (B + groups - 1) / groups;
-  a.n_groups = (B + a.buckets_per_group - 1) / a.buckets_per_group;
-  a.tile_begin = tile_begin;
-  a.out = out;
-  a.ld = n;
-  if (use_join) {
-    hipLaunchKernelGGL(k_join, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), 0, s, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    *used_tiles = true;
-    return hipSuccess;
+  static const bool dbg = getenv("SKS_DEBUG_INTERSECT") != nullptr;
+
+  auto launch = [&](const uint64_t* d, const uint64_t* st, const uint32_t* pos, uint32_t B,
+                    uint32_t P) -> hipError_t {
+    TileArgs a{};
+    a.data = d;
+    a.starts = st;
+    a.sizes = sizes;
+    a.pos = pos;
+    a.n = n;
+    a.B = B;
+    a.P = P;
+    a.sym = sym ? 1 : 0;
+    a.n_col_blocks = n_cb;
+    a.row_begin = row_begin;
+    a.row_end = row_end;
+    a.n_row_blocks = n_rb;
+    uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (2048 + tiles - 1) / tiles));
+    a.buckets_per_group = (B + groups - 1) / groups;
+    a.n_groups = (B + a.buckets_per_group - 1) / a.buckets_per_group;
+    a.tile_begin = tile_begin;
+    a.out = out;
+    a.ld = n;
+    if (dbg)
+      fprintf(stderr, "[sks intersect] merge tiles n=%u B=%u P=%u tiles=%llu groups=%u\n", n, B, P,
+              (unsigned long long)tiles, a.n_groups);
+    const size_t lds_bytes = (size_t)std::max<uint32_t>(P, 1) * kSlots * sizeof(uint64_t) +
+                             kSlots * sizeof(uint32_t);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)(kMaxPart * kSlots * sizeof(uint64_t) + kSlots * sizeof(uint32_t)));
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), lds_bytes, s, a);
+    hipError_t le = hipGetLastError();
+    if (le == hipSuccess) *used_tiles = true;
+    return le;
+  };
+  auto align16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) total += h_sizes[i];
+  if (algo != kIntersectMerge && total < (1ull << 32)) {
+    // hash-bucketed block-major copy of the column sketches (and of the row
+    // range when its blocks are not aligned with the column blocks), then k_join
+    const bool sep_rows = !sym && (row_begin % kTile) != 0;
+    uint64_t r_total = 0;
+    if (sep_rows)
+      for (uint32_t i = row_begin; i < row_end; ++i) r_total += h_sizes[i];
+    // chunk capacity (table load <= cap / kJSlots); mean block-bucket ~ cap / 6
+    static const uint32_t cap = std::min<uint32_t>(
+        kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP")) : kJCap);
+    uint32_t log_b = 0;
+    while ((1ull << log_b) * (cap / 6) < 64ull * max_size && log_b < 14) ++log_b;
+    static const hipError_t attr_c = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k_hb_count), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)((1u << 14) * sizeof(uint32_t)));
+    static const hipError_t attr_s = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k_hb_scatter), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)((1u << 14) * sizeof(uint32_t)));
+    if (attr_c != hipSuccess) return attr_c;
+    if (attr_s != hipSuccess) return attr_s;
+    for (;;) {
+      const uint32_t B = 1u << log_b;
+      const uint64_t len_c = (uint64_t)n_cb * B * 64, len_r = sep_rows ? (uint64_t)n_rb * B * 64 : 0;
+      size_t tmp_c = 0, tmp_r = 0;
+      if ((e = rocprim::exclusive_scan(nullptr, tmp_c, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                       0u, (size_t)(len_c + 1), rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
+      if (sep_rows &&
+          (e = rocprim::exclusive_scan(nullptr, tmp_r, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                       0u, (size_t)(len_r + 1), rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
+      size_t o = 0;
+      const size_t o_ccnt = o; o = align16(o + (len_c + 1) * 4);
+      const size_t o_coff = o; o = align16(o + (len_c + 1) * 4);
+      const size_t o_cdat = o; o = align16(o + total * 8);
+      const size_t o_cids = o; o = align16(o + total);
+      const size_t o_rcnt = o; o = align16(o + (sep_rows ? (len_r + 1) * 4 : 0));
+      const size_t o_roff = o; o = align16(o + (sep_rows ? (len_r + 1) * 4 : 0));
+      const size_t o_rdat = o; o = align16(o + r_total * 8);
+      const size_t o_rids = o; o = align16(o + r_total);
+      const size_t o_stat = o; o = align16(o + 16);
+      const size_t o_tmp = o; o = align16(o + std::max(tmp_c, tmp_r));
+      if ((e = work.reserve(o)) != hipSuccess) return e;
+      char* w = static_cast<char*>(work.ptr);
+      uint32_t* c_cnt = reinterpret_cast<uint32_t*>(w + o_ccnt);
+      uint32_t* c_off = reinterpret_cast<uint32_t*>(w + o_coff);
+      uint64_t* c_dat = reinterpret_cast<uint64_t*>(w + o_cdat);
+      uint8_t* c_ids = reinterpret_cast<uint8_t*>(w + o_cids);
+      uint32_t* r_cnt = reinterpret_cast<uint32_t*>(w + o_rcnt);
+      uint32_t* r_off = reinterpret_cast<uint32_t*>(w + o_roff);
+      uint64_t* r_dat = reinterpret_cast<uint64_t*>(w + o_rdat);
+      uint8_t* r_ids = reinterpret_cast<uint8_t*>(w + o_rids);
+      uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
+      void* tmp = w + o_tmp;
+      if ((e = hipMemsetAsync(c_cnt, 0, (len_c + 1) * 4, s)) != hipSuccess) return e;
+      if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_hb_count, dim3(n), dim3(kB), B * 4, s, data, starts, sizes, 0u, 0u, B,
+                         log_b, c_cnt);
+      if ((e = rocprim::exclusive_scan(tmp, tmp_c, c_cnt, c_off, 0u, (size_t)(len_c + 1),
+                                       rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
+      hipLaunchKernelGGL(k_hb_scatter, dim3(n), dim3(kB), B * 4, s, data, starts, sizes, 0u, 0u, B,
+                         log_b, c_off, c_dat, c_ids);
+      const uint64_t cells = (uint64_t)n_cb * B;
+      hipLaunchKernelGGL(k_hb_stats, dim3((unsigned)((cells + kB - 1) / kB)), dim3(kB), 0, s, c_off,
+                         n_cb, B, stat);
+      if (sep_rows) {
+        const uint32_t rn = row_end - row_begin;
+        if ((e = hipMemsetAsync(r_cnt, 0, (len_r + 1) * 4, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_hb_count, dim3(rn), dim3(kB), B * 4, s, data, starts, sizes, row_begin,
+                           row_begin, B, log_b, r_cnt);
+        if ((e = rocprim::exclusive_scan(tmp, tmp_r, r_cnt, r_off, 0u, (size_t)(len_r + 1),
+                                         rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_hb_scatter, dim3(rn), dim3(kB), B * 4, s, data, starts, sizes,
+                           row_begin, row_begin, B, log_b, r_off, r_dat, r_ids);
+      }
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      uint32_t h_stat = 0;
+      if ((e = hipMemcpyAsync(&h_stat, stat, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+      if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+      if (dbg)
+        fprintf(stderr, "[sks intersect] join n=%u B=%u max block bucket %u tiles=%llu\n", n, B,
+                h_stat, (unsigned long long)tiles);
+      if (h_stat <= cap) {
+        JoinArgs ja{};
+        ja.c_data = c_dat;
+        ja.c_ids = c_ids;
+        ja.c_off = c_off;
+        if (sep_rows) {
+          ja.r_data = r_dat; ja.r_ids = r_ids; ja.r_off = r_off; ja.r_blk0 = 0;
+        } else {
+          ja.r_data = c_dat; ja.r_ids = c_ids; ja.r_off = c_off;
+          ja.r_blk0 = sym ? 0 : row_begin / kTile;
+        }
+        ja.B = B;
+        ja.n = n;
+        ja.n_col_blocks = n_cb;
+        ja.sym = sym ? 1 : 0;
+        ja.row_begin = row_begin;
+        ja.row_end = row_end;
+        ja.tile_begin = tile_begin;
+        ja.out = out;
+        ja.ld = n;
+        ja.cap = cap;
+        ja.dbg = getenv("SKS_JOIN_DEBUG") ? atoi(getenv("SKS_JOIN_DEBUG")) : 0;
+        static const uint64_t wgs = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 2048;
+        const uint32_t groups =
+            (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (wgs + tiles - 1) / tiles));
+        ja.buckets_per_group = (B + groups - 1) / groups;
+        ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
+        hipLaunchKernelGGL(k_join, dim3((unsigned)(tiles * ja.n_groups)), dim3(kB), 0, s, ja);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        *used_tiles = true;
+        return hipSuccess;
+      }
+      // a block-bucket larger than the table: only hash-adversarial inputs
+      if (log_b >= 14) break;
+      ++log_b;
+    }
   }
-  const size_t lds_bytes = (size_t)std::max<uint32_t>(P, 1) * kSlots * sizeof(uint64_t) +
-                           kSlots * sizeof(uint32_t);
-  static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(k_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)(kMaxPart * kSlots * sizeof(uint64_t) + kSlots * sizeof(uint32_t)));
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), lds_bytes, s, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  *used_tiles = true;
-  return hipSuccess;
+
+  // merge tiles: value-range buckets (parts must stay sorted)
+  uint32_t B = 1;
+  while ((uint64_t)B * 32 < max_size) B <<= 1;  // mean part <= 32 elements
+  for (;;) {
+    const size_t o_bounds = 0, o_pos = align16(o_bounds + (size_t)(B + 1) * 8);
+    const size_t o_stats = align16(o_pos + (size_t)n * (B + 1) * 4);
+    if ((e = work.reserve(o_stats + 16)) != hipSuccess) return e;
+    char* w = static_cast<char*>(work.ptr);
+    uint64_t* bounds = reinterpret_cast<uint64_t*>(w + o_bounds);
+    uint32_t* pos = reinterpret_cast<uint32_t*>(w + o_pos);
+    uint32_t* stats = reinterpret_cast<uint32_t*>(w + o_stats);
+    if ((e = hipMemsetAsync(stats, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bounds, dim3((B + 1 + kB - 1) / kB), dim3(kB), 0, s, data, starts, sizes,
+                       n, std::min<uint32_t>(n, 64), B, bounds);
+    const uint64_t items = (uint64_t)n * (B + 1);
+    hipLaunchKernelGGL(k_bucket_pos, dim3((unsigned)((items + kB - 1) / kB)), dim3(kB), 0, s, data,
+                       starts, sizes, n, B, bounds, pos);
+    const uint64_t cells = (uint64_t)n_cb * B;
+    hipLaunchKernelGGL(k_part_stats, dim3((unsigned)((cells + kB - 1) / kB)), dim3(kB), 0, s, pos,
+                       n, B, n_cb, stats);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t h_stats[2];
+    if ((e = hipMemcpyAsync(h_stats, stats, sizeof(h_stats), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint32_t P = h_stats[0];
+    if (P <= (uint32_t)kGoodPart) return launch(data, starts, pos, B, P);
+    if (B >= (1u << 16) || (uint64_t)B * 8 > max_size) {
+      if (P <= (uint32_t)kMaxPart) return launch(data, starts, pos, B, P);
+      return hipSuccess;  // pathological skew: caller falls back to the global kernel
+    }
+    B <<= 1;
+  }
 }
 
 uint64_t intersect_sym_tiles(uint32_t n) {

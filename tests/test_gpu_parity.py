@@ -362,6 +362,11 @@ def test_intersect_kernels_adversarial_arrays(torch_cuda, kernel_ctx, shape):
     ctx.intersect_all(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, n, out.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().reshape(n, n), want)
+    for r0, r1 in ((64, 150), (3, 97)):  # row blocks aligned / not aligned with column blocks
+        rows = torch.full(((r1 - r0) * n,), -5, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_all(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, r0, r1, rows.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(rows.cpu().numpy().reshape(r1 - r0, n), want[r0:r1])
     T = sksffi.intersect_sym_tiles(n)
     sym = torch.full((n * n,), 9, dtype=torch.int32, device="cuda:0")
     ctx.intersect_sym(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, T, sym.data_ptr())

@@ -18,6 +18,7 @@ import bench  # noqa: E402
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    mode = sys.argv[3] if len(sys.argv) > 3 else "family"  # family | indep | same
     ctx = sksffi.Context(0)
     L = bench.C4_LEN
     seg = [0]
@@ -26,6 +27,10 @@ def main():
     buf = torch.empty(seg[-1], dtype=torch.uint8, device="cuda")
     for g in range(n):
         a, m, r = bench.c4_genome_seeds(g)
+        if mode == "indep":
+            a, r = 5000 + g, 0.0
+        elif mode == "same":
+            a, r = 100, 0.0
         ctx.synth_bases(buf.data_ptr() + seg[g], L, a, m, r)
         buf[seg[g] + L] = ord("\n")
     mask = sksffi.mask_generate(31, 21, 0)
@@ -44,7 +49,7 @@ def main():
         if ref is None:
             ref = got
         same = bool(torch.equal(ref, got))
-        print(f"{name:6s} n={n} median {statistics.median(ms[1:]):.3f} ms  min {min(ms[1:]):.3f}"
+        print(f"{name:6s} {mode:6s} n={n} median {statistics.median(ms[1:]):.3f} ms  min {min(ms[1:]):.3f}"
               f"  equal_to_merge={same}  offdiag_sum={int(got.sum() - got.diag().sum())}",
               flush=True)
 
