@@ -8,6 +8,7 @@
 #include <numeric>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sks.h"
@@ -204,11 +205,26 @@ double sks_binomial_estimator(double containment, int kmer_num_ones) {
 int sks_ani_from_counts(const int32_t* inter, const int32_t* size_first, uint64_t n,
                         int kmer_num_ones, double* cont, double* ani) {
   if (n && (!inter || !size_first)) return sks::fail(SKS_E_ARG, "sks_ani_from_counts: null input");
-  for (uint64_t i = 0; i < n; ++i) {
-    double c = sks_containment(inter[i], size_first[i]);
-    if (cont) cont[i] = c;
-    if (ani) ani[i] = sks_binomial_estimator(c, kmer_num_ones);
+  // element-wise and order-free: large batches (an all-vs-all matrix) are split
+  // over host threads; every element is the same scalar double arithmetic
+  auto run = [=](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      double c = sks_containment(inter[i], size_first[i]);
+      if (cont) cont[i] = c;
+      if (ani) ani[i] = sks_binomial_estimator(c, kmer_num_ones);
+    }
+  };
+  const uint64_t kPer = 8192;
+  unsigned T = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  T = (unsigned)std::min<uint64_t>(T, (n + kPer - 1) / kPer);
+  if (T <= 1) {
+    run(0, n);
+    return SKS_OK;
   }
+  std::vector<std::thread> pool;
+  for (unsigned t = 1; t < T; ++t) pool.emplace_back(run, n * t / T, n * (t + 1) / T);
+  run(0, n / T);
+  for (auto& th : pool) th.join();
   return SKS_OK;
 }
 
