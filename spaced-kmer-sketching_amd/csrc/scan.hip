@@ -105,14 +105,49 @@ __device__ __forceinline__ void encode4(uint32_t x, uint32_t& le8, uint32_t& inv
   le8 = (y | (y >> 12)) & 0xFFu;
 }
 
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+// 16 ASCII bytes (x[0..4] funnel-shifted by sb bits) -> 32 bits of
+// little-endian 2-bit codes (base k at bits 2k) and a 16-bit invalid map.
+// Fast path: per dword, the 4 codes are gathered into bits 24..31 by one
+// multiply (c0 + c1<<2 + c2<<4 + c3<<6: the cross products land below bit 24
+// without overlapping), and validity of all 4 bytes is one v_sad_u8 against
+// the expected lower-case letters.  Only a 16-base word holding a non-ACGT
+// byte pays for the exact per-byte invalid bits (encode4).
+__device__ __forceinline__ void pack16(const uint32_t (&x)[5], uint32_t sb, uint32_t& le,
+                                       uint32_t& inv) {
+  uint32_t w[4], g[4], sad = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    w[k] = funnel(x[k + 1], x[k], sb);  // alignbit by 0 returns x[k]
+    const uint32_t low = w[k] | 0x20202020u;
+    const uint32_t code = ((low >> 1) ^ (low >> 2)) & 0x03030303u;
+    const uint32_t expect = __builtin_amdgcn_perm(0u, 0x74676361u, code);
+    sad = __builtin_amdgcn_sad_u8(low, expect, sad);
+    g[k] = code * 0x01041040u;  // gathered codes in bits 24..31
+  }
+  // bytes 3 of g[0..3] -> bytes 0..3 of le
+  const uint32_t g01 = __builtin_amdgcn_perm(g[1], g[0], 0x0c0c0703u);
+  const uint32_t g23 = __builtin_amdgcn_perm(g[3], g[2], 0x0c0c0703u);
+  le = __builtin_amdgcn_perm(g23, g01, 0x05040100u);
+  inv = 0;
+  if (sad) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t le8, inv4;
+      encode4(w[k], le8, inv4);
+      inv |= inv4 << (4 * k);
+    }
+  }
+}
+
 __device__ __forceinline__ uint32_t rev_pairs(uint32_t x) {
   uint32_t r = __builtin_bitreverse32(x);
   return ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
 }
 
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
-  return __builtin_amdgcn_alignbit(hi, lo, s);
-}
 
 template <int MODE>
 struct Queue {
@@ -262,15 +297,8 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
       uint32_t x[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) x[k] = s_raw[wi + k];
-      uint32_t le = 0, inv = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t word = sb ? funnel(x[k + 1], x[k], sb) : x[k];
-        uint32_t le8, inv4;
-        encode4(word, le8, inv4);
-        le |= le8 << (8 * k);
-        inv |= inv4 << (4 * k);
-      }
+      uint32_t le, inv;
+      pack16(x, sb, le, inv);
       s_be[kBeOff + i] = rev_pairs(le);
       s_lc[i] = ~le;
       s_inv[i] = inv;
@@ -427,15 +455,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
       uint32_t x[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) x[k] = s_raw[wi + k];
-      uint32_t le = 0, inv = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        uint32_t word = sb ? funnel(x[k + 1], x[k], sb) : x[k];
-        uint32_t le8, inv4;
-        encode4(word, le8, inv4);
-        le |= le8 << (8 * k);
-        inv |= inv4 << (4 * k);
-      }
+      uint32_t le, inv;
+      pack16(x, sb, le, inv);
       s_be[i] = rev_pairs(le);
       s_lc[i] = ~le;
       s_inv[i] = inv;
