@@ -265,15 +265,26 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
     n_tiles = sksffi.intersect_sym_tiles(n)
     dev = "cuda" if world > 1 and os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
 
+    prof = os.environ.get("SKS_SWEEP_PROFILE") is not None
+    phase = {"sketch": 0.0, "pairs": 0.0, "host": 0.0}
+
     def ani_for_seed(s):
+        t0 = time.perf_counter()
         ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, masks[s], sksffi.SKS_BOTTOM_S, C4_S)
         ss.export(padded.data_ptr(), C4_S, sizes.data_ptr())
+        if prof:
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
         ctx.intersect_sym(padded.data_ptr(), starts.data_ptr(), sizes.data_ptr(), 1, n, 0,
                           n_tiles, mat.data_ptr())
         counts = mat.cpu().numpy()
+        t2 = time.perf_counter()
         del ss
         size_first = np.repeat(np.diag(counts).astype(np.int32), n)
         _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones[s])
+        phase["sketch"] += t1 - t0
+        phase["pairs"] += t2 - t1
+        phase["host"] += time.perf_counter() - t2
         return torch.from_numpy(ani.reshape(n, n))
 
     total = 0.0
@@ -289,6 +300,8 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
             total += dt
             timed += 1
     t = total / max(timed, 1)
+    if prof:
+        log("[sweep phases, all iterations, s]", {k: round(v, 4) for k, v in phase.items()})
     c = cons.numpy()
     return {
         "metric": "seed-sweep genome-pairs ANI/s", "value": C5_SEEDS * n * n / t,
