@@ -166,7 +166,7 @@ def c4_genome_seeds(g):
 
 def run_pairs(ctx, world, rank, mask, steps, warmup):
     import sks_dist
-    per, g0, g1 = sks_dist.genome_shard(C4_GENOMES, world, rank)
+    _, g0, g1 = sks_dist.block_shard(C4_GENOMES, world, rank)
     n_local = g1 - g0
     seg = [0]
     for _ in range(n_local):
@@ -177,15 +177,38 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
         ctx.synth_bases(buf.data_ptr() + seg[i], C4_LEN, anc_seed, mut_seed, rate)
         buf[seg[i] + C4_LEN] = ord("\n")
     torch.cuda.synchronize()
-    stride = C4_S
-    local = torch.full((per, stride), -1, dtype=torch.int64, device="cuda")
-    local_sz = torch.zeros(per, dtype=torch.int32, device="cuda")
-    starts = torch.arange(per * world, dtype=torch.int64, device="cuda") * stride
     mat = torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32, device="cuda")
+    nb_local = (n_local + 63) // 64
+    dev = "cuda" if os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
 
-    def count_sym(src, src_sz, n, t0, t1, out):
-        ctx.intersect_sym(src.data_ptr(), starts.data_ptr(), src_sz.data_ptr(), 1, n, t0, t1,
-                          out.data_ptr())
+    lay_bufs = {}
+
+    def layout_fns(ss, sizes_h):
+        data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
+        tot = int(sizes_h.astype(np.int64).sum())
+
+        def build(log_b):
+            B1 = (1 << log_b) + 1
+            key = (tot, log_b)
+            if key not in lay_bufs:  # layout buffers persist across steps
+                lay_bufs.clear()
+                lay_bufs[key] = (torch.empty(max(tot, 1), dtype=torch.int64, device="cuda"),
+                                 torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda"),
+                                 torch.empty(max(nb_local * B1, 1), dtype=torch.int32, device="cuda"),
+                                 torch.empty(nb_local + 1, dtype=torch.int64, device="cuda"))
+            out = lay_bufs[key]
+            mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b,
+                                       *(t.data_ptr() for t in out))
+            return tuple(t.to(dev) for t in out) + (mx,)
+
+        def count(n, log_b, d, i, b, s, t0, t1, out):
+            lay = [t.to("cuda") for t in (d, i, b, s)]
+            tgt = out if out.is_cuda else torch.empty(out.shape, dtype=out.dtype, device="cuda")
+            ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in lay), t0, t1,
+                                     tgt.data_ptr())
+            if tgt is not out:
+                out.copy_(tgt.cpu())
+        return build, count
 
     t_sketch = t_pairs = 0.0
     timed = 0
@@ -194,13 +217,22 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ss = None
+        local_sizes = np.zeros(0, np.uint32)
         if n_local:
             ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, C4_S)
-            ss.export(local.data_ptr(), stride, local_sz.data_ptr())
+            local_sizes = ss.sizes().copy()
+        local_max = int(local_sizes.max()) if n_local else 0
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        # all-gather sketches, symmetric tiles of this rank, all-reduce counts
-        sks_dist.all_vs_all(local, local_sz, C4_GENOMES, world, rank, count_sym, out=mat)
+        # layouts of this rank's blocks, all-gathered; symmetric join tiles of
+        # this rank; all-reduce of the counts
+        build, count = layout_fns(ss, local_sizes)
+        out = mat if dev == "cuda" else torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32)
+        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max, sksffi.join_layout_log_b,
+                                       sksffi.join_layout_capacity(), build, count, device=dev,
+                                       out=out if dev == "cuda" else None)
+        if dev != "cuda":
+            mat.copy_(res)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ts, tp = max_over_ranks(t1 - t0, world), max_over_ranks(t2 - t1, world)
@@ -221,7 +253,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
     t_pairs /= max(timed, 1)
     if rank == 0:
         assert (counts == counts.T).all() and counts[0, 1] > 0
-        assert (sizes[:n_local] == local_sz.cpu().numpy()[:n_local]).all()
+        assert (sizes[g0:g1] == local_sizes[:n_local]).all()
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s", "scaling": "strong",
@@ -231,9 +263,12 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
         "ani_mean_all_pairs": float(np.mean(ani)),
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
                    "genome_len": C4_LEN, "s": C4_S, "w": W, "k": K,
-                   "pair_sharding": "upper-triangle 64x64 tiles split over ranks",
-                   "collective": ("all_gather_into_tensor sketches + all_reduce counts (RCCL)"
+                   "pair_sharding": "block-aligned genomes per rank; upper-triangle 64x64 "
+                                    "join tiles split over ranks",
+                   "collective": ("all_gather_into_tensor join layouts + all_reduce counts (RCCL)"
                                   if world > 1 else "none")},
+        "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
+        "ms_end_to_end": (t_sketch + t_pairs) * 1e3,
     }
 
 

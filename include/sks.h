@@ -222,6 +222,35 @@ int sks_intersect_sym(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_st
                       const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t tile_begin,
                       uint64_t tile_end, int32_t* d_out);
 
+/* ---- join layout: all-vs-all across GPUs ------------------------------------------------
+ * The all-pairs join kernel (sks_intersect_all / _sym, SKS_INTERSECT_JOIN) reads
+ * a "join layout": blocks of 64 consecutive sketches, their u64 elements
+ * hash-bucketed into 2^log_b buckets and stored block-major.  Exposing it lets a
+ * multi-GPU caller build the layout of its own sketches only and all-gather
+ * layouts instead of raw sketches (no replicated build):
+ *   data   u64[total]            elements, block-major (total = sum of sizes)
+ *   ids    u8[total]             slot of each element's sketch in its block
+ *   boff   u32[nb * (2^log_b+1)] bucket starts inside each block (nb = ceil(n/64))
+ *   bstart u64[nb + 1]           first element of each block in data/ids; [nb] = total
+ * Layouts of consecutive sketch ranges that each start at a multiple of 64 can
+ * be concatenated: append data/ids/boff and add the data offset to bstart. */
+/* log_b for a largest sketch of max_sketch_size elements (all ranks must agree). */
+uint32_t sks_join_layout_log_b(uint32_t max_sketch_size);
+/* Largest block-bucket population sks_intersect_sym_layout accepts. */
+uint32_t sks_join_layout_capacity(void);
+/* Builds the layout of sketches (d_data, d_starts, d_sizes)[0, n) (u64 elements)
+ * into caller buffers; *max_block_bucket (host) receives the largest
+ * block-bucket population — above sks_join_layout_capacity() use log_b + 1. */
+int sks_join_layout_build(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
+                          const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_out_data,
+                          uint8_t* d_out_ids, uint32_t* d_out_boff, uint64_t* d_out_bstart,
+                          uint32_t* max_block_bucket);
+/* sks_intersect_sym over a join layout of n sketches: upper-triangle 64x64 tiles
+ * [tile_begin, tile_end) into the n x n int32 matrix d_out (zeroed first). */
+int sks_intersect_sym_layout(sks_ctx* ctx, uint32_t n, uint32_t log_b, const uint64_t* d_data,
+                             const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+                             uint64_t tile_begin, uint64_t tile_end, int32_t* d_out);
+
 /* ---- FASTA ingress (device) — fasta_processing.cpp:79-133 on the GPU ------------------
  * d_raw: the n_raw bytes of one FASTA file in device memory (the host only reads
  * the file).  Writes to d_stream exactly the bytes sks_fasta_stream() holds for

@@ -1017,6 +1017,55 @@ int sks_intersect_sym(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   return SKS_OK;
 }
 
+uint32_t sks_join_layout_log_b(uint32_t max_sketch_size) { return sks::join_log_b(max_sketch_size); }
+uint32_t sks_join_layout_capacity(void) { return sks::join_cap(); }
+
+int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
+                          const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_out_data,
+                          uint8_t* d_out_ids, uint32_t* d_out_boff, uint64_t* d_out_bstart,
+                          uint32_t* max_block_bucket) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_join_layout_build: null ctx");
+  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_join_layout_build: log_b > 14");
+  if (!d_out_bstart || (n && (!d_starts || !d_sizes || !d_out_boff)))
+    return sks::fail(SKS_E_ARG, "sks_join_layout_build: null argument");
+  DeviceGuard g(c->device);
+  const size_t tmp = sks::join_layout_temp_bytes(n, log_b);
+  SKS_HIP(c->iwork.reserve(tmp + 64));
+  char* w = static_cast<char*>(c->iwork.ptr);
+  uint32_t* stat = reinterpret_cast<uint32_t*>(w + ((tmp + 15) & ~(size_t)15));
+  SKS_HIP(hipMemsetAsync(stat, 0, 4, c->stream));
+  if (n == 0) {
+    SKS_HIP(hipMemsetAsync(d_out_bstart, 0, 8, c->stream));
+  } else {
+    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, 0, n, log_b, d_out_data, d_out_ids,
+                                   d_out_boff, d_out_bstart, stat, w, tmp, c->stream));
+  }
+  uint32_t h = 0;
+  SKS_HIP(hipMemcpyAsync(&h, stat, 4, hipMemcpyDeviceToHost, c->stream));
+  SKS_HIP(hipStreamSynchronize(c->stream));
+  if (max_block_bucket) *max_block_bucket = h;
+  return SKS_OK;
+}
+
+int sks_intersect_sym_layout(sks_ctx* c, uint32_t n, uint32_t log_b, const uint64_t* d_data,
+                             const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+                             uint64_t tile_begin, uint64_t tile_end, int32_t* d_out) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: null ctx");
+  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: log_b > 14");
+  if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: bad tile range");
+  if (n && (!d_boff || !d_bstart || !d_out))
+    return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  SKS_HIP(hipMemsetAsync(d_out, 0, (uint64_t)n * n * sizeof(int32_t), c->stream));
+  if (n) {
+    const sks::JoinLayout L{d_data, d_ids, d_boff, d_bstart};
+    SKS_HIP(sks::join_launch(L, 0, L, n, log_b, true, 0, n, tile_begin, tile_end, d_out, c->stream));
+  }
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
 // Device time of the last intersection call (after the stream has reached it).
 int sks_ctx_last_intersect_ms(sks_ctx* c, float* ms) {
   if (!c || !ms) return sks::fail(SKS_E_ARG, "null argument");

@@ -382,6 +382,7 @@ constexpr int kJLog = 11;
 constexpr int kJCap = kJSlots / 2;          // column elements per chunk (load <= 1/2)
 constexpr int kJMade = kJCap / kB;          // column elements per thread per chunk (4)
 constexpr int kJWin = 256;                  // bucket offsets staged per window
+constexpr uint32_t kJMaxLogB = 14;          // B <= 16384 (LDS histogram of k_hb_count)
 constexpr int kCntLd = kTile + 1;
 constexpr uint64_t kEmpty = ~0ull;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
@@ -438,23 +439,26 @@ __global__ __launch_bounds__(kB) void k_hb_scatter(const uint64_t* __restrict__ 
   }
 }
 
-// Largest block-bucket population (one thread per (blk, b)).
-__global__ void k_hb_stats(const uint32_t* __restrict__ off, uint32_t n_blk, uint32_t B,
-                           uint32_t* __restrict__ stat) {
+// Compact per-block bucket starts: boff[blk][b] = off[(blk, b, 0)] - block start
+// (b = 0..B), bstart[blk] = block start (bstart[n_blk] = total), and the
+// largest block-bucket population into *stat.  One thread per (blk, b <= B).
+__global__ void k_hb_compact(const uint32_t* __restrict__ off, uint32_t n_blk, uint32_t B,
+                             uint32_t* __restrict__ boff, uint64_t* __restrict__ bstart,
+                             uint32_t* __restrict__ stat) {
   const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  if (idx >= (uint64_t)n_blk * B) return;
-  const uint32_t d = off[(idx + 1) * 64] - off[idx * 64];
-  atomicMax(stat, d);
+  if (idx >= (uint64_t)n_blk * (B + 1)) return;
+  const uint32_t blk = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
+  const uint32_t base = off[(uint64_t)blk * B * 64];
+  const uint32_t v = off[((uint64_t)blk * B + b) * 64];
+  boff[idx] = v - base;
+  if (b == 0) bstart[blk] = base;
+  if (blk == n_blk - 1 && b == B) bstart[n_blk] = v;
+  if (b < B) atomicMax(stat, off[((uint64_t)blk * B + b + 1) * 64] - v);
 }
 
 struct JoinArgs {
-  const uint64_t* r_data;
-  const uint8_t* r_ids;
-  const uint32_t* r_off;
-  uint32_t r_blk0;  // row block I of the tile = block r_blk0 + I of the row layout
-  const uint64_t* c_data;
-  const uint8_t* c_ids;
-  const uint32_t* c_off;
+  JoinLayout r, c;  // row blocks (tile row I = block r_blk0 + I) and column blocks
+  uint32_t r_blk0;
   uint32_t B, n, n_col_blocks, n_groups, buckets_per_group;
   int sym;
   uint32_t row_begin, row_end;
@@ -476,19 +480,23 @@ struct JoinChunk {
   uint32_t rid[kJRowPf];
 };
 
-__device__ __forceinline__ void join_fetch(const JoinArgs& a, uint32_t cs, uint32_t ce, uint32_t rs,
-                                           uint32_t re, int tid, JoinChunk& c) {
+__device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cdata,
+                                           const uint8_t* __restrict__ cids,
+                                           const uint64_t* __restrict__ rdata,
+                                           const uint8_t* __restrict__ rids, uint32_t cs,
+                                           uint32_t ce, uint32_t rs, uint32_t re, int tid,
+                                           JoinChunk& c) {
 #pragma unroll
   for (int u = 0; u < kJMade; ++u) {
     const uint32_t k = cs + tid + kB * u;
-    c.cv[u] = k < ce ? a.c_data[k] : 0;
-    c.cid[u] = k < ce ? a.c_ids[k] : 0xFFu;
+    c.cv[u] = k < ce ? cdata[k] : 0;
+    c.cid[u] = k < ce ? cids[k] : 0xFFu;
   }
 #pragma unroll
   for (int u = 0; u < kJRowPf; ++u) {
     const uint32_t k = rs + tid + kB * u;
-    c.rv[u] = k < re ? a.r_data[k] : 0;
-    c.rid[u] = k < re ? a.r_ids[k] : 0xFFu;
+    c.rv[u] = k < re ? rdata[k] : 0;
+    c.rid[u] = k < re ? rids[k] : 0xFFu;
   }
 }
 
@@ -513,8 +521,14 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
   const uint32_t row_lim = a.sym ? a.n : a.row_end;
   const uint32_t col0 = J * kTile;
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t* roff = a.r_off + (uint64_t)(a.r_blk0 + I) * a.B * 64;
-  const uint32_t* coff = a.c_off + (uint64_t)J * a.B * 64;
+  const uint32_t rblk = a.r_blk0 + I;
+  const uint64_t rb = a.r.bstart[rblk], cb = a.c.bstart[J];
+  const uint64_t* rdata = a.r.data + rb;
+  const uint8_t* rids = a.r.ids + rb;
+  const uint64_t* cdata = a.c.data + cb;
+  const uint8_t* cids = a.c.ids + cb;
+  const uint32_t* roff = a.r.boff + (uint64_t)rblk * (a.B + 1);
+  const uint32_t* coff = a.c.boff + (uint64_t)J * (a.B + 1);
   const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);  // slots < r_valid are rows
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(s_tab);  // [2h] key, [2h+1] mask
 
@@ -540,8 +554,8 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     const uint32_t we = min(b1, wb + kJWin);
     __syncthreads();  // previous window fully consumed
     for (uint32_t i = tid; i <= we - wb; i += kB) {
-      s_roff[i] = roff[(uint64_t)(wb + i) * 64];
-      s_coff[i] = coff[(uint64_t)(wb + i) * 64];
+      s_roff[i] = roff[wb + i];
+      s_coff[i] = coff[wb + i];
     }
     __syncthreads();
     // chunk = whole buckets [bs, be) whose column elements fit the table: the
@@ -560,7 +574,8 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
     uint32_t bs = wb, be = chunk_end(wb);
     JoinChunk cur;
-    join_fetch(a, s_coff[0], s_coff[be - wb], s_roff[0], s_roff[be - wb], tid, cur);
+    join_fetch(cdata, cids, rdata, rids, s_coff[0], s_coff[be - wb], s_roff[0], s_roff[be - wb],
+               tid, cur);
     while (bs < we) {
       const uint32_t cs = s_coff[bs - wb], ce = s_coff[be - wb];
       const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
@@ -569,7 +584,8 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
       const uint32_t nbe = nbs < we ? chunk_end(nbs) : nbs;
       JoinChunk nxt;
       if (nbs < we)
-        join_fetch(a, s_coff[nbs - wb], s_coff[nbe - wb], s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
+        join_fetch(cdata, cids, rdata, rids, s_coff[nbs - wb], s_coff[nbe - wb], s_roff[nbs - wb],
+                   s_roff[nbe - wb], tid, nxt);
 
       // 1) insert the column elements: every first CAS in flight together,
       //    then the collisions walk on
@@ -633,9 +649,9 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
         if (m) add_hits(r, m);
       }
       for (uint32_t k = rs + tid + kB * kJRowPf; k < re; k += kB) {
-        const uint32_t r = a.r_ids[k];
+        const uint32_t r = rids[k];
         if (r >= r_valid) continue;
-        const uint64_t v = a.r_data[k];
+        const uint64_t v = rdata[k];
         unsigned long long m = 0;
         if (v == kEmpty) {
           m = special;
@@ -712,6 +728,100 @@ hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* sta
 
 namespace sks {
 
+uint32_t join_cap() {
+  static const uint32_t cap = std::min<uint32_t>(
+      kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP")) : kJCap);
+  return cap;
+}
+
+// Bucket count for the join: mean block-bucket population ~ cap / 6, so a
+// chunk holds several whole buckets.
+uint32_t join_log_b(uint32_t max_size) {
+  uint32_t log_b = 0;
+  while ((1ull << log_b) * (join_cap() / 6) < 64ull * max_size && log_b < kJMaxLogB) ++log_b;
+  return log_b;
+}
+
+size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b) {
+  const uint64_t len = (uint64_t)((count + kTile - 1) / kTile) * (1ull << log_b) * 64;
+  size_t scan = 0;
+  (void)rocprim::exclusive_scan(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                (size_t)(len + 1), rocprim::plus<uint32_t>(), (hipStream_t)0);
+  return ((2 * (len + 1) * 4 + 15) & ~(size_t)15) + scan + 16;
+}
+
+hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                             uint32_t first, uint32_t count, uint32_t log_b, uint64_t* out_data,
+                             uint8_t* out_ids, uint32_t* out_boff, uint64_t* out_bstart,
+                             uint32_t* d_stat, void* temp, size_t temp_bytes, hipStream_t s) {
+  static const hipError_t attr_c = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_hb_count), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)((1u << kJMaxLogB) * sizeof(uint32_t)));
+  static const hipError_t attr_s = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_hb_scatter), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)((1u << kJMaxLogB) * sizeof(uint32_t)));
+  if (attr_c != hipSuccess) return attr_c;
+  if (attr_s != hipSuccess) return attr_s;
+  if (count == 0) return hipSuccess;
+  const uint32_t B = 1u << log_b;
+  const uint32_t n_blk = (count + kTile - 1) / kTile;
+  const uint64_t len = (uint64_t)n_blk * B * 64;
+  uint32_t* cnt = static_cast<uint32_t*>(temp);
+  uint32_t* off = cnt + (len + 1);
+  const size_t head = ((2 * (len + 1) * 4 + 15) & ~(size_t)15);
+  if (temp_bytes < head) return hipErrorInvalidValue;
+  void* scan_tmp = static_cast<char*>(temp) + head;
+  size_t scan_bytes = temp_bytes - head;
+  hipError_t e;
+  if ((e = hipMemsetAsync(cnt, 0, (len + 1) * 4, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_hb_count, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first, first,
+                     B, log_b, cnt);
+  if ((e = rocprim::exclusive_scan(scan_tmp, scan_bytes, cnt, off, 0u, (size_t)(len + 1),
+                                   rocprim::plus<uint32_t>(), s)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(k_hb_scatter, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first,
+                     first, B, log_b, off, out_data, out_ids);
+  const uint64_t cells = (uint64_t)n_blk * (B + 1);
+  hipLaunchKernelGGL(k_hb_compact, dim3((unsigned)((cells + kB - 1) / kB)), dim3(kB), 0, s, off,
+                     n_blk, B, out_boff, out_bstart, d_stat);
+  return hipGetLastError();
+}
+
+hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t n,
+                       uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
+                       uint64_t tile_begin, uint64_t tile_end, int32_t* out, hipStream_t s) {
+  const uint32_t n_cb = (n + kTile - 1) / kTile;
+  const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
+  const uint64_t all_tiles = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
+  if (!sym) { tile_begin = 0; tile_end = all_tiles; }
+  tile_end = std::min(tile_end, all_tiles);
+  if (tile_begin >= tile_end) return hipSuccess;
+  const uint64_t tiles = tile_end - tile_begin;
+  const uint32_t B = 1u << log_b;
+  JoinArgs ja{};
+  ja.r = rows;
+  ja.c = cols;
+  ja.r_blk0 = r_blk0;
+  ja.B = B;
+  ja.n = n;
+  ja.n_col_blocks = n_cb;
+  ja.sym = sym ? 1 : 0;
+  ja.row_begin = row_begin;
+  ja.row_end = row_end;
+  ja.tile_begin = tile_begin;
+  ja.out = out;
+  ja.ld = n;
+  ja.cap = join_cap();
+  ja.dbg = getenv("SKS_JOIN_DEBUG") ? atoi(getenv("SKS_JOIN_DEBUG")) : 0;
+  static const uint64_t wgs = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 2048;
+  const uint32_t groups =
+      (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (wgs + tiles - 1) / tiles));
+  ja.buckets_per_group = (B + groups - 1) / groups;
+  ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
+  hipLaunchKernelGGL(k_join, dim3((unsigned)(tiles * ja.n_groups)), dim3(kB), 0, s, ja);
+  return hipGetLastError();
+}
+
 // Tiled all-pairs for u64 sketches.  Host-synchronous (reads sizes and bucket
 // positions back to pick the bucket count).  mode: sym (upper-triangle tiles
 // [tile_begin, tile_end) into a full n x n matrix) or rows.
@@ -782,116 +892,62 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     // hash-bucketed block-major copy of the column sketches (and of the row
     // range when its blocks are not aligned with the column blocks), then k_join
     const bool sep_rows = !sym && (row_begin % kTile) != 0;
+    const uint32_t rn = row_end - row_begin;
     uint64_t r_total = 0;
     if (sep_rows)
       for (uint32_t i = row_begin; i < row_end; ++i) r_total += h_sizes[i];
-    // chunk capacity (table load <= cap / kJSlots); mean block-bucket ~ cap / 6
-    static const uint32_t cap = std::min<uint32_t>(
-        kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP")) : kJCap);
-    uint32_t log_b = 0;
-    while ((1ull << log_b) * (cap / 6) < 64ull * max_size && log_b < 14) ++log_b;
-    static const hipError_t attr_c = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(k_hb_count), hipFuncAttributeMaxDynamicSharedMemorySize,
-        (int)((1u << 14) * sizeof(uint32_t)));
-    static const hipError_t attr_s = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(k_hb_scatter), hipFuncAttributeMaxDynamicSharedMemorySize,
-        (int)((1u << 14) * sizeof(uint32_t)));
-    if (attr_c != hipSuccess) return attr_c;
-    if (attr_s != hipSuccess) return attr_s;
+    uint32_t log_b = join_log_b(max_size);
     for (;;) {
       const uint32_t B = 1u << log_b;
-      const uint64_t len_c = (uint64_t)n_cb * B * 64, len_r = sep_rows ? (uint64_t)n_rb * B * 64 : 0;
-      size_t tmp_c = 0, tmp_r = 0;
-      if ((e = rocprim::exclusive_scan(nullptr, tmp_c, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                       0u, (size_t)(len_c + 1), rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
-      if (sep_rows &&
-          (e = rocprim::exclusive_scan(nullptr, tmp_r, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                       0u, (size_t)(len_r + 1), rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
+      const size_t tmp_c = join_layout_temp_bytes(n, log_b);
+      const size_t tmp_r = sep_rows ? join_layout_temp_bytes(rn, log_b) : 0;
       size_t o = 0;
-      const size_t o_ccnt = o; o = align16(o + (len_c + 1) * 4);
-      const size_t o_coff = o; o = align16(o + (len_c + 1) * 4);
       const size_t o_cdat = o; o = align16(o + total * 8);
       const size_t o_cids = o; o = align16(o + total);
-      const size_t o_rcnt = o; o = align16(o + (sep_rows ? (len_r + 1) * 4 : 0));
-      const size_t o_roff = o; o = align16(o + (sep_rows ? (len_r + 1) * 4 : 0));
+      const size_t o_cbof = o; o = align16(o + (size_t)n_cb * (B + 1) * 4);
+      const size_t o_cbst = o; o = align16(o + (size_t)(n_cb + 1) * 8);
       const size_t o_rdat = o; o = align16(o + r_total * 8);
       const size_t o_rids = o; o = align16(o + r_total);
+      const size_t o_rbof = o; o = align16(o + (sep_rows ? (size_t)n_rb * (B + 1) * 4 : 0));
+      const size_t o_rbst = o; o = align16(o + (sep_rows ? (size_t)(n_rb + 1) * 8 : 0));
       const size_t o_stat = o; o = align16(o + 16);
       const size_t o_tmp = o; o = align16(o + std::max(tmp_c, tmp_r));
       if ((e = work.reserve(o)) != hipSuccess) return e;
       char* w = static_cast<char*>(work.ptr);
-      uint32_t* c_cnt = reinterpret_cast<uint32_t*>(w + o_ccnt);
-      uint32_t* c_off = reinterpret_cast<uint32_t*>(w + o_coff);
-      uint64_t* c_dat = reinterpret_cast<uint64_t*>(w + o_cdat);
-      uint8_t* c_ids = reinterpret_cast<uint8_t*>(w + o_cids);
-      uint32_t* r_cnt = reinterpret_cast<uint32_t*>(w + o_rcnt);
-      uint32_t* r_off = reinterpret_cast<uint32_t*>(w + o_roff);
-      uint64_t* r_dat = reinterpret_cast<uint64_t*>(w + o_rdat);
-      uint8_t* r_ids = reinterpret_cast<uint8_t*>(w + o_rids);
+      JoinLayout cl{reinterpret_cast<uint64_t*>(w + o_cdat), reinterpret_cast<uint8_t*>(w + o_cids),
+                    reinterpret_cast<uint32_t*>(w + o_cbof), reinterpret_cast<uint64_t*>(w + o_cbst)};
+      JoinLayout rl = cl;
       uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
-      void* tmp = w + o_tmp;
-      if ((e = hipMemsetAsync(c_cnt, 0, (len_c + 1) * 4, s)) != hipSuccess) return e;
       if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_hb_count, dim3(n), dim3(kB), B * 4, s, data, starts, sizes, 0u, 0u, B,
-                         log_b, c_cnt);
-      if ((e = rocprim::exclusive_scan(tmp, tmp_c, c_cnt, c_off, 0u, (size_t)(len_c + 1),
-                                       rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_hb_scatter, dim3(n), dim3(kB), B * 4, s, data, starts, sizes, 0u, 0u, B,
-                         log_b, c_off, c_dat, c_ids);
-      const uint64_t cells = (uint64_t)n_cb * B;
-      hipLaunchKernelGGL(k_hb_stats, dim3((unsigned)((cells + kB - 1) / kB)), dim3(kB), 0, s, c_off,
-                         n_cb, B, stat);
+      if ((e = join_layout_build(data, starts, sizes, 0, n, log_b, const_cast<uint64_t*>(cl.data),
+                                 const_cast<uint8_t*>(cl.ids), const_cast<uint32_t*>(cl.boff),
+                                 const_cast<uint64_t*>(cl.bstart), stat, w + o_tmp, tmp_c, s)) != hipSuccess)
+        return e;
       if (sep_rows) {
-        const uint32_t rn = row_end - row_begin;
-        if ((e = hipMemsetAsync(r_cnt, 0, (len_r + 1) * 4, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_hb_count, dim3(rn), dim3(kB), B * 4, s, data, starts, sizes, row_begin,
-                           row_begin, B, log_b, r_cnt);
-        if ((e = rocprim::exclusive_scan(tmp, tmp_r, r_cnt, r_off, 0u, (size_t)(len_r + 1),
-                                         rocprim::plus<uint32_t>(), s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_hb_scatter, dim3(rn), dim3(kB), B * 4, s, data, starts, sizes,
-                           row_begin, row_begin, B, log_b, r_off, r_dat, r_ids);
+        rl = JoinLayout{reinterpret_cast<uint64_t*>(w + o_rdat), reinterpret_cast<uint8_t*>(w + o_rids),
+                        reinterpret_cast<uint32_t*>(w + o_rbof), reinterpret_cast<uint64_t*>(w + o_rbst)};
+        if ((e = join_layout_build(data, starts, sizes, row_begin, rn, log_b,
+                                   const_cast<uint64_t*>(rl.data), const_cast<uint8_t*>(rl.ids),
+                                   const_cast<uint32_t*>(rl.boff), const_cast<uint64_t*>(rl.bstart),
+                                   stat, w + o_tmp, tmp_r, s)) != hipSuccess)
+          return e;
       }
-      if ((e = hipGetLastError()) != hipSuccess) return e;
       uint32_t h_stat = 0;
       if ((e = hipMemcpyAsync(&h_stat, stat, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
       if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
       if (dbg)
         fprintf(stderr, "[sks intersect] join n=%u B=%u max block bucket %u tiles=%llu\n", n, B,
                 h_stat, (unsigned long long)tiles);
-      if (h_stat <= cap) {
-        JoinArgs ja{};
-        ja.c_data = c_dat;
-        ja.c_ids = c_ids;
-        ja.c_off = c_off;
-        if (sep_rows) {
-          ja.r_data = r_dat; ja.r_ids = r_ids; ja.r_off = r_off; ja.r_blk0 = 0;
-        } else {
-          ja.r_data = c_dat; ja.r_ids = c_ids; ja.r_off = c_off;
-          ja.r_blk0 = sym ? 0 : row_begin / kTile;
-        }
-        ja.B = B;
-        ja.n = n;
-        ja.n_col_blocks = n_cb;
-        ja.sym = sym ? 1 : 0;
-        ja.row_begin = row_begin;
-        ja.row_end = row_end;
-        ja.tile_begin = tile_begin;
-        ja.out = out;
-        ja.ld = n;
-        ja.cap = cap;
-        ja.dbg = getenv("SKS_JOIN_DEBUG") ? atoi(getenv("SKS_JOIN_DEBUG")) : 0;
-        static const uint64_t wgs = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 2048;
-        const uint32_t groups =
-            (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (wgs + tiles - 1) / tiles));
-        ja.buckets_per_group = (B + groups - 1) / groups;
-        ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
-        hipLaunchKernelGGL(k_join, dim3((unsigned)(tiles * ja.n_groups)), dim3(kB), 0, s, ja);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+      if (h_stat <= join_cap()) {
+        const uint32_t r_blk0 = sep_rows ? 0 : (sym ? 0 : row_begin / kTile);
+        if ((e = join_launch(rl, r_blk0, cl, n, log_b, sym, row_begin, row_end, tile_begin, tile_end,
+                             out, s)) != hipSuccess)
+          return e;
         *used_tiles = true;
         return hipSuccess;
       }
       // a block-bucket larger than the table: only hash-adversarial inputs
-      if (log_b >= 14) break;
+      if (log_b >= kJMaxLogB) break;
       ++log_b;
     }
   }

@@ -109,6 +109,30 @@ constexpr int kIntersectJoin = 2;    // k_join (LDS hash join), merge tiles if i
 constexpr int kIntersectGlobal = 3;  // one wavefront per pair from global memory
 uint64_t intersect_sym_tiles(uint32_t n);
 
+// Join layout (input of k_join, intersect.hip): blocks of 64 consecutive
+// sketches, elements hash-bucketed into B = 2^log_b buckets and stored block-major.
+// Block k's elements are data[bstart[k] ..] / ids[bstart[k] ..] (ids = slot
+// in the block); its bucket b starts boff[k * (B + 1) + b] elements in.
+struct JoinLayout {
+  const uint64_t* data;
+  const uint8_t* ids;
+  const uint32_t* boff;
+  const uint64_t* bstart;
+};
+uint32_t join_cap();                       // elements per join chunk (table capacity)
+uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch of max_size
+size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b);
+// Layout of sketches [first, first + count) into out_*; out_bstart gets
+// ceil(count/64) + 1 entries (the last = element total); *d_stat is raised to
+// the largest block-bucket population (the join needs it <= join_cap()).
+hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                             uint32_t first, uint32_t count, uint32_t log_b, uint64_t* out_data,
+                             uint8_t* out_ids, uint32_t* out_boff, uint64_t* out_bstart,
+                             uint32_t* d_stat, void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t n,
+                       uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
+                       uint64_t tile_begin, uint64_t tile_end, int32_t* out, hipStream_t s);
+
 // ---- device FASTA ingress (ingress.hip) -------------------------------------------------
 // strings_from_fasta on the device: writes the host parser's record stream
 // (fasta.cpp) to `out` and each record's '\n' position to rec_end (optional).

@@ -113,3 +113,88 @@ def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
         sum_matrix(acc)
     acc /= n_seeds
     return acc, mine
+
+
+# ---- all-vs-all over gathered join layouts ------------------------------------------------
+# The join kernel's input (sks_join_layout_build) is built per 64-sketch block,
+# so each rank builds the layout of its OWN block-aligned genome range and the
+# ranks all-gather layouts instead of raw sketches: nothing is rebuilt on every
+# rank, and the gathered bytes (9 B per element + bucket starts) are about the
+# same as the padded sketches.  Block k of the gathered layout is block
+# k - r*bpr of rank r, so its start is shifted by r * (padded layout size).
+
+def block_shard(n_genomes, world, rank):
+    """(blocks per rank, g0, g1): genome range of `rank`, whole 64-sketch blocks."""
+    n_blk = (n_genomes + TILE - 1) // TILE
+    bpr = max(1, (n_blk + world - 1) // world)
+    g0 = min(n_genomes, rank * bpr * TILE)
+    return bpr, g0, min(n_genomes, g0 + bpr * TILE)
+
+
+def _max_over(x, world, device):
+    if world == 1:
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
+def _gather_flat(t, world):
+    if world == 1:
+        return t
+    if dist.get_backend() == "nccl":
+        out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+    host = t.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host)
+    return torch.cat(parts).to(t.device)
+
+
+def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity, build, count,
+                    device="cpu", out=None):
+    """Full n x n int32 intersection matrix on every rank.
+
+    build(log_b) -> (data u64[tot], ids u8[tot], boff u32[nb*(B+1)], bstart u64[nb+1],
+                     max_block_bucket) for this rank's block-aligned genomes (block_shard);
+    count(n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out) fills `out`
+    (zeroed first) with the counts of upper-triangle tiles [tile_begin, tile_end), both halves
+    — the contract of sks_intersect_sym_layout."""
+    bpr, g0, g1 = block_shard(n_genomes, world, rank)
+    log_b = log_b_for(_max_over(local_max_size, world, device))
+    while True:
+        data, ids, boff, bstart, mb = build(log_b)
+        if _max_over(mb, world, device) <= capacity or log_b >= 14:
+            break
+        log_b += 1
+    B1 = (1 << log_b) + 1
+    t0, t1 = tile_shard(sym_tiles(n_genomes), world, rank)
+    if out is None:
+        out = torch.empty((n_genomes, n_genomes), dtype=torch.int32, device=device)
+    if world == 1:  # the local layout is the whole layout
+        count(n_genomes, log_b, data, ids, boff, bstart, t0, t1, out)
+        return out
+    nb_local = (g1 - g0 + TILE - 1) // TILE
+    tot = int(bstart[nb_local].item()) if nb_local else 0
+    cap_e = max(1, _max_over(tot, world, device))
+    # pad to the common per-rank shape; missing blocks are empty
+    pd = torch.zeros(cap_e, dtype=torch.int64, device=device)
+    pi = torch.zeros(cap_e, dtype=torch.uint8, device=device)
+    pb = torch.zeros(bpr * B1, dtype=torch.int32, device=device)
+    ps = torch.full((bpr + 1,), tot, dtype=torch.int64, device=device)
+    if tot:
+        pd[:tot] = data[:tot]
+        pi[:tot] = ids[:tot]
+    if nb_local:
+        pb[: nb_local * B1] = boff[: nb_local * B1]
+        ps[: nb_local + 1] = bstart[: nb_local + 1]
+    g_data, g_ids, g_boff = _gather_flat(pd, world), _gather_flat(pi, world), _gather_flat(pb, world)
+    g_bst = _gather_flat(ps, world).view(world, bpr + 1)[:, :bpr]
+    g_bst = (g_bst + torch.arange(world, device=device, dtype=torch.int64).view(world, 1) * cap_e)
+    g_bst = torch.cat([g_bst.reshape(-1),
+                       torch.tensor([world * cap_e], dtype=torch.int64, device=device)])
+    count(n_genomes, log_b, g_data, g_ids, g_boff, g_bst, t0, t1, out)
+    if world > 1:
+        sum_matrix(out)
+    return out

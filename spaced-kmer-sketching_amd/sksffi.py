@@ -53,7 +53,8 @@ EXPORTED = [
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
     "sks_synth_bases", "sks_intersect_sym", "sks_intersect_sym_tiles",
-    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_ctx_set_intersect_kernel", "sks_fasta_parse_device",
+    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_ctx_set_intersect_kernel", "sks_join_layout_log_b",
+    "sks_join_layout_capacity", "sks_join_layout_build", "sks_intersect_sym_layout", "sks_fasta_parse_device",
     "sks_ctx_last_ingress_ms", "sks_kmer_list_build", "sks_kmer_list_free", "sks_kmer_list_total",
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
@@ -100,6 +101,14 @@ def lib():
     L.sks_ctx_last_timings.argtypes = [vp, C.POINTER(Timings)]
     L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
     L.sks_ctx_set_intersect_kernel.argtypes = [vp, C.c_int]
+    L.sks_join_layout_log_b.argtypes = [C.c_uint32]
+    L.sks_join_layout_log_b.restype = C.c_uint32
+    L.sks_join_layout_capacity.argtypes = []
+    L.sks_join_layout_capacity.restype = C.c_uint32
+    L.sks_join_layout_build.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp,
+                                        C.POINTER(C.c_uint32)]
+    L.sks_intersect_sym_layout.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint64,
+                                           C.c_uint64, vp]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_device.argtypes = [vp]
@@ -174,6 +183,14 @@ def mask_contiguous(length):
 
 def frac_min_hash(kmer, mask, window, nonce=1, flavour=0):
     return int(lib().sks_frac_min_hash(_mask_arr(kmer), _mask_arr(mask), window, nonce, flavour))
+
+
+def join_layout_log_b(max_sketch_size):
+    return int(lib().sks_join_layout_log_b(max_sketch_size))
+
+
+def join_layout_capacity():
+    return int(lib().sks_join_layout_capacity())
 
 
 def intersect_sym_tiles(n):
@@ -264,6 +281,21 @@ class Context:
 
     def set_scan_grid(self, grid):
         check(lib().sks_ctx_set_scan_grid(self.h, grid))
+
+    def join_layout_build(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_data, out_ids,
+                          out_boff, out_bstart):
+        """sks_join_layout_build; returns the largest block-bucket population."""
+        mx = C.c_uint32(0)
+        check(lib().sks_join_layout_build(self.h, C.c_void_p(data_ptr), C.c_void_p(starts_ptr),
+                                          C.c_void_p(sizes_ptr), n, log_b, C.c_void_p(out_data),
+                                          C.c_void_p(out_ids), C.c_void_p(out_boff),
+                                          C.c_void_p(out_bstart), C.byref(mx)))
+        return mx.value
+
+    def intersect_sym_layout(self, n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out):
+        check(lib().sks_intersect_sym_layout(self.h, n, log_b, C.c_void_p(data), C.c_void_p(ids),
+                                             C.c_void_p(boff), C.c_void_p(bstart), tile_begin,
+                                             tile_end, C.c_void_p(out)))
 
     def set_intersect_kernel(self, kind):
         """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL (sks.h); all give identical counts."""

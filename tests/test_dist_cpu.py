@@ -156,3 +156,107 @@ def test_seed_sweep_gloo_matches_single_process(world):
         # north-star ANI tolerance is 1e-9
         assert np.allclose(results[r][0], want, rtol=0, atol=1e-12)
     assert want[0, 0] == 1.0 and 0 < want[0, 2] < 1
+
+
+# ---- config 4 over gathered join layouts (sks_dist.all_vs_all_join) ------------------
+PHI = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _np_layout(sketches, log_b):
+    """numpy restatement of sks_join_layout_build: blocks of 64, hash buckets
+    (v * phi) >> (64 - log_b), block-major; returns torch tensors like the ABI."""
+    B = 1 << log_b
+    data, ids, boff, bstart, mx = [], [], [], [0], 0
+    for b0 in range(0, len(sketches), 64):
+        blk = sketches[b0:b0 + 64]
+        with np.errstate(over="ignore"):
+            hb = [(s * PHI) >> np.uint64(64 - log_b) if log_b else np.zeros(len(s), np.uint64)
+                  for s in blk]
+        start = len(data)
+        offs = []
+        for b in range(B):
+            offs.append(len(data) - start)
+            here = 0
+            for slot, (s, h) in enumerate(zip(blk, hb)):
+                sel = s[h == b]
+                data.extend(sel.tolist())
+                ids.extend([slot] * len(sel))
+                here += len(sel)
+            mx = max(mx, here)
+        offs.append(len(data) - start)
+        boff.extend(offs)
+        bstart.append(len(data))
+    as_t = lambda x, dt: torch.tensor(np.array(x, dtype=np.uint64).view(np.int64) if dt == torch.int64
+                                       else np.array(x), dtype=dt)
+    return (as_t(data, torch.int64), torch.tensor(ids, dtype=torch.uint8),
+            torch.tensor(boff, dtype=torch.int32), as_t(bstart, torch.int64), mx)
+
+
+def _np_count_layout(n, log_b, data, ids, boff, bstart, t0, t1, out):
+    """Counts from a gathered layout (decodes block k's sketches by id)."""
+    out.zero_()
+    B1 = (1 << log_b) + 1
+    d = data.numpy().view(np.uint64)
+
+    def sketches_of(k):
+        a = int(bstart[k])
+        e = a + int(boff[k * B1 + B1 - 1])
+        vals, sl = d[a:e], ids[a:e].numpy()
+        return [np.sort(vals[sl == i]) for i in range(64)]
+    for t in range(t0, t1):
+        I, J = sks_dist.sym_tile_coords(t, n)
+        ri, cj = sketches_of(I), sketches_of(J)
+        for a in range(64):
+            for b in range(64):
+                i, j = I * 64 + a, J * 64 + b
+                if i < n and j < n:
+                    c = np.intersect1d(ri[a], cj[b], assume_unique=True).size
+                    out[i, j] = c
+                    out[j, i] = c
+
+
+def _join_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sk = [s.astype(np.uint64) for s in _sketches()]
+    _, g0, g1 = sks_dist.block_shard(N_GENOMES, world, rank)
+    mine = sk[g0:g1]
+    mat = sks_dist.all_vs_all_join(
+        N_GENOMES, world, rank, max((len(s) for s in mine), default=0),
+        lambda m: 3, capacity=10**9, build=lambda lb: _np_layout(mine, lb),
+        count=_np_count_layout)
+    q.put((rank, mat.numpy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_vs_all_join_layout_gather_gloo(world):
+    """Ranks build layouts of their own block-aligned genomes, all-gather them and
+    count their tile share: every rank ends with the single-process matrix."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sk = _sketches()
+    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(N_GENOMES)]
+                     for i in range(N_GENOMES)])
+    for r in range(world):
+        assert np.array_equal(results[r], want)
+
+
+def test_block_shard_covers_whole_blocks():
+    for n in (1, 64, 65, 130, 1000):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                bpr, g0, g1 = sks_dist.block_shard(n, world, r)
+                assert (g0 % 64 == 0 or g0 == n) and (g1 == n or (g1 - g0) == bpr * 64)
+                seen += list(range(g0, g1))
+            assert seen == list(range(n))

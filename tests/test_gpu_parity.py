@@ -372,3 +372,58 @@ def test_intersect_kernels_adversarial_arrays(torch_cuda, kernel_ctx, shape):
     ctx.intersect_sym(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, T, sym.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(sym.cpu().numpy().reshape(n, n), want)
+
+
+def test_join_layout_build_and_concat(torch_cuda, ctx):
+    """sks_join_layout_build + sks_intersect_sym_layout: one layout of all
+    sketches, and two layouts of block-aligned halves concatenated the way the
+    multi-GPU all-gather does (data/ids/boff appended, bstart shifted), both give
+    the oracle matrix, for every tile range split."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    n = 150
+    base = [np.unique(rng.integers(0, 2**62, size=2500, dtype=np.uint64)) for _ in range(3)]
+    sk = []
+    for i in range(n):
+        b = base[i % 3]
+        keep = b[rng.random(b.size) < 0.2 + 0.7 * ((i * 5) % 9) / 9]
+        extra = rng.integers(0, 2**64 - 1, size=int(rng.integers(0, 300)), dtype=np.uint64)
+        sk.append(np.unique(np.concatenate([keep, extra, np.array([2**64 - 1], np.uint64)]))
+                  if i % 7 == 0 else np.unique(np.concatenate([keep, extra])))
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)]
+                     for i in range(n)])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    log_b = sksffi.join_layout_log_b(max(len(s) for s in sk))
+    B1 = (1 << log_b) + 1
+    cap = sksffi.join_layout_capacity()
+
+    def build(first, count):
+        tot = int(sum(len(s) for s in sk[first:first + count]))
+        nb = (count + 63) // 64
+        out = (torch.empty(max(tot, 1), dtype=torch.int64, device="cuda:0"),
+               torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda:0"),
+               torch.empty(nb * B1, dtype=torch.int32, device="cuda:0"),
+               torch.empty(nb + 1, dtype=torch.int64, device="cuda:0"))
+        mx = ctx.join_layout_build(d.data_ptr(), st.data_ptr() + 8 * first, sz.data_ptr() + 4 * first,
+                                   count, log_b, *(t.data_ptr() for t in out))
+        assert mx <= cap
+        torch.cuda.synchronize()
+        assert int(out[3][nb].item()) == tot
+        return out, tot
+
+    T = sksffi.intersect_sym_tiles(n)
+    (a_d, a_i, a_b, a_s), _ = build(0, n)
+    (p_d, p_i, p_b, p_s), tot0 = build(0, 64)
+    (q_d, q_i, q_b, q_s), tot1 = build(64, n - 64)
+    cat_d = torch.cat([p_d[:tot0], q_d[:tot1]])
+    cat_i = torch.cat([p_i[:tot0], q_i[:tot1]])
+    cat_b = torch.cat([p_b, q_b])
+    cat_s = torch.cat([p_s[:1], q_s + tot0])
+    for layout in ((a_d, a_i, a_b, a_s), (cat_d, cat_i, cat_b, cat_s)):
+        acc = np.zeros((n, n), dtype=np.int64)
+        for (t0, t1) in [(0, 1), (1, 4), (4, T)]:
+            out = torch.full((n * n,), 7, dtype=torch.int32, device="cuda:0")
+            ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in layout), t0, t1, out.data_ptr())
+            torch.cuda.synchronize()
+            acc += out.cpu().numpy().reshape(n, n)
+        assert np.array_equal(acc, want)
