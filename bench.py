@@ -132,6 +132,59 @@ def make_c3(ctx, seed_base):
     return buf, n_bytes
 
 
+def run_end_to_end(ctx, mask, buf, steps):
+    """Config 3 from FASTA bytes in host memory (SURVEY §8d "end-to-end"): the
+    genome as a FASTA file image (80-column lines, one '>' header per contig) in
+    pinned host memory; a step = H2D copy + device strings_from_fasta
+    (sks_fasta_parse_device) + sketch build + D2H of the sketch.  The sketch
+    must equal the HBM-resident run's."""
+    contig_starts, n_bytes, _ = c3_layout()
+    parts = []
+    nl = torch.full((C3_CONTIG_LEN // 80, 1), ord("\n"), dtype=torch.uint8, device="cuda")
+    for i, s0 in enumerate(contig_starts):
+        hdr = torch.tensor(list(f">syn_3_{i}\n".encode()), dtype=torch.uint8, device="cuda")
+        body = buf[s0:s0 + C3_CONTIG_LEN].view(-1, 80)
+        parts += [hdr, torch.cat([body, nl], dim=1).reshape(-1)]
+    dev_fa = torch.cat(parts)
+    total = dev_fa.numel()
+    host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    host.copy_(dev_fa)
+    del dev_fa, parts
+    raw = torch.empty(total, dtype=torch.uint8, device="cuda")
+    stream = torch.empty(total + 1, dtype=torch.uint8, device="cuda")
+    ref = ctx.sketch_build(buf.data_ptr(), n_bytes, [0, n_bytes], W, mask, sksffi.SKS_FRAC_MOD,
+                           C3_FRAC).sketch(0)
+    out = torch.empty(len(ref) + 1, dtype=torch.int64, pin_memory=True)
+    ph = {"h2d": 0.0, "parse": 0.0, "sketch": 0.0, "d2h": 0.0}
+    tot = 0.0
+    for it in range(steps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        raw.copy_(host, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        nb, nrec = ctx.fasta_parse_device(raw.data_ptr(), total, stream.data_ptr(), total + 1)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ss = ctx.sketch_build(stream.data_ptr(), nb, [0, nb], W, mask, sksffi.SKS_FRAC_MOD, C3_FRAC)
+        t3 = time.perf_counter()
+        size = ss.copy_into(0, out.data_ptr())
+        t4 = time.perf_counter()
+        del ss
+        if it == 0:
+            got = out[:size].numpy().view(np.uint64)
+            assert nb == n_bytes and nrec == C3_CONTIGS and np.array_equal(got, ref[:, 0])
+            continue
+        for k, d in zip(ph, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            ph[k] += d / steps
+        tot += (t4 - t0) / steps
+    return {"ms": tot * 1e3, "kmers_per_s": c3_windows() / tot, "fasta_bytes": total,
+            "ms_phases": {k: v * 1e3 for k, v in ph.items()},
+            "pcie_h2d_GBps": total / ph["h2d"] / 1e9,
+            "note": "pinned host FASTA -> H2D -> sks_fasta_parse_device -> sks_sketch_build "
+                    "-> D2H sketch; sketch equals the HBM-resident run's"}
+
+
 def cpu_baseline_c3(mask, budget_bases):
     """Reference-faithful port, 1 core (the reference sketches one genome on one
     worker, kmer_set.cpp:124), on the first `budget_bases` of contig 0."""
@@ -361,6 +414,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pairs", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"))
     args = ap.parse_args()
@@ -413,6 +467,10 @@ def main():
         pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 3)),
                           warmup=1)
 
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = run_end_to_end(ctx, mask, buf, steps=2)
+
     sweep = None
     if not args.no_sweep:
         sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1)
@@ -439,6 +497,7 @@ def main():
             "cpu_baseline": cpu,
             "pairs": pairs,
             "seed_sweep": sweep,
+            "end_to_end": e2e,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

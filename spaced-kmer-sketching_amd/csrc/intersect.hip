@@ -466,7 +466,6 @@ struct JoinArgs {
   int32_t* out;
   uint64_t ld;
   uint32_t cap;  // column elements per chunk (<= kJCap): table load <= cap / kJSlots
-  int dbg;  // timing experiments only (SKS_JOIN_DEBUG): 1 = no table work, 2 = inserts only
 };
 
 // Elements of one chunk held in registers: column elements k = cs + tid + 256u
@@ -594,7 +593,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
 #pragma unroll
       for (int u = 0; u < kJMade; ++u) {
         hs[u] = kNoSlot;
-        if (a.dbg != 1 && cs + tid + kB * u < ce) {
+        if (cs + tid + kB * u < ce) {
           const uint64_t v = cur.cv[u];
           if (v == kEmpty) {
             atomicOr(&s_special, 1ull << cur.cid[u]);
@@ -632,7 +631,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
 #pragma unroll
       for (int u = 0; u < kJRowPf; ++u) {
         const uint32_t r = cur.rid[u];
-        if (r >= r_valid || a.dbg) continue;
+        if (r >= r_valid) continue;
         const uint64_t v = cur.rv[u];
         unsigned long long m;
         if (v == kEmpty) {
@@ -812,7 +811,6 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.out = out;
   ja.ld = n;
   ja.cap = join_cap();
-  ja.dbg = getenv("SKS_JOIN_DEBUG") ? atoi(getenv("SKS_JOIN_DEBUG")) : 0;
   static const uint64_t wgs = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 2048;
   const uint32_t groups =
       (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, (wgs + tiles - 1) / tiles));

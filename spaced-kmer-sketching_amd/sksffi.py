@@ -471,6 +471,11 @@ class SketchSet:
             return np.stack([buf, np.zeros_like(buf)], axis=1)
         return buf.reshape(-1, 2)
 
+    def copy_into(self, i, host_ptr):
+        """Sketch i (size * elem_words u64) into caller memory (e.g. pinned); returns size."""
+        check(lib().sks_sketch_set_copy(self.h, i, C.c_void_p(host_ptr)))
+        return int(self.sizes()[i])
+
     def device_ptrs(self):
         L = lib()
         return (L.sks_sketch_set_device_data(self.h), L.sks_sketch_set_device_starts(self.h),
