@@ -354,7 +354,9 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
     dev = "cuda" if world > 1 and os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
 
     prof = os.environ.get("SKS_SWEEP_PROFILE") is not None
-    phase = {"sketch": 0.0, "pairs": 0.0, "host": 0.0}
+    phase = {"sketch": 0.0, "pairs": 0.0}
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=1)
 
     def ani_for_seed(s):
         t0 = time.perf_counter()
@@ -368,12 +370,14 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
         counts = mat.cpu().numpy()
         t2 = time.perf_counter()
         del ss
-        size_first = np.repeat(np.diag(counts).astype(np.int32), n)
-        _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones[s])
+
+        def host_ani():  # runs beside the next seed's GPU work (ctypes drops the GIL)
+            size_first = np.repeat(np.diag(counts).astype(np.int32), n)
+            _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones[s])
+            return torch.from_numpy(ani.reshape(n, n))
         phase["sketch"] += t1 - t0
         phase["pairs"] += t2 - t1
-        phase["host"] += time.perf_counter() - t2
-        return torch.from_numpy(ani.reshape(n, n))
+        return pool.submit(host_ani)
 
     total = 0.0
     timed = 0
@@ -387,6 +391,7 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
         if it >= warmup:
             total += dt
             timed += 1
+    pool.shutdown()
     t = total / max(timed, 1)
     if prof:
         log("[sweep phases, all iterations, s]", {k: round(v, 4) for k, v in phase.items()})

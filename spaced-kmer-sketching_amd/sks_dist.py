@@ -107,8 +107,11 @@ def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
     local_seeds): the mean over all seeds of the ANI matrices, on every rank."""
     acc = torch.zeros((n_genomes, n_genomes), dtype=torch.float64, device=device)
     mine = seed_shard(n_seeds, world, rank)
-    for s in mine:
-        acc += ani_for_seed(s).to(device)
+    # ani_for_seed may return a future (host ANI of seed s overlapping the GPU
+    # work of seed s + 1); resolve all of them, then sum in seed order
+    parts = [ani_for_seed(s) for s in mine]
+    for r in parts:
+        acc += (r.result() if hasattr(r, "result") else r).to(device)
     if world > 1:
         sum_matrix(acc)
     acc /= n_seeds
