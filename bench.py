@@ -210,6 +210,51 @@ def cpu_baseline_c3(mask, budget_bases):
                       f"oracle/ref_port.cpp, {dt:.1f} s"}
 
 
+def cpu_threads():
+    """Host cores this process may use (the GPU box gives a share of a larger
+    machine: os.cpu_count() shows all of it), capped at 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_crosscheck_c3(ctx, buf, mask, sample_bytes):
+    """Optimised multi-core CPU cross-check: the oracle restatement
+    (u128 rolling windows, exact hash; oracle/sks_oracle.cpp) on the first
+    `sample_bytes` of the config-3 genome, cut into one chunk per thread with
+    (w-1)-base halos, the chunk sets unioned.  Checked equal to the GPU sketch of
+    the same prefix."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from concurrent.futures import ThreadPoolExecutor
+    T = cpu_threads()
+    host = buf[:sample_bytes].cpu().numpy().tobytes()
+    cuts = [sample_bytes * i // T for i in range(T + 1)]
+
+    def one(i):
+        a, b = cuts[i], min(sample_bytes, cuts[i + 1] + W - 1)
+        sk, nw = pyoracle.sketch(pyoracle.cut_runs(host[a:b]), W, mask, "frac", C3_FRAC)
+        return sk[:, 0], nw
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(one, range(T)))
+    union = np.unique(np.concatenate([r[0] for r in res]))
+    dt = time.perf_counter() - t0
+    windows = sum(r[1] for r in res)
+    dev = torch.empty(sample_bytes + 1, dtype=torch.uint8, device="cuda")
+    dev[:sample_bytes] = buf[:sample_bytes]
+    dev[sample_bytes] = ord("\n")
+    gpu = ctx.sketch_build(dev.data_ptr(), sample_bytes + 1, [0, sample_bytes + 1], W, mask,
+                           sksffi.SKS_FRAC_MOD, C3_FRAC)
+    assert np.array_equal(gpu.sketch(0)[:, 0], union) and int(gpu.windows()[0]) == windows
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": T, "kind": "port (optimised)",
+            "sample": f"first {sample_bytes / 1e6:.0f} MB of the config-3 genome, {T} chunks with "
+                      f"(w-1) halos, oracle/sks_oracle.cpp u128 rolling window, "
+                      f"{dt:.1f} s; set equal to the GPU's"}
+
+
 # ---- config 4 ------------------------------------------------------------------------
 def c4_genome_seeds(g):
     anc = g // (C4_GENOMES // C4_ANCESTORS)
@@ -217,7 +262,29 @@ def c4_genome_seeds(g):
     return 100 + anc, 1000 + g, desc * 0.001
 
 
-def run_pairs(ctx, world, rank, mask, steps, warmup):
+def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100):
+    """Reference-faithful pair phase on the host (oracle/ref_port.cpp: unordered_map
+    kmer_sets, probe-the-larger intersection, threads over pairs like the
+    reference's cilk_for, kmer_set.cpp:23-41,167-184) over all ordered pairs of
+    the first `n_sets` config-4 genomes' sketches (same family: sharing is high).
+    Counts are checked against the GPU matrix."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    T = cpu_threads()
+    ss = ctx.sketch_build(buf.data_ptr(), seg[n_sets], seg[:n_sets + 1], W, mask,
+                          sksffi.SKS_BOTTOM_S, C4_S)
+    sets = [pyoracle.refport_set_from_elems(ss.sketch(i), W, mask) for i in range(n_sets)]
+    t0 = time.perf_counter()
+    got = pyoracle.refport_all_pairs(sets, threads=T)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(got, counts[:n_sets, :n_sets])
+    return {"value": n_sets * n_sets / dt, "unit": "ordered pairs/s", "cores": T, "kind": "port",
+            "sample": f"all {n_sets}x{n_sets} ordered pairs of the first {n_sets} genomes "
+                      f"(s={C4_S}), oracle/ref_port.cpp, {T} threads over pairs, {dt:.2f} s; "
+                      f"counts equal the GPU's"}
+
+
+def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
     import sks_dist
     _, g0, g1 = sks_dist.block_shard(C4_GENOMES, world, rank)
     n_local = g1 - g0
@@ -307,6 +374,9 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
     if rank == 0:
         assert (counts == counts.T).all() and counts[0, 1] > 0
         assert (sizes[g0:g1] == local_sizes[:n_local]).all()
+    cpu = None
+    if cpu_pairs and rank == 0 and world == 1:
+        cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s", "scaling": "strong",
@@ -320,6 +390,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup):
                                     "join tiles split over ranks",
                    "collective": ("all_gather_into_tensor join layouts + all_reduce counts (RCCL)"
                                   if world > 1 else "none")},
+        "cpu_baseline": cpu,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
         "ms_end_to_end": (t_sketch + t_pairs) * 1e3,
     }
@@ -416,6 +487,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample-mb", type=int, default=60)
+    ap.add_argument("--cpu-crosscheck-mb", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pairs", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
@@ -470,7 +542,7 @@ def main():
     pairs = None
     if not args.no_pairs:
         pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 3)),
-                          warmup=1)
+                          warmup=1, cpu_pairs=not args.no_cpu_baseline)
 
     e2e = None
     if world == 1 and not args.no_e2e:
@@ -480,9 +552,10 @@ def main():
     if not args.no_sweep:
         sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1)
 
-    cpu = None
+    cpu = cpu_x = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_c3(mask, args.cpu_sample_mb * 1_000_000)
+        cpu_x = cpu_crosscheck_c3(ctx, buf, mask, args.cpu_crosscheck_mb * 1_000_000)
 
     if rank == 0:
         line = {
@@ -500,6 +573,7 @@ def main():
                          "kernel": "scan_kernel<frac, boost-mix>", "kernel_ms": scan_avg_ms,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "cpu_crosscheck": cpu_x,
             "pairs": pairs,
             "seed_sweep": sweep,
             "end_to_end": e2e,
