@@ -210,6 +210,57 @@ def cpu_baseline_c3(mask, budget_bases):
                       f"oracle/ref_port.cpp, {dt:.1f} s"}
 
 
+def run_c3_sharded(ctx, world, rank, mask, buf, steps, warmup):
+    """Config 3 strong scaling: ONE 3 Gb genome (rank 0's) cut into `world`
+    chunks with (w-1)-base halos; each rank sketches its chunk, the chunk sets are
+    all-gathered and unioned (sks_sketch_union).  The reference cannot split a
+    genome at all (one cilk worker per file, kmer_set.cpp:124).  Rank 0 checks
+    the result against its whole-genome sketch."""
+    import sks_dist
+    g = buf if rank == 0 else make_c3(ctx, seed_base=3)[0]
+    _, n_bytes, _ = c3_layout()
+    dev = "cuda" if os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
+
+    def build_chunk(a, b):
+        ss = ctx.sketch_build(g.data_ptr() + a, b - a, [0, b - a], W, mask, sksffi.SKS_FRAC_MOD,
+                              C3_FRAC)
+        k = int(ss.sizes()[0])
+        out = torch.empty(max(k, 1), dtype=torch.int64, device="cuda")
+        ss.export(out.data_ptr(), max(k, 1), torch.zeros(1, dtype=torch.int32,
+                                                         device="cuda").data_ptr())
+        nw = int(ss.windows()[0])
+        del ss
+        return out[:k].to(dev), nw
+
+    def union(t):
+        t = t.to("cuda").contiguous()
+        out = torch.empty_like(t)
+        k = ctx.sketch_union(t.data_ptr(), t.numel(), out.data_ptr())
+        return out[:k]
+
+    tot = 0.0
+    for it in range(warmup + steps):
+        barrier(world)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sk, nw = sks_dist.sketch_genome_sharded(n_bytes, W, world, rank, build_chunk, union, dev)
+        torch.cuda.synchronize()
+        dt = max_over_ranks(time.perf_counter() - t0, world)
+        if it >= warmup:
+            tot += dt / steps
+    assert nw == c3_windows()
+    if rank == 0:
+        whole = ctx.sketch_build(buf.data_ptr(), n_bytes, [0, n_bytes], W, mask,
+                                 sksffi.SKS_FRAC_MOD, C3_FRAC).sketch(0)[:, 0]
+        assert np.array_equal(sk.cpu().numpy().view(np.uint64), whole)
+    return {"metric": "k-mers hashed/s, one genome", "value": nw / tot, "unit": "k-mers/s",
+            "scaling": "strong", "ms_per_genome": tot * 1e3, "sketch_size": int(sk.numel()),
+            "config": {"workload": "config3 genome split across ranks ((w-1) halos), union",
+                       "collective": "all_gather of chunk sketches + all_reduce of windows"
+                       if world > 1 else "none"},
+            "check": "equals the whole-genome sketch (rank 0)"}
+
+
 def cpu_threads():
     """Host cores this process may use (the GPU box gives a share of a larger
     machine: os.cpu_count() shows all of it), capped at 16."""
@@ -492,6 +543,7 @@ def main():
     ap.add_argument("--no-pairs", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-c3-sharded", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"))
     args = ap.parse_args()
@@ -544,6 +596,10 @@ def main():
         pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 3)),
                           warmup=1, cpu_pairs=not args.no_cpu_baseline)
 
+    c3s = None
+    if not args.no_c3_sharded:
+        c3s = run_c3_sharded(ctx, world, rank, mask, buf, steps=3, warmup=1)
+
     e2e = None
     if world == 1 and not args.no_e2e:
         e2e = run_end_to_end(ctx, mask, buf, steps=2)
@@ -577,6 +633,7 @@ def main():
             "pairs": pairs,
             "seed_sweep": sweep,
             "end_to_end": e2e,
+            "c3_one_genome_sharded": c3s,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

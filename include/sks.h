@@ -222,6 +222,14 @@ int sks_intersect_sym(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_st
                       const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t tile_begin,
                       uint64_t tile_end, int32_t* d_out);
 
+/* ---- sketch union (no reference equivalent) --------------------------------------------
+ * Sorted unique union of n u64 k-mers (any order, duplicates allowed): e.g. the
+ * FracMinHash sketches of chunks of one genome cut with (w-1)-base halos, whose
+ * union is the genome's sketch (FracMinHash keeps a k-mer on its own hash).
+ * d_out holds n values; *n_out (host) = distinct values.  Narrow (w <= 32) only. */
+int sks_sketch_union(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64_t* d_out,
+                     uint64_t* n_out);
+
 /* ---- join layout: all-vs-all across GPUs ------------------------------------------------
  * The all-pairs join kernel (sks_intersect_all / _sym, SKS_INTERSECT_JOIN) reads
  * a "join layout": blocks of 64 consecutive sketches, their u64 elements

@@ -301,6 +301,37 @@ hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint6
   return hipGetLastError();
 }
 
+// Sorted unique union of n u64 values (any order, duplicates allowed) into out;
+// *n_out = number of distinct values (host, after a stream sync).  The sort runs
+// on a scratch copy; `tmp` holds it and the rocPRIM temporaries.
+hipError_t sort_unique_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* n_out,
+                           Scratch& tmp, hipStream_t s) {
+  *n_out = 0;
+  if (n == 0) return hipSuccess;
+  if (n >= (1ull << 32)) return hipErrorInvalidValue;
+  size_t sort_bytes = 0, uniq_bytes = 0;
+  hipError_t e;
+  if ((e = rocprim::radix_sort_keys(nullptr, sort_bytes, in, out, (size_t)n, 0, 64, s)) != hipSuccess)
+    return e;
+  if ((e = rocprim::unique(nullptr, uniq_bytes, out, out, (uint64_t*)nullptr, (size_t)n,
+                           rocprim::equal_to<uint64_t>(), s)) != hipSuccess)
+    return e;
+  const size_t o_sorted = 0, o_cnt = (n * 8 + 15) & ~(size_t)15, o_tmp = o_cnt + 16;
+  if ((e = tmp.reserve(o_tmp + std::max(sort_bytes, uniq_bytes))) != hipSuccess) return e;
+  char* w = static_cast<char*>(tmp.ptr);
+  uint64_t* sorted = reinterpret_cast<uint64_t*>(w + o_sorted);
+  uint64_t* d_cnt = reinterpret_cast<uint64_t*>(w + o_cnt);
+  void* t = w + o_tmp;
+  size_t tb = tmp.bytes - o_tmp;
+  if ((e = rocprim::radix_sort_keys(t, tb, in, sorted, (size_t)n, 0, 64, s)) != hipSuccess) return e;
+  tb = tmp.bytes - o_tmp;
+  if ((e = rocprim::unique(t, tb, sorted, out, d_cnt, (size_t)n, rocprim::equal_to<uint64_t>(), s)) !=
+      hipSuccess)
+    return e;
+  if ((e = hipMemcpyAsync(n_out, d_cnt, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,
                         uint64_t mut_thresh, uint64_t pos_offset, hipStream_t s) {
   if (n == 0) return hipSuccess;

@@ -201,3 +201,35 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     if world > 1:
         sum_matrix(out)
     return out
+
+
+# ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------
+# FracMinHash keeps a k-mer on its own hash, so the sketch of a genome is the
+# union of the sketches of chunks cut with (w-1)-base halos: rank r scans the
+# windows that start in [r*n/world, (r+1)*n/world), the chunk sets are
+# all-gathered (padded to the largest) and every rank forms the sorted union.
+
+def genome_chunk(n_bytes, w, world, rank):
+    a = n_bytes * rank // world
+    b = n_bytes * (rank + 1) // world
+    return a, min(n_bytes, b + w - 1) if b > a else b
+
+
+def sketch_genome_sharded(n_bytes, w, world, rank, build_chunk, union, device="cpu"):
+    """build_chunk(a, b) -> (int64 tensor of the chunk's sorted k-mers, windows);
+    union(t) -> sorted distinct values of t.  Returns (sketch, total windows) on
+    every rank."""
+    a, b = genome_chunk(n_bytes, w, world, rank)
+    vals, nw = build_chunk(a, b)
+    if world == 1:
+        return vals, nw
+    k = vals.numel()
+    kmax = max(1, _max_over(k, world, device))
+    pad = torch.zeros(kmax, dtype=torch.int64, device=device)
+    pad[:k] = vals
+    g = _gather_flat(pad, world).view(world, kmax)
+    sizes = _gather_flat(torch.tensor([k], dtype=torch.int64, device=device), world)
+    keep = torch.arange(kmax, device=device).view(1, kmax) < sizes.view(world, 1)
+    t = torch.tensor([nw], dtype=torch.int64, device=device)
+    dist.all_reduce(t)
+    return union(g[keep]), int(t.item())

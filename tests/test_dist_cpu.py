@@ -260,3 +260,48 @@ def test_block_shard_covers_whole_blocks():
                 assert (g0 % 64 == 0 or g0 == n) and (g1 == n or (g1 - g0) == bpr * 64)
                 seen += list(range(g0, g1))
             assert seen == list(range(n))
+
+
+# ---- one genome chunk-sharded across ranks (sks_dist.sketch_genome_sharded) ----------
+GENOME_LEN, GW = 250_000, 31
+
+
+def _genome():
+    g = synth.bases(GENOME_LEN, seed=91)
+    g[100_000:100_040] = ord("N")
+    return g.tobytes()
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = _genome()
+    m = O.mask(GW, 21, 0)
+
+    def build_chunk(a, b):
+        sk, nw = O.sketch(O.cut_runs(g[a:b]), GW, m, "frac", 50)
+        return torch.from_numpy(sk[:, 0].view(np.int64).copy()), nw
+    union = lambda t: torch.unique(t, sorted=True)
+    sk, nw = sks_dist.sketch_genome_sharded(len(g), GW, world, rank, build_chunk, union)
+    q.put((rank, sk.numpy(), nw))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_one_genome_sharded_gloo(world):
+    """Every rank's union of the chunk sketches equals the whole genome's sketch,
+    and the windows add up (no window counted twice across a halo)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want, nw = O.sketch(O.cut_runs(_genome()), GW, O.mask(GW, 21, 0), "frac", 50)
+    for _, sk, n in res:
+        assert np.array_equal(sk.view(np.uint64), want[:, 0]) and n == nw

@@ -231,6 +231,13 @@ def test_frac_chunk_union_property(torch_cuda, ctx):
         parts.append(ss.sketch(0))
     union = np.unique(np.concatenate([p[:, 0] for p in parts]))
     assert np.array_equal(union, S200[:, 0])
+    # the same union on the device (sks_sketch_union, used by the sharded build)
+    cat = torch.from_numpy(np.concatenate([p[:, 0] for p in parts]).view(np.int64)).to("cuda:0")
+    uo = torch.empty_like(cat)
+    k = ctx.sketch_union(cat.data_ptr(), cat.numel(), uo.data_ptr())
+    torch.cuda.synchronize()
+    assert k == len(S200) and np.array_equal(uo[:k].cpu().numpy().view(np.uint64), S200[:, 0])
+    assert ctx.sketch_union(cat.data_ptr(), 0, uo.data_ptr()) == 0
     assert int(whole.windows()[0]) == (1000 - w + 1) + (L - 1100 - w + 1)
     s1000 = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, sksffi.SKS_FRAC_MOD, 1000)
     S1000 = s1000.sketch(0)
