@@ -370,6 +370,8 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st));
   const bool has_val = bottom || S.wide;
   if (has_val) SKS_HIP(sks::compact_regions(rv, col(c, 1), d_src, d_csr, k, max_len, st));
+  // narrow bottom-s records carry the k-mer as key: hash it here (scan.hip)
+  if (bottom && !S.wide) SKS_HIP(sks::launch_fmh_narrow(col(c, 0), T, S.kconst, S.pol.flavour, st));
   if (bottom && S.wide) SKS_HIP(sks::compact_regions(rh, col(c, 2), d_src, d_csr, k, max_len, st));
 
   const int mask_lo_bits = end_bit_of(S.mask_lo);

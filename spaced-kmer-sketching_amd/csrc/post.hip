@@ -237,6 +237,12 @@ inline unsigned grid_for(uint64_t n) {
   return (unsigned)std::min<uint64_t>(std::max<uint64_t>(g, 1), 65535);
 }
 
+template <int FLAVOUR>
+__global__ void k_fmh_narrow(uint64_t* __restrict__ keys, uint64_t n, uint64_t kconst) {
+  const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (i < n) keys[i] = hash_bitset128<FLAVOUR>(keys[i], 0) ^ kconst;
+}
+
 }  // namespace
 
 hipError_t seg_sort_keys(const uint64_t* keys_in, uint64_t* keys_out, uint64_t total,
@@ -357,6 +363,17 @@ hipError_t launch_materialise(const uint8_t* seq, const uint64_t* seg_begin, uin
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_materialise, dim3(grid_for(n)), dim3(kB), 0, s, seq, seg_begin, n_seg, pos, n,
                      w, mask_lo, mask_hi, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_fmh_narrow(uint64_t* keys, uint64_t n, uint64_t kconst, int flavour,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + kB - 1) / kB;
+  if (flavour == 0)
+    hipLaunchKernelGGL(k_fmh_narrow<0>, dim3((unsigned)blocks), dim3(kB), 0, s, keys, n, kconst);
+  else
+    hipLaunchKernelGGL(k_fmh_narrow<1>, dim3((unsigned)blocks), dim3(kB), 0, s, keys, n, kconst);
   return hipGetLastError();
 }
 

@@ -366,8 +366,11 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
         emit<MODE>(p, q, g.seg, g.win0 + (uint64_t)(kWPT * tid) + j, 0);  // window start byte
       } else {
         const uint64_t c = canon(j);
+        // bottom-s: the candidate's fmh is recomputed after compaction
+        // (launch_fmh_narrow) instead of here, where the whole wave would wait
+        // on the ~45-VALU hash for the ~5% of lanes holding a candidate
         if constexpr (MODE == kModeFrac) emit<MODE>(p, q, g.seg, c, 0);
-        else emit<MODE>(p, q, g.seg, fmh_narrow<FLAVOUR>(p, c), c);
+        else emit<MODE>(p, q, g.seg, c, c);
       }
     }
 

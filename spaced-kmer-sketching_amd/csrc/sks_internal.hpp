@@ -30,7 +30,8 @@ struct ScanParams {
   // bottom-s pre-filter: keep fmh <= seg_thresh[seg]
   const uint64_t* seg_thresh;
   // output records: frac narrow key=C; frac wide key=lo val=hi;
-  // bottom narrow key=fmh val=C; bottom wide key=fmh val=lo hi=hi
+  // bottom narrow key=C (fmh filled in by launch_fmh_narrow) val=C;
+  // bottom wide key=fmh val=lo hi=hi
   uint64_t* out_key;
   uint64_t* out_val;
   uint64_t* out_hi;
@@ -160,6 +161,8 @@ hipError_t launch_materialise(const uint8_t* seq, const uint64_t* seg_begin, uin
                               const uint64_t* pos, uint64_t n, int w, uint64_t mask_lo,
                               uint64_t mask_hi, uint64_t* out, hipStream_t s);
 hipError_t launch_iota(uint64_t* out, uint64_t n, hipStream_t s);
+// keys[i] = frac_min_hash of the narrow canonical k-mer keys[i] (in place).
+hipError_t launch_fmh_narrow(uint64_t* keys, uint64_t n, uint64_t kconst, int flavour, hipStream_t s);
 hipError_t launch_gather(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
                          hipStream_t s);
 hipError_t launch_interleave(const uint64_t* lo, const uint64_t* hi, uint64_t n, uint64_t* out,
