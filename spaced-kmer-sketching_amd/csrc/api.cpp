@@ -368,10 +368,9 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
 
   // dense columns
   SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st));
-  const bool has_val = bottom || S.wide;
+  // narrow bottom-s records carry the k-mer as key (its fmh is recomputed here)
+  const bool has_val = S.wide || (bottom && S.wide);
   if (has_val) SKS_HIP(sks::compact_regions(rv, col(c, 1), d_src, d_csr, k, max_len, st));
-  // narrow bottom-s records carry the k-mer as key: hash it here (scan.hip)
-  if (bottom && !S.wide) SKS_HIP(sks::launch_fmh_narrow(col(c, 0), T, S.kconst, S.pol.flavour, st));
   if (bottom && S.wide) SKS_HIP(sks::compact_regions(rh, col(c, 2), d_src, d_csr, k, max_len, st));
 
   const int mask_lo_bits = end_bit_of(S.mask_lo);
@@ -419,6 +418,54 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
 
   // bottom-s
   const uint64_t s = S.pol.param;
+  if (!S.wide) {
+    // sort the candidate k-mers, unique them, then select the s with the smallest
+    // (fmh, k-mer) per genome in LDS (k_bottom_select, post.hip): one key-only
+    // sort instead of a (fmh, k-mer) pair sort followed by a second sort
+    SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, mask_lo_bits, c->tmp, st));
+    SKS_HIP(sks::seg_unique_scan(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos, d_uniq,
+                                 c->tmp, st));
+    SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    SKS_HIP(hipStreamSynchronize(st));
+    uint64_t max_keep_uniq = 0;
+    for (uint32_t i = 0; i < k; ++i)
+      if (uniq[i] >= s || thresh[ok[i]] == ~0ull) max_keep_uniq = std::max(max_keep_uniq, uniq[i]);
+    if (max_keep_uniq <= sks::bottom_select_capacity()) {
+      std::vector<uint64_t> limit(k, 0);
+      std::vector<uint32_t> keep_segs;
+      std::vector<uint64_t> keep_off(1, 0);
+      for (uint32_t i = 0; i < k; ++i) {
+        if (uniq[i] >= s || thresh[ok[i]] == ~0ull) {
+          limit[i] = std::min<uint64_t>(s, uniq[i]);
+          final_size_local[ok[i]] = limit[i];
+          keep_segs.push_back(seg_ids[ok[i]]);
+          keep_off.push_back(keep_off.back() + limit[i]);
+        } else {
+          retry_local.push_back(ok[i]);  // too few candidates under the threshold
+        }
+      }
+      std::vector<uint64_t> dst = prefix(limit), uoff = prefix(uniq);
+      const uint64_t U = dst[k];
+      // every distinct candidate, contiguous per genome at uoff
+      SKS_HIP(sks::seg_unique_scatter(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos,
+                                      nullptr, nullptr, col(c, 5), nullptr, st));
+      MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
+      size_t o_uoff = arena2.add(uoff), o_lim = arena2.add(limit), o_dst = arena2.add(dst);
+      SKS_TRY(arena2.upload());
+      SKS_TRY(alloc_u64(&po.d, U));
+      po.segs = keep_segs;
+      po.off = keep_off;
+      SKS_HIP(sks::launch_bottom_select(col(c, 5), arena2.ptr(o_uoff), arena2.ptr(o_dst),
+                                        arena2.ptr(o_lim), k, S.kconst, S.pol.flavour, po.d, st));
+      SKS_HIP(hipStreamSynchronize(st));
+      passes.push_back(po);
+      return SKS_OK;
+    }
+    // a genome with more distinct candidates than the LDS select holds: the
+    // general path below, on (fmh, k-mer) pairs
+    SKS_HIP(hipMemcpyAsync(col(c, 1), col(c, 0), T * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    SKS_HIP(sks::launch_fmh_narrow(col(c, 0), T, S.kconst, S.pol.flavour, st));
+  }
   const uint64_t* LO;  // columns ordered by (fmh, C)
   const uint64_t* HI = nullptr;
   if (!S.wide) {

@@ -38,6 +38,7 @@ namespace {
 
 constexpr int kB = 256;
 constexpr uint64_t kBigSegment = 1ull << 21;  // device-wide sort per segment above this
+constexpr uint32_t kSelCap = 18432;  // distinct candidates per genome k_bottom_select holds in LDS
 
 template <bool PAIRS>
 hipError_t sort_impl(const uint64_t* keys_in, uint64_t* keys_out, const uint64_t* vals_in,
@@ -237,6 +238,108 @@ inline unsigned grid_for(uint64_t n) {
   return (unsigned)std::min<uint64_t>(std::max<uint64_t>(g, 1), 65535);
 }
 
+// ---- bottom-s selection over C-sorted unique candidates ---------------------------------
+// One workgroup per genome.  The genome's distinct candidate k-mers arrive sorted
+// by value; their fmh values are computed into LDS, the s-th smallest fmh F* is
+// found by an 8-bit-digit radix select, and the kept k-mers — fmh < F*, plus the
+// first (in k-mer order) of those with fmh == F* up to s — are written in
+// k-mer order: exactly the s distinct k-mers with the smallest (fmh, k-mer).
+constexpr int kSelB = 1024;
+constexpr int kSelWaves = kSelB / 64;
+
+// exclusive block scan of a predicate; returns this thread's rank, *total = count
+__device__ __forceinline__ uint32_t block_rank(bool p, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t bal = __ballot(p);
+  const uint32_t in_wave = (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+  if (lane == 0) wsum[wave] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) {
+    const uint32_t c = wsum[w];
+    before += w < wave ? c : 0u;
+    all += c;
+  }
+  __syncthreads();
+  *total = all;
+  return before + in_wave;
+}
+
+template <int FLAVOUR>
+__global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restrict__ uk,
+                                                         const uint64_t* __restrict__ uoff,
+                                                         const uint64_t* __restrict__ dst_off,
+                                                         const uint64_t* __restrict__ limit,
+                                                         uint64_t kconst,
+                                                         uint64_t* __restrict__ out) {
+  extern __shared__ uint64_t f[];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t wsum[kSelWaves];
+  __shared__ uint32_t s_digit, s_below;
+  const uint32_t g = blockIdx.x;
+  const uint64_t b = uoff[g], n = uoff[g + 1] - b;
+  const uint64_t lim = limit[g];
+  const int tid = threadIdx.x;
+  if (lim == 0) return;
+  uint64_t* dst = out + dst_off[g];
+  if (n <= lim) {  // every distinct candidate is kept
+    for (uint64_t i = tid; i < n; i += kSelB) dst[i] = uk[b + i];
+    return;
+  }
+  for (uint64_t i = tid; i < n; i += kSelB) f[i] = hash_bitset128<FLAVOUR>(uk[b + i], 0) ^ kconst;
+  uint64_t prefix = 0, pmask = 0;
+  uint32_t k = (uint32_t)lim;  // rank (1-based) of the wanted fmh among the prefix matches
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kSelB) hist[i] = 0;
+    __syncthreads();
+    for (uint64_t i = tid; i < n; i += kSelB) {
+      const uint64_t v = f[i];
+      if ((v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: the digit where the running count reaches k
+      uint32_t h4[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { h4[q] = hist[4 * tid + q]; sum += h4[q]; }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += t;
+      }
+      const uint64_t bal = __ballot(incl >= k);
+      const int L = __builtin_ctzll(bal);
+      if (tid == L) {
+        uint32_t c = incl - sum;
+        int q = 0;
+        while (c + h4[q] < k) c += h4[q++];
+        s_digit = 4 * L + q;
+        s_below = c;
+      }
+    }
+    __syncthreads();
+    prefix |= (uint64_t)s_digit << shift;
+    pmask |= 255ull << shift;
+    k -= s_below;
+    __syncthreads();
+  }
+  // prefix = F*; keep fmh < F* and the first k with fmh == F*, in k-mer order
+  uint32_t eq_base = 0, out_base = 0;
+  for (uint64_t base = 0; base < n; base += kSelB) {
+    const uint64_t i = base + tid;
+    const uint64_t v = i < n ? f[i] : ~0ull;
+    const bool eq = i < n && v == prefix;
+    uint32_t eq_tot, keep_tot;
+    const uint32_t eq_rank = eq_base + block_rank(eq, wsum, &eq_tot);
+    const bool keep = i < n && (v < prefix || (eq && eq_rank < k));
+    const uint32_t pos = out_base + block_rank(keep, wsum, &keep_tot);
+    if (keep) dst[pos] = uk[b + i];
+    eq_base += eq_tot;
+    out_base += keep_tot;
+  }
+}
+
 template <int FLAVOUR>
 __global__ void k_fmh_narrow(uint64_t* __restrict__ keys, uint64_t n, uint64_t kconst) {
   const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
@@ -374,6 +477,28 @@ hipError_t launch_fmh_narrow(uint64_t* keys, uint64_t n, uint64_t kconst, int fl
     hipLaunchKernelGGL(k_fmh_narrow<0>, dim3((unsigned)blocks), dim3(kB), 0, s, keys, n, kconst);
   else
     hipLaunchKernelGGL(k_fmh_narrow<1>, dim3((unsigned)blocks), dim3(kB), 0, s, keys, n, kconst);
+  return hipGetLastError();
+}
+
+uint32_t bottom_select_capacity() { return kSelCap; }
+
+hipError_t launch_bottom_select(const uint64_t* uk, const uint64_t* d_uoff, const uint64_t* d_dst,
+                                const uint64_t* d_lim, uint32_t n_seg, uint64_t kconst,
+                                int flavour, uint64_t* out, hipStream_t s) {
+  if (n_seg == 0) return hipSuccess;
+  const size_t lds = (size_t)kSelCap * sizeof(uint64_t);
+  static const hipError_t a0 = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_bottom_select<0>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const hipError_t a1 = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_bottom_select<1>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (a0 != hipSuccess) return a0;
+  if (a1 != hipSuccess) return a1;
+  if (flavour == 0)
+    hipLaunchKernelGGL(k_bottom_select<0>, dim3(n_seg), dim3(kSelB), lds, s, uk, d_uoff, d_dst, d_lim,
+                       kconst, out);
+  else
+    hipLaunchKernelGGL(k_bottom_select<1>, dim3(n_seg), dim3(kSelB), lds, s, uk, d_uoff, d_dst, d_lim,
+                       kconst, out);
   return hipGetLastError();
 }
 

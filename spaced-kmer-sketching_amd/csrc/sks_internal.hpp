@@ -161,6 +161,14 @@ hipError_t launch_materialise(const uint8_t* seq, const uint64_t* seg_begin, uin
                               const uint64_t* pos, uint64_t n, int w, uint64_t mask_lo,
                               uint64_t mask_hi, uint64_t* out, hipStream_t s);
 hipError_t launch_iota(uint64_t* out, uint64_t n, hipStream_t s);
+// Bottom-s from C-sorted distinct candidates (uk, segment g at [uoff[g], uoff[g+1])):
+// writes the min(limit[g], n_g) k-mers with the smallest (fmh, k-mer), in k-mer
+// order, to out + dst[g].  Needs every n_g with limit[g] > 0 to be at most
+// bottom_select_capacity().
+uint32_t bottom_select_capacity();
+hipError_t launch_bottom_select(const uint64_t* uk, const uint64_t* d_uoff, const uint64_t* d_dst,
+                                const uint64_t* d_lim, uint32_t n_seg, uint64_t kconst,
+                                int flavour, uint64_t* out, hipStream_t s);
 // keys[i] = frac_min_hash of the narrow canonical k-mer keys[i] (in place).
 hipError_t launch_fmh_narrow(uint64_t* keys, uint64_t n, uint64_t kconst, int flavour, hipStream_t s);
 hipError_t launch_gather(const uint64_t* src, const uint64_t* idx, uint64_t n, uint64_t* out,
