@@ -145,6 +145,21 @@ def test_bottom_s(torch_cuda, ctx, w, k):
             check_against_oracle(ss, genomes, w, m, "bottom", s, flavour)
 
 
+def test_bottom_s_many_genomes(torch_cuda, ctx):
+    """300 genomes in one build (one select workgroup each), related and
+    unrelated, lengths around the candidate margin, both flavours."""
+    genomes = []
+    for i in range(300):
+        L = 2000 + 517 * (i % 41)
+        genomes.append(synth.bases(L, seed=800 + i % 7, mut_seed=1200 + i,
+                                   mut_rate=0.01 * (i % 5)).tobytes())
+    m = O.mask(31, 21, 2)
+    for flavour in (0, 1):
+        for s_ in (1, 200, 1500):
+            ss, _ = build(torch_cuda, ctx, genomes, 31, m, "bottom", s_, flavour)
+            check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
+
+
 def test_bottom_s_low_complexity_forces_threshold_retry(torch_cuda, ctx):
     # periodic genome: few distinct k-mers, so the first threshold pass finds
     # fewer than s candidates and the build must raise the threshold
