@@ -1088,6 +1088,14 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
   if (!d_out_bstart || (n && (!d_starts || !d_sizes || !d_out_boff)))
     return sks::fail(SKS_E_ARG, "sks_join_layout_build: null argument");
   DeviceGuard g(c->device);
+  if (n) {  // bucket starts are u32: the layout must hold < 2^32 elements
+    std::vector<uint32_t> h_sizes(n);
+    SKS_HIP(hipMemcpy(h_sizes.data(), d_sizes, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint64_t total = 0;
+    for (uint32_t v : h_sizes) total += v;
+    if (total >= (1ull << 32))
+      return sks::fail(SKS_E_UNSUPPORTED, "sks_join_layout_build: >= 2^32 elements in one layout");
+  }
   const size_t tmp = sks::join_layout_temp_bytes(n, log_b);
   SKS_HIP(c->iwork.reserve(tmp + 64));
   char* w = static_cast<char*>(c->iwork.ptr);

@@ -886,7 +886,11 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
 
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) total += h_sizes[i];
-  if (algo != kIntersectMerge && total < (1ull << 32)) {
+  // the join's per-(block, bucket, slot) counting arrays take 8 B x 64 x B per
+  // block; beyond a few GB of them (very many sketches) the merge tiles are used
+  const bool join_fits = total < (1ull << 32) &&
+                         join_layout_temp_bytes(n, join_log_b(max_size)) < (8ull << 30);
+  if (algo != kIntersectMerge && join_fits) {
     // hash-bucketed block-major copy of the column sketches (and of the row
     // range when its blocks are not aligned with the column blocks), then k_join
     const bool sep_rows = !sym && (row_begin % kTile) != 0;
