@@ -57,7 +57,16 @@ static int sketch(int argc, char** argv) {
   }
   bool same = true;
   for (int i = 0; i < n; ++i) same = same && data[i].elements == serial[i].elements;
-  std::printf("],\"serial_equal\":%s,\"inter\":[", same ? "true" : "false");
+  std::printf("],\"serial_equal\":%s,", same ? "true" : "false");
+  if (!same) {  // diagnostics: the serial build's sets
+    std::printf("\"serial_sets\":[");
+    for (int i = 0; i < n; ++i) {
+      if (i) std::printf(",");
+      hexset(serial[i]);
+    }
+    std::printf("],");
+  }
+  std::printf("\"inter\":[");
   for (size_t i = 0; i < inter.size(); ++i) std::printf("%s%d", i ? "," : "", inter[i]);
   std::printf("],\"inter_serial_equal\":%s,\"ani\":[", inter == inter2 ? "true" : "false");
   for (size_t i = 0; i < inter.size(); ++i) {

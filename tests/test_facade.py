@@ -66,7 +66,8 @@ def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
     n = len(files)
     inter = [O.intersect(sk[i], sk[j]) for i in range(n) for j in range(n)]
     assert out["inter"] == inter
-    assert out["serial_equal"] and out["inter_serial_equal"] and out["runs_equal"] and out["cut_equal"]
+    for flag in ("serial_equal", "inter_serial_equal", "runs_equal", "cut_equal"):
+        assert out[flag], flag
     assert out["single01"] == inter[1]
     kk = bin(m).count("1") // 2
     assert out["k"] == kk
