@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <random>
 #include <string>
@@ -132,18 +133,110 @@ std::vector<uint64_t> prefix(const std::vector<uint64_t>& v) {
 // One completed pass: final sketches of `segs` (global segment ids) in CSR.
 struct PassOut {
   uint64_t* d = nullptr;          // elements (elem_words u64 each)
+  size_t bytes = 0;               // allocation size of d
   std::vector<uint32_t> segs;
   std::vector<uint64_t> off;      // CSR in elements, size segs.size() + 1
 };
 
+// Device block cache for sketch arrays. hipFree of a sketch-sized array unmaps
+// it (≈160 us for config 3's 24 MB set, measured with --hip-trace), more than
+// the build's whole host-side post-processing; released arrays are parked here
+// and handed to later builds instead. Blocks are plain hipMalloc memory.
+struct CachedBlock {
+  int device;
+  void* p;
+  size_t bytes;
+};
+std::mutex g_cache_mu;
+void trim_device_cache(int device);
+std::vector<CachedBlock> g_cache;  // most recently released last
+constexpr size_t kCacheMaxBlocks = 16;
+constexpr size_t kCacheMaxBytes = size_t(4) << 30;
+
+size_t cache_bytes_locked() {
+  size_t t = 0;
+  for (const auto& b : g_cache) t += b.bytes;
+  return t;
+}
+
+int current_device() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d;
+}
+
+// A cached block of at least `bytes` (and at most 2x + 1 MB, so a small request
+// does not pin a large block), or a fresh hipMalloc.
+hipError_t dev_alloc(void** p, size_t bytes) {
+  bytes = std::max<size_t>(bytes, 8);
+  const int dev = current_device();
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    size_t best = g_cache.size();
+    for (size_t i = 0; i < g_cache.size(); ++i) {
+      const CachedBlock& b = g_cache[i];
+      if (b.device != dev || b.bytes < bytes || b.bytes > 2 * bytes + (size_t(1) << 20)) continue;
+      if (best == g_cache.size() || b.bytes < g_cache[best].bytes) best = i;
+    }
+    if (best != g_cache.size()) {
+      *p = g_cache[best].p;
+      g_cache.erase(g_cache.begin() + best);
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory) {  // give the cache back and retry once
+    (void)hipGetLastError();
+    trim_device_cache(dev);
+    e = hipMalloc(p, bytes);
+  }
+  return e;
+}
+
+// Parks a block whose last use has completed (the caller guarantees it; see
+// sks_sketch_set_free); evicts the oldest blocks beyond the cache limits.
+void dev_release(void* p, size_t bytes) {
+  if (!p) return;
+  std::vector<void*> evict;
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_cache.push_back({current_device(), p, std::max<size_t>(bytes, 8)});
+    while (g_cache.size() > kCacheMaxBlocks ||
+           (g_cache.size() > 1 && cache_bytes_locked() > kCacheMaxBytes)) {
+      evict.push_back(g_cache.front().p);
+      g_cache.erase(g_cache.begin());
+    }
+  }
+  for (void* q : evict) (void)hipFree(q);
+}
+
+void trim_device_cache(int device) {
+  std::vector<void*> drop;
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (size_t i = 0; i < g_cache.size();) {
+      if (g_cache[i].device == device) {
+        drop.push_back(g_cache[i].p);
+        g_cache.erase(g_cache.begin() + i);
+      } else {
+        ++i;
+      }
+    }
+  }
+  for (void* q : drop) (void)hipFree(q);
+}
+
+// Pass buffers are only used on the ctx stream, synchronised before this runs.
 void free_passes(std::vector<PassOut>& passes) {
   for (auto& p : passes)
-    if (p.d) (void)hipFree(p.d);
+    if (p.d) dev_release(p.d, p.bytes);
   passes.clear();
 }
 
-int alloc_u64(uint64_t** p, uint64_t words) {
-  SKS_HIP(hipMalloc(reinterpret_cast<void**>(p), std::max<uint64_t>(words, 1) * sizeof(uint64_t)));
+int alloc_u64(uint64_t** p, uint64_t words, size_t* bytes_out = nullptr) {
+  const size_t bytes = std::max<uint64_t>(words, 1) * sizeof(uint64_t);
+  SKS_HIP(dev_alloc(reinterpret_cast<void**>(p), bytes));
+  if (bytes_out) *bytes_out = bytes;
   return SKS_OK;
 }
 
@@ -265,6 +358,7 @@ int sks_ctx_destroy(sks_ctx* c) {
   c->meta.release();
   c->iwork.release();
   c->ingress.release();
+  trim_device_cache(c->device);
   (void)hipEventDestroy(c->ev_begin);
   (void)hipEventDestroy(c->ev_end);
   (void)hipEventDestroy(c->ev_s0);
@@ -366,8 +460,11 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   const uint64_t* rv = reinterpret_cast<uint64_t*>(c->rec[1].ptr);
   const uint64_t* rh = reinterpret_cast<uint64_t*>(c->rec[2].ptr);
 
-  // dense columns
-  SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st));
+  // dense columns; narrow keys are packed to their mask bits for the sorts
+  // (sks::BitRuns) and expanded again when the unique elements are scattered
+  const sks::BitRuns runs = S.wide ? sks::BitRuns{} : sks::bit_runs(S.mask_lo);
+  const int key_bits = S.wide ? 64 : std::max(1, __builtin_popcountll(S.mask_lo));
+  SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st, &runs));
   // narrow bottom-s records carry the k-mer as key (its fmh is recomputed here)
   const bool has_val = S.wide || (bottom && S.wide);
   if (has_val) SKS_HIP(sks::compact_regions(rv, col(c, 1), d_src, d_csr, k, max_len, st));
@@ -386,7 +483,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     const uint64_t* K;   // sorted unique columns source
     const uint64_t* K2 = nullptr;
     if (!S.wide) {
-      SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, mask_lo_bits, c->tmp, st));
+      SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, key_bits, c->tmp, st));
       K = col(c, 3);
     } else {
       // (lo, hi) -> sort by lo, then stable by hi  => ascending 128-bit order
@@ -402,10 +499,10 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     SKS_HIP(hipStreamSynchronize(st));
     po.off = prefix(uniq);
     const uint64_t U = po.off[k];
-    SKS_TRY(alloc_u64(&po.d, U * S.ew));
+    SKS_TRY(alloc_u64(&po.d, U * S.ew, &po.bytes));
     if (!S.wide) {
       SKS_HIP(sks::seg_unique_scatter(K, nullptr, T, max_len, d_csr, k, d_flag, d_pos, nullptr, nullptr,
-                                      po.d, nullptr, st));
+                                      po.d, nullptr, st, &runs));
     } else {
       SKS_HIP(sks::seg_unique_scatter(K2, K, T, max_len, d_csr, k, d_flag, d_pos, nullptr, nullptr,
                                       col(c, 7), col(c, 8), st));
@@ -422,7 +519,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     // sort the candidate k-mers, unique them, then select the s with the smallest
     // (fmh, k-mer) per genome in LDS (k_bottom_select, post.hip): one key-only
     // sort instead of a (fmh, k-mer) pair sort followed by a second sort
-    SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, mask_lo_bits, c->tmp, st));
+    SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, key_bits, c->tmp, st));
     SKS_HIP(sks::seg_unique_scan(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos, d_uniq,
                                  c->tmp, st));
     SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -448,11 +545,11 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
       const uint64_t U = dst[k];
       // every distinct candidate, contiguous per genome at uoff
       SKS_HIP(sks::seg_unique_scatter(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos,
-                                      nullptr, nullptr, col(c, 5), nullptr, st));
+                                      nullptr, nullptr, col(c, 5), nullptr, st, &runs));
       MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
       size_t o_uoff = arena2.add(uoff), o_lim = arena2.add(limit), o_dst = arena2.add(dst);
       SKS_TRY(arena2.upload());
-      SKS_TRY(alloc_u64(&po.d, U));
+      SKS_TRY(alloc_u64(&po.d, U, &po.bytes));
       po.segs = keep_segs;
       po.off = keep_off;
       SKS_HIP(sks::launch_bottom_select(col(c, 5), arena2.ptr(o_uoff), arena2.ptr(o_dst),
@@ -463,6 +560,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     }
     // a genome with more distinct candidates than the LDS select holds: the
     // general path below, on (fmh, k-mer) pairs
+    SKS_HIP(sks::launch_bits_expand(col(c, 0), T, runs, st));
     SKS_HIP(hipMemcpyAsync(col(c, 1), col(c, 0), T * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     SKS_HIP(sks::launch_fmh_narrow(col(c, 0), T, S.kconst, S.pol.flavour, st));
   }
@@ -516,7 +614,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   d_csr = arena2.ptr(o_csr2);
   uint64_t* d_lim = arena2.ptr(o_lim);
   uint64_t* d_dst = arena2.ptr(o_dst);
-  SKS_TRY(alloc_u64(&po.d, U * S.ew));
+  SKS_TRY(alloc_u64(&po.d, U * S.ew, &po.bytes));
   po.segs = keep_segs;
   po.off = keep_off;
   if (!S.wide) {
@@ -769,9 +867,9 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
     }
   }
   if (rc == SKS_OK) rc = alloc_u64(&set->d_starts, n_seg);
-  if (rc == SKS_OK && hipMalloc(reinterpret_cast<void**>(&set->d_sizes),
+  if (rc == SKS_OK && dev_alloc(reinterpret_cast<void**>(&set->d_sizes),
                                 std::max<uint32_t>(n_seg, 1) * sizeof(uint32_t)) != hipSuccess)
-    rc = sks::fail(SKS_E_HIP, "sks_sketch_build: hipMalloc failed");
+    rc = sks::fail(SKS_E_HIP, "sks_sketch_build: device allocation failed");
   if (rc == SKS_OK && n_seg) {
     if (hipMemcpyAsync(set->d_starts, set->starts.data(), n_seg * sizeof(uint64_t),
                        hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -801,9 +899,14 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
 int sks_sketch_set_free(sks_sketch_set* set) {
   if (!set) return SKS_OK;
   DeviceGuard g(set->device);
-  if (set->d_data) (void)hipFree(set->d_data);
-  if (set->d_starts) (void)hipFree(set->d_starts);
-  if (set->d_sizes) (void)hipFree(set->d_sizes);
+  // hipFree's contract: work queued on the arrays (any stream) completes before
+  // they are reused; then they go to the block cache instead of being unmapped
+  if (set->d_data || set->d_starts || set->d_sizes) (void)hipDeviceSynchronize();
+  uint64_t total = 0;
+  for (uint32_t v : set->sizes) total += v;
+  dev_release(set->d_data, std::max<uint64_t>(total * set->elem_words, 1) * 8);
+  dev_release(set->d_starts, std::max<uint32_t>(set->n, 1) * 8);
+  dev_release(set->d_sizes, std::max<uint32_t>(set->n, 1) * 4);
   delete set;
   return SKS_OK;
 }

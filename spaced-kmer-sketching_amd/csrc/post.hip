@@ -93,13 +93,32 @@ hipError_t sort_impl(const uint64_t* keys_in, uint64_t* keys_out, const uint64_t
                                               (unsigned)n_seg, d_off, d_off + 1, 0, end_bit, s);
 }
 
+__device__ __forceinline__ uint64_t runs_pack(uint64_t x, const BitRuns& r) {
+  uint64_t o = 0;
+  for (uint32_t i = 0; i < r.n; ++i) o |= ((x >> r.src[i]) & r.bits[i]) << r.dst[i];
+  return o;
+}
+
+__device__ __forceinline__ uint64_t runs_expand(uint64_t x, const BitRuns& r) {
+  uint64_t o = 0;
+  for (uint32_t i = 0; i < r.n; ++i) o |= ((x >> r.dst[i]) & r.bits[i]) << r.src[i];
+  return o;
+}
+
+template <bool PACK>
 __global__ void k_compact(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
-                          const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ dst_off) {
+                          const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ dst_off,
+                          const BitRuns runs) {
   const uint32_t g = blockIdx.y;
   const uint64_t len = dst_off[g + 1] - dst_off[g];
   const uint64_t so = src_off[g], d0 = dst_off[g];
   for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < len; i += (uint64_t)gridDim.x * kB)
-    dst[d0 + i] = src[so + i];
+    dst[d0 + i] = PACK ? runs_pack(src[so + i], runs) : src[so + i];
+}
+
+__global__ void k_bits_expand(uint64_t* __restrict__ keys, uint64_t n, const BitRuns runs) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kB)
+    keys[i] = runs_expand(keys[i], runs);
 }
 
 __global__ void k_flags(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ keys2,
@@ -118,11 +137,12 @@ __global__ void k_uniq_counts(const uint64_t* __restrict__ pos, const uint64_t* 
   if (g < n_seg) uniq[g] = pos[off[g + 1]] - pos[off[g]];
 }
 
+template <bool EXPAND>
 __global__ void k_scatter(const uint64_t* __restrict__ vals, const uint64_t* __restrict__ vals2,
                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ flag,
                           const uint64_t* __restrict__ pos, const uint64_t* __restrict__ limit,
                           const uint64_t* __restrict__ dst_off, uint64_t* __restrict__ out,
-                          uint64_t* __restrict__ out2) {
+                          uint64_t* __restrict__ out2, const BitRuns runs) {
   const uint32_t g = blockIdx.y;
   const uint64_t b = off[g], e = off[g + 1];
   const uint64_t p0 = pos[b], lim = limit ? limit[g] : ~0ull, d0 = dst_off ? dst_off[g] : p0;
@@ -130,7 +150,7 @@ __global__ void k_scatter(const uint64_t* __restrict__ vals, const uint64_t* __r
     if (!flag[i]) continue;
     uint64_t r = pos[i] - p0;
     if (r < lim) {
-      out[d0 + r] = vals[i];
+      out[d0 + r] = EXPAND ? runs_expand(vals[i], runs) : vals[i];
       if (out2) out2[d0 + r] = vals2[i];
     }
   }
@@ -364,10 +384,41 @@ hipError_t seg_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const uin
 
 hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d_src_off,
                            const uint64_t* d_dst_off, uint32_t n_seg, uint64_t max_len,
-                           hipStream_t s) {
+                           hipStream_t s, const BitRuns* pack) {
   if (n_seg == 0 || max_len == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_compact, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, src, dst,
-                     d_src_off, d_dst_off);
+  if (pack && pack->n)
+    hipLaunchKernelGGL(k_compact<true>, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, src, dst,
+                       d_src_off, d_dst_off, *pack);
+  else
+    hipLaunchKernelGGL(k_compact<false>, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, src, dst,
+                       d_src_off, d_dst_off, BitRuns{});
+  return hipGetLastError();
+}
+
+BitRuns bit_runs(uint64_t mask) {
+  BitRuns r;
+  int at = 0;
+  for (int b = 0; b < 64;) {
+    if (!((mask >> b) & 1)) {
+      ++b;
+      continue;
+    }
+    int e = b;
+    while (e < 64 && ((mask >> e) & 1)) ++e;
+    const int len = e - b;
+    r.src[r.n] = (uint8_t)b;
+    r.dst[r.n] = (uint8_t)at;
+    r.bits[r.n] = len == 64 ? ~0ull : ((1ull << len) - 1);
+    ++r.n;
+    at += len;
+    b = e;
+  }
+  return r;
+}
+
+hipError_t launch_bits_expand(uint64_t* keys, uint64_t n, const BitRuns& runs, hipStream_t s) {
+  if (n == 0 || runs.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bits_expand, dim3(grid_for(n)), dim3(kB), 0, s, keys, n, runs);
   return hipGetLastError();
 }
 
@@ -402,11 +453,15 @@ hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint6
                               const uint32_t* d_flag,
                               const uint64_t* d_pos, const uint64_t* d_limit,
                               const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
-                              hipStream_t s) {
+                              hipStream_t s, const BitRuns* expand) {
   if (n_seg == 0 || total == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter, dim3(grid_for(std::min<uint64_t>(max_len, 1ull << 24)), n_seg),
-                     dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos, d_limit, d_dst_off, out,
-                     out2);
+  const dim3 grid(grid_for(std::min<uint64_t>(max_len, 1ull << 24)), n_seg);
+  if (expand && expand->n)
+    hipLaunchKernelGGL(k_scatter<true>, grid, dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos,
+                       d_limit, d_dst_off, out, out2, *expand);
+  else
+    hipLaunchKernelGGL(k_scatter<false>, grid, dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos,
+                       d_limit, d_dst_off, out, out2, BitRuns{});
   return hipGetLastError();
 }
 

@@ -63,10 +63,24 @@ hipError_t seg_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const uin
                           uint64_t* vals_out, uint64_t total, const std::vector<uint64_t>& host_off,
                           const uint64_t* d_off, int end_bit, Scratch& tmp, hipStream_t s);
 
-// Compact sparse survivor regions [off[g], off[g] + cnt[g]) into dense CSR.
+// Maximal runs of set bits of a 64-bit k-mer mask. Masked k-mers only have
+// mask bits set, so gathering those bits into the low popcount(mask) bits
+// (a pext) is order-preserving and injective: the post-scan sorts then run
+// ceil(popcount / 8) radix passes instead of ceil(top bit / 8)
+// (config 3, w=31/k=21: 42 bits instead of 62, 6 passes instead of 8).
+struct BitRuns {
+  uint32_t n = 0;           // 0: identity
+  uint8_t src[32], dst[32];  // run start in the k-mer / in the packed key
+  uint64_t bits[32];         // low-aligned run masks
+};
+BitRuns bit_runs(uint64_t mask);
+hipError_t launch_bits_expand(uint64_t* keys, uint64_t n, const BitRuns& runs, hipStream_t s);
+
+// Compact sparse survivor regions [off[g], off[g] + cnt[g]) into dense CSR,
+// packing each value's mask bits when `pack` is given.
 hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d_src_off,
                            const uint64_t* d_dst_off, uint32_t n_seg, uint64_t max_len,
-                           hipStream_t s);
+                           hipStream_t s, const BitRuns* pack = nullptr);
 
 // Per-segment unique of sorted keys (optionally by a (key, key2) pair):
 // writes d_flag_pos (exclusive scan of "first of run" flags) and per-segment
@@ -87,7 +101,7 @@ hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint6
                               const uint32_t* d_flag,
                               const uint64_t* d_pos, const uint64_t* d_limit,
                               const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
-                              hipStream_t s);
+                              hipStream_t s, const BitRuns* expand = nullptr);
 
 // ---- intersection (intersect.hip) ---------------------------------------------------
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
