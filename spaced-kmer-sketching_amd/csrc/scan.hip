@@ -537,6 +537,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
   wflush(count_seg);
 }
 
+constexpr int kGridOversubscribe = 16;
+
 template <class K>
 int occupancy_grid(K kernel, int device) {
   int per_cu = 0;
@@ -556,7 +558,12 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
                        hipStream_t stream, int grid_override) {
   if (p.n_tiles == 0) return hipSuccess;
   auto pick = [&](auto kernel) -> hipError_t {
-    int grid = grid_override > 0 ? grid_override : occupancy_grid(kernel, device);
+    // Oversubscribe the resident slots 16x (config 3: 16384 workgroups of ~45
+    // tiles): the workgroup dispatcher then refills CUs as ranges finish, which
+    // evens out per-CU speed differences and keeps every SIMD at its wave limit
+    // (the occupancy query reports 4 workgroups per CU; LDS allows 6). Measured
+    // on config 3 (tools/scan_grid_sweep.py): 5.95 ms at 1x, 5.19 ms at 8x-16x.
+    int grid = grid_override > 0 ? grid_override : kGridOversubscribe * occupancy_grid(kernel, device);
     if ((uint64_t)grid > p.n_tiles) grid = (int)p.n_tiles;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, p);
     return hipGetLastError();
