@@ -262,6 +262,53 @@ def test_frac_chunk_union_property(torch_cuda, ctx):
         assert sksffi.frac_min_hash(int(x), m, w, 1, 0) % 1000 == 0
 
 
+def test_concurrent_contexts_on_streams(torch_cuda, ctx):
+    """bench.py's headline mode: builds from several host threads, one context
+    per HIP stream, in flight together (and sets freed while another thread
+    builds) give the serial build's sketches; small genomes also match the oracle."""
+    import threading
+    torch = torch_cuda
+    L, w = 12_000_000, 31
+    m = O.mask(31, 21, 0)
+    dev = torch.empty(L + 1, dtype=torch.uint8, device="cuda:0")
+    ctx.synth_bases(dev.data_ptr(), L, 91)
+    dev[L] = ord("\n")
+    dev[5000:5100] = ord("N")
+    torch.cuda.synchronize()
+    jobs = [(sksffi.SKS_FRAC_MOD, 1000), (sksffi.SKS_FRAC_MOD, 200), (sksffi.SKS_BOTTOM_S, 5000)]
+    want = {j: ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, *j).sketch(0) for j in jobs}
+    small = _genomes(5, [30_000, 20_011])
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    ctxs = [sksffi.Context(0, st.cuda_stream) for st in streams]
+    bad = []
+
+    def worker(i):
+        try:
+            for r in range(4):
+                kind, param = jobs[(i + r) % len(jobs)]
+                ss = ctxs[i].sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, kind, param)
+                if not np.array_equal(ss.sketch(0), want[(kind, param)]):
+                    bad.append((i, r, kind, param))
+                del ss  # frees while the other threads build
+            stream = b"".join(g + b"\n" for g in small)
+            d_small = upload(torch, stream)
+            torch.cuda.synchronize()  # the upload ran on torch's stream, not ctxs[i]'s
+            offs = np.cumsum([0] + [len(g) + 1 for g in small])
+            sm = ctxs[i].sketch_build(d_small.data_ptr(), len(stream), offs, w, m,
+                                      sksffi.SKS_FRAC_MOD, 200)
+            check_against_oracle(sm, small, w, m, "frac", 200)
+        except Exception as e:  # reported below
+            bad.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(3)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize()
+    assert not bad, bad
+
+
 def test_argument_errors(torch_cuda, ctx):
     torch = torch_cuda
     d = upload(torch, b"ACGTACGT\n")
