@@ -395,7 +395,8 @@ __device__ __forceinline__ uint32_t join_hash(uint64_t v) {
 }
 
 // One workgroup per sketch i in [first, first + count): per-bucket element
-// counts into counts[(blk * B + b) * 64 + slot], blk/slot of i - base.
+// counts into counts[(blk * 64 + slot) * B + b] (one contiguous row per
+// sketch, so the writes coalesce), blk/slot of i - base.
 __global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ data,
                                                  const uint64_t* __restrict__ starts,
                                                  const uint32_t* __restrict__ sizes,
@@ -409,9 +410,54 @@ __global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ da
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < sz; e += kB) atomicAdd(&h[bucket_hash(src[e], log_b)], 1u);
   __syncthreads();
-  const uint32_t blk = (i - base) >> 6, slot = (i - base) & 63;
-  uint32_t* dst = counts + (uint64_t)blk * B * 64 + slot;
-  for (uint32_t b = threadIdx.x; b < B; b += kB) dst[(uint64_t)b * 64] = h[b];
+  uint32_t* dst = counts + (uint64_t)(i - base) * B;  // (blk * 64 + slot) * B
+  for (uint32_t b = threadIdx.x; b < B; b += kB) dst[b] = h[b];
+}
+
+// colsum[blk * B + b] = elements of bucket b in block blk (all 64 slots);
+// colsum[n_blk * B] = 0 so that its exclusive scan ends with the total.
+__global__ void k_hb_colsum(const uint32_t* __restrict__ counts, uint32_t n_blk, uint32_t B,
+                            uint32_t* __restrict__ colsum) {
+  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  const uint64_t cells = (uint64_t)n_blk * B;
+  if (idx > cells) return;
+  if (idx == cells) {
+    colsum[idx] = 0;
+    return;
+  }
+  const uint64_t blk = idx / B, b = idx % B;
+  const uint32_t* c = counts + blk * 64 * B + b;
+  uint32_t t = 0;
+#pragma unroll 8
+  for (int slot = 0; slot < 64; ++slot) t += c[(uint64_t)slot * B];
+  colsum[idx] = t;
+}
+
+// From bbase = exclusive scan of colsum: each sketch's cursor for each bucket,
+// off[(blk * 64 + slot) * B + b] = bbase[blk * B + b] + counts of the slots
+// before it; the per-block bucket starts boff[blk][b] (b = 0..B), bstart and
+// the largest block-bucket population (*stat) of the JoinLayout.
+__global__ void k_hb_offsets(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bbase,
+                             uint32_t n_blk, uint32_t B, uint32_t* __restrict__ off,
+                             uint32_t* __restrict__ boff, uint64_t* __restrict__ bstart,
+                             uint32_t* __restrict__ stat) {
+  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (idx >= (uint64_t)n_blk * (B + 1)) return;
+  const uint32_t blk = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
+  const uint32_t base = bbase[(uint64_t)blk * B];
+  const uint32_t v = bbase[(uint64_t)blk * B + b];  // b == B: the next block's start
+  boff[idx] = v - base;
+  if (b == 0) bstart[blk] = base;
+  if (blk == n_blk - 1 && b == B) bstart[n_blk] = v;
+  if (b == B) return;
+  atomicMax(stat, bbase[(uint64_t)blk * B + b + 1] - v);
+  const uint64_t row0 = (uint64_t)blk * 64 * B + b;
+  uint32_t run = v;
+#pragma unroll 8
+  for (int slot = 0; slot < 64; ++slot) {
+    off[row0 + (uint64_t)slot * B] = run;
+    run += counts[row0 + (uint64_t)slot * B];
+  }
 }
 
 // Scatter each sketch's elements to its (blk, b, slot) ranges (order inside a
@@ -427,9 +473,9 @@ __global__ __launch_bounds__(kB) void k_hb_scatter(const uint64_t* __restrict__ 
   const uint32_t i = first + blockIdx.x;
   const uint32_t sz = sizes[i];
   const uint64_t* src = data + starts[i];
-  const uint32_t blk = (i - base) >> 6, slot = (i - base) & 63;
-  const uint32_t* o = off + (uint64_t)blk * B * 64 + slot;
-  for (uint32_t b = threadIdx.x; b < B; b += kB) cur[b] = o[(uint64_t)b * 64];
+  const uint32_t slot = (i - base) & 63;
+  const uint32_t* o = off + (uint64_t)(i - base) * B;  // this sketch's cursors
+  for (uint32_t b = threadIdx.x; b < B; b += kB) cur[b] = o[b];
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < sz; e += kB) {
     const uint64_t v = src[e];
@@ -437,23 +483,6 @@ __global__ __launch_bounds__(kB) void k_hb_scatter(const uint64_t* __restrict__ 
     out[d] = v;
     ids[d] = (uint8_t)slot;
   }
-}
-
-// Compact per-block bucket starts: boff[blk][b] = off[(blk, b, 0)] - block start
-// (b = 0..B), bstart[blk] = block start (bstart[n_blk] = total), and the
-// largest block-bucket population into *stat.  One thread per (blk, b <= B).
-__global__ void k_hb_compact(const uint32_t* __restrict__ off, uint32_t n_blk, uint32_t B,
-                             uint32_t* __restrict__ boff, uint64_t* __restrict__ bstart,
-                             uint32_t* __restrict__ stat) {
-  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  if (idx >= (uint64_t)n_blk * (B + 1)) return;
-  const uint32_t blk = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
-  const uint32_t base = off[(uint64_t)blk * B * 64];
-  const uint32_t v = off[((uint64_t)blk * B + b) * 64];
-  boff[idx] = v - base;
-  if (b == 0) bstart[blk] = base;
-  if (blk == n_blk - 1 && b == B) bstart[n_blk] = v;
-  if (b < B) atomicMax(stat, off[((uint64_t)blk * B + b + 1) * 64] - v);
 }
 
 struct JoinArgs {
@@ -741,12 +770,19 @@ uint32_t join_log_b(uint32_t max_size) {
   return log_b;
 }
 
+// temp = counts[len] | off[len] | colsum[cells + 1] | bbase[cells + 1] | scan
+// temporaries, len = n_blk * 64 * B, cells = n_blk * B.
+static size_t layout_head_bytes(uint64_t len, uint64_t cells) {
+  return ((2 * len + 2 * (cells + 1)) * 4 + 15) & ~(size_t)15;
+}
+
 size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b) {
-  const uint64_t len = (uint64_t)((count + kTile - 1) / kTile) * (1ull << log_b) * 64;
+  const uint64_t n_blk = (count + kTile - 1) / kTile;
+  const uint64_t cells = n_blk * (1ull << log_b), len = cells * 64;
   size_t scan = 0;
   (void)rocprim::exclusive_scan(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                (size_t)(len + 1), rocprim::plus<uint32_t>(), (hipStream_t)0);
-  return ((2 * (len + 1) * 4 + 15) & ~(size_t)15) + scan + 16;
+                                (size_t)(cells + 1), rocprim::plus<uint32_t>(), (hipStream_t)0);
+  return layout_head_bytes(len, cells) + scan + 16;
 }
 
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
@@ -764,25 +800,30 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   if (count == 0) return hipSuccess;
   const uint32_t B = 1u << log_b;
   const uint32_t n_blk = (count + kTile - 1) / kTile;
-  const uint64_t len = (uint64_t)n_blk * B * 64;
+  const uint64_t cells = (uint64_t)n_blk * B, len = cells * 64;
   uint32_t* cnt = static_cast<uint32_t*>(temp);
-  uint32_t* off = cnt + (len + 1);
-  const size_t head = ((2 * (len + 1) * 4 + 15) & ~(size_t)15);
+  uint32_t* off = cnt + len;
+  uint32_t* colsum = off + len;
+  uint32_t* bbase = colsum + (cells + 1);
+  const size_t head = layout_head_bytes(len, cells);
   if (temp_bytes < head) return hipErrorInvalidValue;
   void* scan_tmp = static_cast<char*>(temp) + head;
   size_t scan_bytes = temp_bytes - head;
   hipError_t e;
-  if ((e = hipMemsetAsync(cnt, 0, (len + 1) * 4, s)) != hipSuccess) return e;
+  // slots past `count` in the last block have no workgroup: zero counts
+  if ((e = hipMemsetAsync(cnt, 0, len * 4, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_hb_count, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first, first,
                      B, log_b, cnt);
-  if ((e = rocprim::exclusive_scan(scan_tmp, scan_bytes, cnt, off, 0u, (size_t)(len + 1),
+  hipLaunchKernelGGL(k_hb_colsum, dim3((unsigned)((cells + 1 + kB - 1) / kB)), dim3(kB), 0, s, cnt,
+                     n_blk, B, colsum);
+  if ((e = rocprim::exclusive_scan(scan_tmp, scan_bytes, colsum, bbase, 0u, (size_t)(cells + 1),
                                    rocprim::plus<uint32_t>(), s)) != hipSuccess)
     return e;
+  const uint64_t bcells = (uint64_t)n_blk * (B + 1);
+  hipLaunchKernelGGL(k_hb_offsets, dim3((unsigned)((bcells + kB - 1) / kB)), dim3(kB), 0, s, cnt,
+                     bbase, n_blk, B, off, out_boff, out_bstart, d_stat);
   hipLaunchKernelGGL(k_hb_scatter, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first,
                      first, B, log_b, off, out_data, out_ids);
-  const uint64_t cells = (uint64_t)n_blk * (B + 1);
-  hipLaunchKernelGGL(k_hb_compact, dim3((unsigned)((cells + kB - 1) / kB)), dim3(kB), 0, s, off,
-                     n_blk, B, out_boff, out_bstart, d_stat);
   return hipGetLastError();
 }
 
