@@ -11,7 +11,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/round_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+# --inflight 1: every scan launch runs alone, so the trace average is the
+# kernel time bench.py reports for the roofline (its serial pass)
+ARGS="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --inflight 1"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $ARGS > $OUT/bench_traced.json 2> $OUT/trace.log
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $ARGS --no-pairs --no-sweep > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $ARGS --no-pairs --no-sweep > $OUT/write.log 2>&1
