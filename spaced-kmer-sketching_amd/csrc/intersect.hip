@@ -377,8 +377,11 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 // workgroup streams the column block in coalesced chunks of whole buckets
 // that fit the table (<= kJCap elements) and the row block's same buckets
 // with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
-constexpr int kJSlots = 2048;               // hash slots
-constexpr int kJLog = 11;
+#ifndef SKS_JOIN_LOG_SLOTS
+#define SKS_JOIN_LOG_SLOTS 11
+#endif
+constexpr int kJLog = SKS_JOIN_LOG_SLOTS;
+constexpr int kJSlots = 1 << kJLog;          // hash slots
 constexpr int kJCap = kJSlots / 2;          // column elements per chunk (load <= 1/2)
 constexpr int kJMade = kJCap / kB;          // column elements per thread per chunk (4)
 constexpr int kJWin = 256;                  // bucket offsets staged per window
