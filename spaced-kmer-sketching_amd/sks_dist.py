@@ -166,10 +166,21 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     — the contract of sks_intersect_sym_layout."""
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
     log_b = log_b_for(_max_over(local_max_size, world, device))
+    nb_local = (g1 - g0 + TILE - 1) // TILE
     while True:
         data, ids, boff, bstart, mb = build(log_b)
-        if _max_over(mb, world, device) <= capacity or log_b >= 14:
-            break
+        if world == 1:
+            if mb <= capacity or log_b >= 14:
+                break
+        else:
+            # one all-reduce for the capacity check and the padded layout size
+            tot = bstart[nb_local:nb_local + 1].to(device=device, dtype=torch.int64) if nb_local \
+                else torch.zeros(1, dtype=torch.int64, device=device)
+            both = torch.cat([torch.tensor([int(mb)], dtype=torch.int64, device=device), tot])
+            dist.all_reduce(both, op=dist.ReduceOp.MAX)
+            mb_all, cap_e = (int(v) for v in both.cpu())
+            if mb_all <= capacity or log_b >= 14:
+                break
         log_b += 1
     B1 = (1 << log_b) + 1
     t0, t1 = tile_shard(sym_tiles(n_genomes), world, rank)
@@ -178,28 +189,30 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     if world == 1:  # the local layout is the whole layout
         count(n_genomes, log_b, data, ids, boff, bstart, t0, t1, out)
         return out
-    nb_local = (g1 - g0 + TILE - 1) // TILE
-    tot = int(bstart[nb_local].item()) if nb_local else 0
-    cap_e = max(1, _max_over(tot, world, device))
-    # pad to the common per-rank shape; missing blocks are empty
+    tot = int(bstart[nb_local]) if nb_local else 0
+    cap_e = max(1, cap_e)
+    # pad to the common per-rank shape (missing blocks are empty); bucket and
+    # block starts travel together in one int32 gather (< 2^32 per layout)
     pd = torch.zeros(cap_e, dtype=torch.int64, device=device)
     pi = torch.zeros(cap_e, dtype=torch.uint8, device=device)
-    pb = torch.zeros(bpr * B1, dtype=torch.int32, device=device)
-    ps = torch.full((bpr + 1,), tot, dtype=torch.int64, device=device)
+    meta = torch.zeros(bpr * B1 + bpr + 1, dtype=torch.int32, device=device)
+    meta[bpr * B1:] = tot
     if tot:
         pd[:tot] = data[:tot]
         pi[:tot] = ids[:tot]
     if nb_local:
-        pb[: nb_local * B1] = boff[: nb_local * B1]
-        ps[: nb_local + 1] = bstart[: nb_local + 1]
-    g_data, g_ids, g_boff = _gather_flat(pd, world), _gather_flat(pi, world), _gather_flat(pb, world)
-    g_bst = _gather_flat(ps, world).view(world, bpr + 1)[:, :bpr]
-    g_bst = (g_bst + torch.arange(world, device=device, dtype=torch.int64).view(world, 1) * cap_e)
+        meta[: nb_local * B1] = boff[: nb_local * B1].to(device=device, dtype=torch.int32)
+        meta[bpr * B1: bpr * B1 + nb_local + 1] = bstart[: nb_local + 1].to(device=device,
+                                                                              dtype=torch.int32)
+    g_data, g_ids, g_meta = _gather_flat(pd, world), _gather_flat(pi, world), _gather_flat(meta, world)
+    g_meta = g_meta.view(world, bpr * B1 + bpr + 1)
+    g_boff = g_meta[:, : bpr * B1].reshape(-1).contiguous()
+    g_bst = g_meta[:, bpr * B1: bpr * B1 + bpr].to(torch.int64) & 0xFFFFFFFF
+    g_bst = g_bst + torch.arange(world, device=device, dtype=torch.int64).view(world, 1) * cap_e
     g_bst = torch.cat([g_bst.reshape(-1),
                        torch.tensor([world * cap_e], dtype=torch.int64, device=device)])
     count(n_genomes, log_b, g_data, g_ids, g_boff, g_bst, t0, t1, out)
-    if world > 1:
-        sum_matrix(out)
+    sum_matrix(out)
     return out
 
 
