@@ -157,7 +157,11 @@ def run_c3_inflight(device, buf, n_bytes, mask, steps, inflight, world):
     def worker(i):
         try:
             for _ in range(i, steps, inflight):
-                kept[i].append(build(ctxs[i]))
+                ss = build(ctxs[i])
+                kept[i].append((int(ss.windows()[0]), int(ss.sizes()[0])))
+                # stream-ordered free: the arrays return to the block cache
+                # without waiting for the other build in flight
+                ss.free(stream=streams[i].cuda_stream)
         except Exception as e:  # surfaced after the join
             errors.append(e)
 
@@ -174,8 +178,8 @@ def run_c3_inflight(device, buf, n_bytes, mask, steps, inflight, world):
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     if errors:
         raise errors[0]
-    windows = sum(int(ss.windows()[0]) for k in kept for ss in k)
-    sizes = {int(ss.sizes()[0]) for k in kept for ss in k}
+    windows = sum(w for k in kept for w, _ in k)
+    sizes = {z for k in kept for _, z in k}
     assert windows == steps * c3_windows(), (windows, steps * c3_windows())
     del kept
     total = sum_over_ranks(windows, world)
@@ -498,7 +502,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
 
 
 # ---- config 5 ------------------------------------------------------------------------
-def run_seed_sweep(ctx, world, rank, steps, warmup):
+def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
     """Config 5: 8 spaced seeds (w=31/k=21, mask seeds 0..7) over the first 200
     genomes of config 4, bottom-s s=10000; per seed: sketch all genomes, count
     all 200 x 200 ordered pairs (symmetric tiles), containment + ANI on the host
@@ -518,38 +522,44 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
     torch.cuda.synchronize()
     masks = [sksffi.mask_generate(W, K, s) for s in range(C5_SEEDS)]
     ones = [bin(m).count("1") // 2 for m in masks]
-    padded = torch.full((n, C4_S), -1, dtype=torch.int64, device="cuda")
-    sizes = torch.zeros(n, dtype=torch.int32, device="cuda")
     starts = torch.arange(n, dtype=torch.int64, device="cuda") * C4_S
-    mat = torch.empty((n, n), dtype=torch.int32, device="cuda")
     n_tiles = sksffi.intersect_sym_tiles(n)
     dev = "cuda" if world > 1 and os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
 
-    prof = os.environ.get("SKS_SWEEP_PROFILE") is not None
-    phase = {"sketch": 0.0, "pairs": 0.0}
+    # seeds are independent: `lanes` seeds run at once, each lane a context on its
+    # own HIP stream with its own buffers, driven by its own host thread, so one
+    # seed's post-processing, pair counts and host ANI overlap another's scan
+    import queue
     from concurrent.futures import ThreadPoolExecutor
-    pool = ThreadPoolExecutor(max_workers=1)
+    lanes = queue.Queue()
+    for _ in range(max(1, lanes_n)):
+        st = torch.cuda.Stream()
+        lanes.put({"ctx": sksffi.Context(torch.cuda.current_device(), st.cuda_stream),
+                   "stream": st.cuda_stream,
+                   "padded": torch.full((n, C4_S), -1, dtype=torch.int64, device="cuda"),
+                   "sizes": torch.zeros(n, dtype=torch.int32, device="cuda"),
+                   "mat": torch.empty((n, n), dtype=torch.int32, device="cuda")})
+    pool = ThreadPoolExecutor(max_workers=max(1, lanes_n))
+
+    def seed_job(s):
+        lane = lanes.get()
+        try:
+            c = lane["ctx"]
+            ss = c.sketch_build(buf.data_ptr(), seg[-1], seg, W, masks[s], sksffi.SKS_BOTTOM_S, C4_S)
+            ss.export(lane["padded"].data_ptr(), C4_S, lane["sizes"].data_ptr())
+            c.intersect_sym(lane["padded"].data_ptr(), starts.data_ptr(), lane["sizes"].data_ptr(),
+                            1, n, 0, n_tiles, lane["mat"].data_ptr())
+            c.synchronize()
+            counts = lane["mat"].cpu().numpy()
+            ss.free(stream=lane["stream"])  # no device-wide wait (the other lane runs)
+        finally:
+            lanes.put(lane)
+        size_first = np.repeat(np.diag(counts).astype(np.int32), n)
+        _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones[s])
+        return torch.from_numpy(ani.reshape(n, n))
 
     def ani_for_seed(s):
-        t0 = time.perf_counter()
-        ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, masks[s], sksffi.SKS_BOTTOM_S, C4_S)
-        ss.export(padded.data_ptr(), C4_S, sizes.data_ptr())
-        if prof:
-            torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        ctx.intersect_sym(padded.data_ptr(), starts.data_ptr(), sizes.data_ptr(), 1, n, 0,
-                          n_tiles, mat.data_ptr())
-        counts = mat.cpu().numpy()
-        t2 = time.perf_counter()
-        del ss
-
-        def host_ani():  # runs beside the next seed's GPU work (ctypes drops the GIL)
-            size_first = np.repeat(np.diag(counts).astype(np.int32), n)
-            _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones[s])
-            return torch.from_numpy(ani.reshape(n, n))
-        phase["sketch"] += t1 - t0
-        phase["pairs"] += t2 - t1
-        return pool.submit(host_ani)
+        return pool.submit(seed_job, s)
 
     total = 0.0
     timed = 0
@@ -565,8 +575,6 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
             timed += 1
     pool.shutdown()
     t = total / max(timed, 1)
-    if prof:
-        log("[sweep phases, all iterations, s]", {k: round(v, 4) for k, v in phase.items()})
     c = cons.numpy()
     return {
         "metric": "seed-sweep genome-pairs ANI/s", "value": C5_SEEDS * n * n / t,
@@ -577,6 +585,7 @@ def run_seed_sweep(ctx, world, rank, steps, warmup):
         "config": {"workload": "config5 seed sweep", "genomes": n, "genome_len": C4_LEN,
                    "seeds": C5_SEEDS, "s": C4_S, "w": W, "k": K,
                    "sharding": "seeds over ranks", "consensus": "mean ANI over seeds",
+                   "seeds_in_flight": max(1, lanes_n),
                    "collective": ("all_reduce of ANI sums (RCCL)" if world > 1 and dev == "cuda"
                                   else ("all_reduce (gloo)" if world > 1 else "none"))},
     }
@@ -636,9 +645,8 @@ def main():
 
     # headline pass: `inflight` builds at once (host threads, one context per
     # HIP stream), so one build's sort / unique / host syncs run under the next
-    # build's scan. Every build is complete and its sketch kept in HBM when the
-    # clock stops; the sketches are freed after it (freeing synchronises the
-    # device, as hipFree does).
+    # build's scan. Each build is complete when sks_sketch_build returns; its
+    # set is then freed in stream order (sks_sketch_set_free_on_stream).
     value, elapsed, inflight_sizes = run_c3_inflight(local, buf, n_bytes, mask, args.steps,
                                                      args.inflight, world)
     assert inflight_sizes == {sizes[0]}, (inflight_sizes, sizes[0])
@@ -668,7 +676,8 @@ def main():
 
     sweep = None
     if not args.no_sweep:
-        sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1)
+        sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1,
+                               lanes_n=args.inflight)
 
     cpu = cpu_x = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -131,7 +131,15 @@ typedef struct sks_sketch_set sks_sketch_set;
 int sks_sketch_build(sks_ctx* ctx, const uint8_t* d_seq, uint64_t n_bytes, const uint64_t* seg_off,
                      uint32_t n_seg, int window, const uint64_t mask[2], const sks_policy* policy,
                      sks_sketch_set** out);
+/* Frees the set. Like hipFree, it first waits for all work queued on the
+ * device; the arrays then go to a per-process block cache for later builds. */
 int sks_sketch_set_free(sks_sketch_set* set);
+/* Stream-ordered free (the hipFreeAsync contract): every use of the set must
+ * be ordered before the current end of `stream` (a hipStream_t, NULL = the
+ * null stream). Does not wait; the arrays are reused only once that point of
+ * `stream` has completed. Lets several host threads build and free
+ * concurrently without the device-wide wait of sks_sketch_set_free. */
+int sks_sketch_set_free_on_stream(sks_sketch_set* set, void* stream);
 uint32_t sks_sketch_set_num(const sks_sketch_set* set);
 int sks_sketch_set_elem_words(const sks_sketch_set* set); /* 1 or 2 */
 /* Host copies of per-sketch sizes (kmer_set::kmer_set_size, kmer.hpp:186-189)

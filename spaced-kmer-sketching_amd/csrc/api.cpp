@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -24,6 +25,47 @@ thread_local std::string g_last_error;
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
+}
+
+namespace {
+struct PinnedStage {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+// never freed: a thread_local destructor could run after the HIP runtime has
+// been torn down at process exit
+thread_local PinnedStage t_stage;
+
+hipError_t stage_reserve(size_t bytes) {
+  if (bytes <= t_stage.bytes) return hipSuccess;
+  if (t_stage.p) (void)hipHostFree(t_stage.p);
+  t_stage.p = nullptr;
+  t_stage.bytes = 0;
+  size_t nb = std::max<size_t>(bytes, size_t(1) << 16);
+  nb = (nb + 4095) & ~size_t(4095);
+  hipError_t e = hipHostMalloc(&t_stage.p, nb, hipHostMallocDefault);
+  if (e == hipSuccess) t_stage.bytes = nb;
+  return e;
+}
+}  // namespace
+
+hipError_t pinned_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  hipError_t e;
+  if ((e = stage_reserve(bytes)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(t_stage.p, src, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  std::memcpy(dst, t_stage.p, bytes);
+  return hipSuccess;
+}
+
+hipError_t pinned_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  hipError_t e;
+  if ((e = stage_reserve(bytes)) != hipSuccess) return e;
+  std::memcpy(t_stage.p, src, bytes);
+  if ((e = hipMemcpyAsync(dst, t_stage.p, bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);  // the stage is reused by the next copy
 }
 
 }  // namespace sks
@@ -102,8 +144,7 @@ class MetaArena {
   int upload() {
     size_t bytes = c_->meta_host.size() * sizeof(uint64_t);
     SKS_HIP(c_->meta.reserve(bytes));
-    SKS_HIP(hipMemcpyAsync(c_->meta.ptr, c_->meta_host.data(), bytes, hipMemcpyHostToDevice,
-                           c_->stream));
+    SKS_HIP(sks::pinned_h2d(c_->meta.ptr, c_->meta_host.data(), bytes, c_->stream));
     return SKS_OK;
   }
   uint64_t* ptr(size_t off) const { return reinterpret_cast<uint64_t*>(c_->meta.ptr) + off; }
@@ -146,6 +187,7 @@ struct CachedBlock {
   int device;
   void* p;
   size_t bytes;
+  hipEvent_t ready;  // null, or the stream point after which the block is free
 };
 std::mutex g_cache_mu;
 void trim_device_cache(int device);
@@ -174,8 +216,16 @@ hipError_t dev_alloc(void** p, size_t bytes) {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     size_t best = g_cache.size();
     for (size_t i = 0; i < g_cache.size(); ++i) {
-      const CachedBlock& b = g_cache[i];
+      CachedBlock& b = g_cache[i];
       if (b.device != dev || b.bytes < bytes || b.bytes > 2 * bytes + (size_t(1) << 20)) continue;
+      if (b.ready) {  // stream-ordered release: reusable once its event has completed
+        if (hipEventQuery(b.ready) != hipSuccess) {
+          (void)hipGetLastError();  // hipErrorNotReady is not an error here
+          continue;
+        }
+        (void)hipEventDestroy(b.ready);
+        b.ready = nullptr;
+      }
       if (best == g_cache.size() || b.bytes < g_cache[best].bytes) best = i;
     }
     if (best != g_cache.size()) {
@@ -193,37 +243,76 @@ hipError_t dev_alloc(void** p, size_t bytes) {
   return e;
 }
 
-// Parks a block whose last use has completed (the caller guarantees it; see
-// sks_sketch_set_free); evicts the oldest blocks beyond the cache limits.
-void dev_release(void* p, size_t bytes) {
-  if (!p) return;
-  std::vector<void*> evict;
+// Parks a block whose last use has completed (ready == null; the caller
+// guarantees it, see sks_sketch_set_free) or completes at the event `ready`;
+// evicts the oldest blocks beyond the cache limits (hipFree waits for them).
+void dev_release(void* p, size_t bytes, hipEvent_t ready = nullptr) {
+  if (!p) {
+    if (ready) (void)hipEventDestroy(ready);
+    return;
+  }
+  std::vector<CachedBlock> evict;
   {
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    g_cache.push_back({current_device(), p, std::max<size_t>(bytes, 8)});
+    g_cache.push_back({current_device(), p, std::max<size_t>(bytes, 8), ready});
     while (g_cache.size() > kCacheMaxBlocks ||
            (g_cache.size() > 1 && cache_bytes_locked() > kCacheMaxBytes)) {
-      evict.push_back(g_cache.front().p);
+      evict.push_back(g_cache.front());
       g_cache.erase(g_cache.begin());
     }
   }
-  for (void* q : evict) (void)hipFree(q);
+  for (const CachedBlock& b : evict) {
+    if (b.ready) (void)hipEventDestroy(b.ready);
+    (void)hipFree(b.p);
+  }
 }
 
 void trim_device_cache(int device) {
-  std::vector<void*> drop;
+  std::vector<CachedBlock> drop;
   {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     for (size_t i = 0; i < g_cache.size();) {
       if (g_cache[i].device == device) {
-        drop.push_back(g_cache[i].p);
+        drop.push_back(g_cache[i]);
         g_cache.erase(g_cache.begin() + i);
       } else {
         ++i;
       }
     }
   }
-  for (void* q : drop) (void)hipFree(q);
+  for (const CachedBlock& b : drop) {
+    if (b.ready) (void)hipEventDestroy(b.ready);
+    (void)hipFree(b.p);
+  }
+}
+
+// Returns a set's arrays to the block cache: at once (the device is idle for
+// them), or ordered after the current end of `stream`.
+void release_set_arrays(sks_sketch_set* set, hipStream_t stream, bool ordered) {
+  uint64_t total = 0;
+  for (uint32_t v : set->sizes) total += v;
+  void* arrays[3] = {set->d_data, set->d_starts, set->d_sizes};
+  const size_t bytes[3] = {std::max<uint64_t>(total * set->elem_words, 1) * 8,
+                           (size_t)std::max<uint32_t>(set->n, 1) * 8,
+                           (size_t)std::max<uint32_t>(set->n, 1) * 4};
+  for (int i = 0; i < 3; ++i) {
+    if (!arrays[i]) continue;
+    hipEvent_t ev = nullptr;
+    if (ordered) {
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(ev, stream) != hipSuccess) {
+        // no event: fall back to waiting for the stream, then release at once
+        if (ev) (void)hipEventDestroy(ev);
+        ev = nullptr;
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(stream);
+      }
+    }
+    dev_release(arrays[i], bytes[i], ev);
+  }
+  set->d_data = nullptr;
+  set->d_starts = nullptr;
+  set->d_sizes = nullptr;
 }
 
 // Pass buffers are only used on the ctx stream, synchronised before this runs.
@@ -495,8 +584,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
       K2 = col(c, 6);  // lo
     }
     SKS_HIP(sks::seg_unique_scan(K, K2, T, max_len, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
-    SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    SKS_HIP(hipStreamSynchronize(st));
+    SKS_HIP(sks::pinned_d2h(uniq.data(), d_uniq, k * sizeof(uint64_t), st));
     po.off = prefix(uniq);
     const uint64_t U = po.off[k];
     SKS_TRY(alloc_u64(&po.d, U * S.ew, &po.bytes));
@@ -522,8 +610,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, key_bits, c->tmp, st));
     SKS_HIP(sks::seg_unique_scan(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos, d_uniq,
                                  c->tmp, st));
-    SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    SKS_HIP(hipStreamSynchronize(st));
+    SKS_HIP(sks::pinned_d2h(uniq.data(), d_uniq, k * sizeof(uint64_t), st));
     uint64_t max_keep_uniq = 0;
     for (uint32_t i = 0; i < k; ++i)
       if (uniq[i] >= s || thresh[ok[i]] == ~0ull) max_keep_uniq = std::max(max_keep_uniq, uniq[i]);
@@ -589,8 +676,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     HI = col(c, 8);
     SKS_HIP(sks::seg_unique_scan(LO, HI, T, max_len, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
   }
-  SKS_HIP(hipMemcpyAsync(uniq.data(), d_uniq, k * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-  SKS_HIP(hipStreamSynchronize(st));
+  SKS_HIP(sks::pinned_d2h(uniq.data(), d_uniq, k * sizeof(uint64_t), st));
   std::vector<uint64_t> limit(k, 0);
   std::vector<uint32_t> keep_segs;
   std::vector<uint64_t> keep_off(1, 0);
@@ -773,9 +859,8 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
     SKS_HIP(hipEventRecord(c->ev_s1, st));
     tm.scan_launches += n_tiles ? 1 : 0;
     std::vector<uint64_t> counts(m), wins(m);
-    SKS_HIP(hipMemcpyAsync(counts.data(), p.seg_count, m * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    SKS_HIP(hipMemcpyAsync(wins.data(), p.seg_windows, m * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    SKS_HIP(hipStreamSynchronize(st));
+    SKS_HIP(sks::pinned_d2h(counts.data(), p.seg_count, m * sizeof(uint64_t), st));
+    SKS_HIP(sks::pinned_d2h(wins.data(), p.seg_windows, m * sizeof(uint64_t), st));
     float ms = 0;
     SKS_HIP(hipEventElapsedTime(&ms, c->ev_s0, c->ev_s1));
     tm.scan_ms += ms;
@@ -871,10 +956,9 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
                                 std::max<uint32_t>(n_seg, 1) * sizeof(uint32_t)) != hipSuccess)
     rc = sks::fail(SKS_E_HIP, "sks_sketch_build: device allocation failed");
   if (rc == SKS_OK && n_seg) {
-    if (hipMemcpyAsync(set->d_starts, set->starts.data(), n_seg * sizeof(uint64_t),
-                       hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(set->d_sizes, set->sizes.data(), n_seg * sizeof(uint32_t),
-                       hipMemcpyHostToDevice, st) != hipSuccess)
+    if (sks::pinned_h2d(set->d_starts, set->starts.data(), n_seg * sizeof(uint64_t), st) !=
+            hipSuccess ||
+        sks::pinned_h2d(set->d_sizes, set->sizes.data(), n_seg * sizeof(uint32_t), st) != hipSuccess)
       rc = sks::fail(SKS_E_HIP, "sks_sketch_build: metadata upload failed");
   }
   if (rc == SKS_OK && hipEventRecord(c->ev_end, st) != hipSuccess)
@@ -902,11 +986,15 @@ int sks_sketch_set_free(sks_sketch_set* set) {
   // hipFree's contract: work queued on the arrays (any stream) completes before
   // they are reused; then they go to the block cache instead of being unmapped
   if (set->d_data || set->d_starts || set->d_sizes) (void)hipDeviceSynchronize();
-  uint64_t total = 0;
-  for (uint32_t v : set->sizes) total += v;
-  dev_release(set->d_data, std::max<uint64_t>(total * set->elem_words, 1) * 8);
-  dev_release(set->d_starts, std::max<uint32_t>(set->n, 1) * 8);
-  dev_release(set->d_sizes, std::max<uint32_t>(set->n, 1) * 4);
+  release_set_arrays(set, nullptr, false);
+  delete set;
+  return SKS_OK;
+}
+
+int sks_sketch_set_free_on_stream(sks_sketch_set* set, void* stream) {
+  if (!set) return SKS_OK;
+  DeviceGuard g(set->device);
+  release_set_arrays(set, reinterpret_cast<hipStream_t>(stream), true);
   delete set;
   return SKS_OK;
 }
@@ -1023,9 +1111,7 @@ int sks_kmer_list_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, cons
     p.seg_windows = reinterpret_cast<unsigned long long*>(arena.ptr(o_win));
     SKS_HIP(sks::launch_scan(p, sks::kModeList, policy->flavour, wide, c->device, st,
                              c->grid_override));
-    SKS_HIP(hipMemcpyAsync(counts.data(), p.seg_count, n_seg * sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, st));
-    SKS_HIP(hipStreamSynchronize(st));
+    SKS_HIP(sks::pinned_d2h(counts.data(), p.seg_count, n_seg * sizeof(uint64_t), st));
     bool overflow = false;
     for (uint32_t g = 0; g < n_seg; ++g)
       if (counts[g] > cap[g]) {
@@ -1193,7 +1279,7 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
   DeviceGuard g(c->device);
   if (n) {  // bucket starts are u32: the layout must hold < 2^32 elements
     std::vector<uint32_t> h_sizes(n);
-    SKS_HIP(hipMemcpy(h_sizes.data(), d_sizes, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    SKS_HIP(sks::pinned_d2h(h_sizes.data(), d_sizes, n * sizeof(uint32_t), c->stream));
     uint64_t total = 0;
     for (uint32_t v : h_sizes) total += v;
     if (total >= (1ull << 32))
@@ -1211,8 +1297,7 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
                                    d_out_boff, d_out_bstart, stat, w, tmp, c->stream));
   }
   uint32_t h = 0;
-  SKS_HIP(hipMemcpyAsync(&h, stat, 4, hipMemcpyDeviceToHost, c->stream));
-  SKS_HIP(hipStreamSynchronize(c->stream));
+  SKS_HIP(sks::pinned_d2h(&h, stat, 4, c->stream));
   if (max_block_bucket) *max_block_bucket = h;
   return SKS_OK;
 }

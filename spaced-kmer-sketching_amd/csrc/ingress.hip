@@ -379,9 +379,8 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
                                  rocprim::plus<uint64_t>(), s));
   uint64_t n_nl = 0;
   uint8_t last = 0;
-  SKS_CK(hipMemcpyAsync(&n_nl, span_off + spans, sizeof n_nl, hipMemcpyDeviceToHost, s));
-  SKS_CK(hipMemcpyAsync(&last, raw + n - 1, 1, hipMemcpyDeviceToHost, s));
-  SKS_CK(hipStreamSynchronize(s));
+  SKS_CK(pinned_d2h(&n_nl, span_off + spans, sizeof n_nl, s));
+  SKS_CK(pinned_d2h(&last, raw + n - 1, 1, s));
   const uint64_t L = n_nl + (last != '\n');  // a trailing partial line is a line
   if (L >= (1ull << 32)) return hipErrorInvalidValue;  // push ranks are u32
 
@@ -460,8 +459,7 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   hipLaunchKernelGGL(k_summary, dim3(1), dim3(1), 0, s, L, out_off, out_len, push_rank, push_cnt,
                      have_after, d_sum);
   Summary h{};
-  SKS_CK(hipMemcpyAsync(&h, d_sum, sizeof h, hipMemcpyDeviceToHost, s));
-  SKS_CK(hipStreamSynchronize(s));
+  SKS_CK(pinned_d2h(&h, d_sum, sizeof h, s));
   *out_bytes = h.total;
   *n_records = h.n_records;
   if (!out) return hipSuccess;  // size query

@@ -877,8 +877,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
   if (n == 0 || out_words == 0) { *used_tiles = true; return hipSuccess; }
   std::vector<uint32_t> h_sizes(n);
-  if ((e = hipMemcpyAsync(h_sizes.data(), sizes, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  if ((e = pinned_d2h(h_sizes.data(), sizes, n * sizeof(uint32_t), s)) != hipSuccess) return e;
   const uint32_t max_size = *std::max_element(h_sizes.begin(), h_sizes.end());
   if (max_size == 0) { *used_tiles = true; return hipSuccess; }
 
@@ -979,8 +978,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
           return e;
       }
       uint32_t h_stat = 0;
-      if ((e = hipMemcpyAsync(&h_stat, stat, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-      if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+      if ((e = pinned_d2h(&h_stat, stat, 4, s)) != hipSuccess) return e;
       if (dbg)
         fprintf(stderr, "[sks intersect] join n=%u B=%u max block bucket %u tiles=%llu\n", n, B,
                 h_stat, (unsigned long long)tiles);
@@ -1020,8 +1018,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
                        n, B, n_cb, stats);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     uint32_t h_stats[2];
-    if ((e = hipMemcpyAsync(h_stats, stats, sizeof(h_stats), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if ((e = pinned_d2h(h_stats, stats, sizeof(h_stats), s)) != hipSuccess) return e;
     const uint32_t P = h_stats[0];
     if (P <= (uint32_t)kGoodPart) return launch(data, starts, pos, B, P);
     if (B >= (1u << 16) || (uint64_t)B * 8 > max_size) {

@@ -492,8 +492,7 @@ hipError_t sort_unique_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64
   if ((e = rocprim::unique(t, tb, sorted, out, d_cnt, (size_t)n, rocprim::equal_to<uint64_t>(), s)) !=
       hipSuccess)
     return e;
-  if ((e = hipMemcpyAsync(n_out, d_cnt, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-  return hipStreamSynchronize(s);
+  return pinned_d2h(n_out, d_cnt, 8, s);
 }
 
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,

@@ -8,6 +8,14 @@
 
 namespace sks {
 
+// Small host<->device copies through a per-thread pinned staging buffer,
+// synchronous on `s` only. A pageable hipMemcpyAsync goes through the
+// runtime's shared staging path: with two contexts building on two streams, one
+// context's 1 KB count read-back waited for the other stream's scan
+// (--hip-trace), serialising the concurrent builds.
+hipError_t pinned_d2h(void* dst, const void* src, size_t bytes, hipStream_t s);
+hipError_t pinned_h2d(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 constexpr int kModeFrac = 0;
 constexpr int kModeBottom = 1;
 constexpr int kModeList = 2;  // FracMinHash test, emits window start positions

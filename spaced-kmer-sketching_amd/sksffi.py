@@ -48,7 +48,7 @@ EXPORTED = [
     "sks_fasta_open", "sks_fasta_close", "sks_fasta_num_records", "sks_fasta_record",
     "sks_fasta_stream", "sks_fasta_stream_bytes", "sks_fasta_runs", "sks_ctx_create",
     "sks_ctx_destroy", "sks_ctx_set_stream", "sks_ctx_synchronize", "sks_ctx_last_timings",
-    "sks_sketch_build", "sks_sketch_set_free", "sks_sketch_set_num", "sks_sketch_set_elem_words",
+    "sks_sketch_build", "sks_sketch_set_free", "sks_sketch_set_free_on_stream", "sks_sketch_set_num", "sks_sketch_set_elem_words",
     "sks_sketch_set_sizes", "sks_sketch_set_windows", "sks_sketch_set_device_data",
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
@@ -135,6 +135,7 @@ def lib():
     L.sks_sketch_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
                                    C.POINTER(Policy), C.POINTER(vp)]
     L.sks_sketch_set_free.argtypes = [vp]
+    L.sks_sketch_set_free_on_stream.argtypes = [vp, vp]
     L.sks_sketch_set_num.argtypes = [vp]
     L.sks_sketch_set_num.restype = C.c_uint32
     L.sks_sketch_set_elem_words.argtypes = [vp]
@@ -415,9 +416,15 @@ class SketchSet:
         self.n = int(lib().sks_sketch_set_num(h))
         self.elem_words = int(lib().sks_sketch_set_elem_words(h))
 
-    def free(self):
+    def free(self, stream=None):
+        """sks_sketch_set_free, or with `stream` (a hipStream_t handle, e.g.
+        torch.cuda.Stream().cuda_stream) sks_sketch_set_free_on_stream: no
+        device-wide wait; every use of the set must be ordered on that stream."""
         if self.h:
-            lib().sks_sketch_set_free(self.h)
+            if stream is None:
+                lib().sks_sketch_set_free(self.h)
+            else:
+                lib().sks_sketch_set_free_on_stream(self.h, C.c_void_p(stream))
             self.h = None
 
     def __del__(self):

@@ -264,8 +264,9 @@ def test_frac_chunk_union_property(torch_cuda, ctx):
 
 def test_concurrent_contexts_on_streams(torch_cuda, ctx):
     """bench.py's headline mode: builds from several host threads, one context
-    per HIP stream, in flight together (and sets freed while another thread
-    builds) give the serial build's sketches; small genomes also match the oracle."""
+    per HIP stream, in flight together (and sets freed, both ways, while another
+    thread builds) give the serial build's sketches; small genomes also match
+    the oracle."""
     import threading
     torch = torch_cuda
     L, w = 12_000_000, 31
@@ -289,7 +290,10 @@ def test_concurrent_contexts_on_streams(torch_cuda, ctx):
                 ss = ctxs[i].sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, kind, param)
                 if not np.array_equal(ss.sketch(0), want[(kind, param)]):
                     bad.append((i, r, kind, param))
-                del ss  # frees while the other threads build
+                if r % 2:  # frees while the other threads build
+                    ss.free(stream=streams[i].cuda_stream)  # stream-ordered
+                else:
+                    del ss  # device-wide wait, as hipFree
             stream = b"".join(g + b"\n" for g in small)
             d_small = upload(torch, stream)
             torch.cuda.synchronize()  # the upload ran on torch's stream, not ctxs[i]'s
