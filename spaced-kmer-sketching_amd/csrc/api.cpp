@@ -1277,15 +1277,15 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
   if (!d_out_bstart || (n && (!d_starts || !d_sizes || !d_out_boff)))
     return sks::fail(SKS_E_ARG, "sks_join_layout_build: null argument");
   DeviceGuard g(c->device);
+  uint64_t total = 0;
   if (n) {  // bucket starts are u32: the layout must hold < 2^32 elements
     std::vector<uint32_t> h_sizes(n);
     SKS_HIP(sks::pinned_d2h(h_sizes.data(), d_sizes, n * sizeof(uint32_t), c->stream));
-    uint64_t total = 0;
     for (uint32_t v : h_sizes) total += v;
     if (total >= (1ull << 32))
       return sks::fail(SKS_E_UNSUPPORTED, "sks_join_layout_build: >= 2^32 elements in one layout");
   }
-  const size_t tmp = sks::join_layout_temp_bytes(n, log_b);
+  const size_t tmp = sks::join_layout_temp_bytes(n, log_b, total);
   SKS_HIP(c->iwork.reserve(tmp + 64));
   char* w = static_cast<char*>(c->iwork.ptr);
   uint32_t* stat = reinterpret_cast<uint32_t*>(w + ((tmp + 15) & ~(size_t)15));
@@ -1293,8 +1293,8 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
   if (n == 0) {
     SKS_HIP(hipMemsetAsync(d_out_bstart, 0, 8, c->stream));
   } else {
-    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, 0, n, log_b, d_out_data, d_out_ids,
-                                   d_out_boff, d_out_bstart, stat, w, tmp, c->stream));
+    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, 0, n, total, log_b, d_out_data,
+                                   d_out_ids, d_out_boff, d_out_bstart, stat, w, tmp, c->stream));
   }
   uint32_t h = 0;
   SKS_HIP(sks::pinned_d2h(&h, stat, 4, c->stream));

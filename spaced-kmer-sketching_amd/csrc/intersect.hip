@@ -404,7 +404,8 @@ __global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ da
                                                  const uint64_t* __restrict__ starts,
                                                  const uint32_t* __restrict__ sizes,
                                                  uint32_t first, uint32_t base, uint32_t B,
-                                                 uint32_t log_b, uint32_t* __restrict__ counts) {
+                                                 uint32_t log_b, uint32_t* __restrict__ counts,
+                                                 uint32_t G, uint32_t* __restrict__ gcounts) {
   extern __shared__ uint32_t h[];
   const uint32_t i = first + blockIdx.x;
   const uint32_t sz = sizes[i];
@@ -415,6 +416,13 @@ __global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ da
   __syncthreads();
   uint32_t* dst = counts + (uint64_t)(i - base) * B;  // (blk * 64 + slot) * B
   for (uint32_t b = threadIdx.x; b < B; b += kB) dst[b] = h[b];
+  // elements per coarse group of B / G consecutive buckets (two-phase scatter)
+  const uint32_t bpg = B / G;
+  for (uint32_t g = threadIdx.x; g < G; g += kB) {
+    uint32_t t = 0;
+    for (uint32_t b = g * bpg; b < (g + 1) * bpg; ++b) t += h[b];
+    gcounts[(uint64_t)(i - base) * G + g] = t;
+  }
 }
 
 // colsum[blk * B + b] = elements of bucket b in block blk (all 64 slots);
@@ -443,7 +451,8 @@ __global__ void k_hb_colsum(const uint32_t* __restrict__ counts, uint32_t n_blk,
 __global__ void k_hb_offsets(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bbase,
                              uint32_t n_blk, uint32_t B, uint32_t* __restrict__ off,
                              uint32_t* __restrict__ boff, uint64_t* __restrict__ bstart,
-                             uint32_t* __restrict__ stat) {
+                             uint32_t* __restrict__ stat, uint32_t G,
+                             const uint32_t* __restrict__ gcounts, uint32_t* __restrict__ goff) {
   const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
   if (idx >= (uint64_t)n_blk * (B + 1)) return;
   const uint32_t blk = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
@@ -461,30 +470,74 @@ __global__ void k_hb_offsets(const uint32_t* __restrict__ counts, const uint32_t
     off[row0 + (uint64_t)slot * B] = run;
     run += counts[row0 + (uint64_t)slot * B];
   }
+  // the first bucket of each coarse group: where each slot's elements of the
+  // group start in the staging array (group-major, then slot)
+  const uint32_t bpg = B / G;
+  if (b % bpg == 0) {
+    const uint64_t grow0 = (uint64_t)blk * 64 * G + b / bpg;
+    uint32_t grun = v;
+    for (int slot = 0; slot < 64; ++slot) {
+      goff[grow0 + (uint64_t)slot * G] = grun;
+      grun += gcounts[grow0 + (uint64_t)slot * G];
+    }
+  }
 }
 
-// Scatter each sketch's elements to its (blk, b, slot) ranges (order inside a
-// range is arbitrary: the join does not need it).
-__global__ __launch_bounds__(kB) void k_hb_scatter(const uint64_t* __restrict__ data,
-                                                   const uint64_t* __restrict__ starts,
-                                                   const uint32_t* __restrict__ sizes,
-                                                   uint32_t first, uint32_t base, uint32_t B,
-                                                   uint32_t log_b, const uint32_t* __restrict__ off,
-                                                   uint64_t* __restrict__ out,
-                                                   uint8_t* __restrict__ ids) {
-  extern __shared__ uint32_t cur[];
+// Phase 1 of the scatter: one workgroup per sketch appends its elements to
+// their coarse group's run for this slot in `stage` (runs of ~|S| / G
+// elements, so the writes are long contiguous runs).
+__global__ __launch_bounds__(kB) void k_hb_stage(const uint64_t* __restrict__ data,
+                                                 const uint64_t* __restrict__ starts,
+                                                 const uint32_t* __restrict__ sizes,
+                                                 uint32_t first, uint32_t base, uint32_t log_b,
+                                                 uint32_t log_g, const uint32_t* __restrict__ goff,
+                                                 uint64_t* __restrict__ stage) {
+  __shared__ uint32_t cur[1u << (kJMaxLogB - 6)];
+  const uint32_t G = 1u << log_g;
   const uint32_t i = first + blockIdx.x;
   const uint32_t sz = sizes[i];
   const uint64_t* src = data + starts[i];
-  const uint32_t slot = (i - base) & 63;
-  const uint32_t* o = off + (uint64_t)(i - base) * B;  // this sketch's cursors
-  for (uint32_t b = threadIdx.x; b < B; b += kB) cur[b] = o[b];
+  const uint32_t* o = goff + (uint64_t)(i - base) * G;
+  for (uint32_t g = threadIdx.x; g < G; g += kB) cur[g] = o[g];
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < sz; e += kB) {
     const uint64_t v = src[e];
-    const uint32_t d = atomicAdd(&cur[bucket_hash(v, log_b)], 1u);
-    out[d] = v;
-    ids[d] = (uint8_t)slot;
+    const uint32_t g = bucket_hash(v, log_b) >> (log_b - log_g);
+    stage[atomicAdd(&cur[g], 1u)] = v;
+  }
+}
+
+// Phase 2: one workgroup per (block, coarse group) places the group's
+// elements (64 slot runs in `stage`) at their (bucket, slot) cells. All its
+// writes fall in the group's own contiguous range of the layout (~|S| * 64 / G
+// elements), which L2 assembles into whole lines.
+__global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ stage,
+                                                 const uint32_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ goff,
+                                                 const uint32_t* __restrict__ gcounts, uint32_t B,
+                                                 uint32_t log_b, uint32_t log_g,
+                                                 uint64_t* __restrict__ out,
+                                                 uint8_t* __restrict__ ids) {
+  __shared__ uint32_t cur[64 * 64];  // [slot][bucket in group], B / G <= 64
+  const uint32_t G = 1u << log_g, bpg = B >> log_g;
+  const uint32_t blk = blockIdx.x >> log_g, g = blockIdx.x & (G - 1);
+  const uint64_t rowb = (uint64_t)blk * 64 * B + (uint64_t)g * bpg;
+  for (uint32_t t = threadIdx.x; t < 64 * bpg; t += kB) {
+    const uint32_t slot = t / bpg, bl = t % bpg;
+    cur[slot * 64 + bl] = off[rowb + (uint64_t)slot * B + bl];
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t slot = wave; slot < 64; slot += kB / 64) {
+    const uint64_t gi = ((uint64_t)blk * 64 + slot) * G + g;
+    const uint32_t s0 = goff[gi], n = gcounts[gi];
+    for (uint32_t e = lane; e < n; e += 64) {
+      const uint64_t v = stage[s0 + e];
+      const uint32_t bl = bucket_hash(v, log_b) - g * bpg;
+      const uint32_t d = atomicAdd(&cur[slot * 64 + bl], 1u);
+      out[d] = v;
+      ids[d] = (uint8_t)slot;
+    }
   }
 }
 
@@ -775,48 +828,58 @@ uint32_t join_log_b(uint32_t max_size) {
 
 // temp = counts[len] | off[len] | colsum[cells + 1] | bbase[cells + 1] | scan
 // temporaries, len = n_blk * 64 * B, cells = n_blk * B.
-static size_t layout_head_bytes(uint64_t len, uint64_t cells) {
-  return ((2 * len + 2 * (cells + 1)) * 4 + 15) & ~(size_t)15;
+// Coarse groups of the two-phase scatter: B / G <= 64 buckets each.
+static uint32_t layout_log_g(uint32_t log_b) { return log_b > 6 ? log_b - 6 : 0; }
+
+// temp = counts[len] | off[len] | colsum[cells + 1] | bbase[cells + 1] |
+// gcounts[glen] | goff[glen] | stage[total] (u64) | scan temporaries, with
+// len = n_blk * 64 * B, cells = n_blk * B, glen = n_blk * 64 * G.
+static size_t layout_head_bytes(uint64_t len, uint64_t cells, uint64_t glen, uint64_t total) {
+  const size_t u32s = ((2 * len + 2 * (cells + 1) + 2 * glen) * 4 + 15) & ~(size_t)15;
+  return u32s + ((std::max<uint64_t>(total, 1) * 8 + 15) & ~(size_t)15);
 }
 
-size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b) {
+size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total) {
   const uint64_t n_blk = (count + kTile - 1) / kTile;
   const uint64_t cells = n_blk * (1ull << log_b), len = cells * 64;
+  const uint64_t glen = n_blk * 64 * (1ull << layout_log_g(log_b));
   size_t scan = 0;
   (void)rocprim::exclusive_scan(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
                                 (size_t)(cells + 1), rocprim::plus<uint32_t>(), (hipStream_t)0);
-  return layout_head_bytes(len, cells) + scan + 16;
+  return layout_head_bytes(len, cells, glen, total) + scan + 16;
 }
 
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                             uint32_t first, uint32_t count, uint32_t log_b, uint64_t* out_data,
-                             uint8_t* out_ids, uint32_t* out_boff, uint64_t* out_bstart,
-                             uint32_t* d_stat, void* temp, size_t temp_bytes, hipStream_t s) {
+                             uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
+                             uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
+                             uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
+                             hipStream_t s) {
   static const hipError_t attr_c = hipFuncSetAttribute(
       reinterpret_cast<const void*>(k_hb_count), hipFuncAttributeMaxDynamicSharedMemorySize,
       (int)((1u << kJMaxLogB) * sizeof(uint32_t)));
-  static const hipError_t attr_s = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(k_hb_scatter), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)((1u << kJMaxLogB) * sizeof(uint32_t)));
   if (attr_c != hipSuccess) return attr_c;
-  if (attr_s != hipSuccess) return attr_s;
   if (count == 0) return hipSuccess;
-  const uint32_t B = 1u << log_b;
+  const uint32_t B = 1u << log_b, log_g = layout_log_g(log_b), G = 1u << log_g;
   const uint32_t n_blk = (count + kTile - 1) / kTile;
-  const uint64_t cells = (uint64_t)n_blk * B, len = cells * 64;
+  const uint64_t cells = (uint64_t)n_blk * B, len = cells * 64, glen = (uint64_t)n_blk * 64 * G;
   uint32_t* cnt = static_cast<uint32_t*>(temp);
   uint32_t* off = cnt + len;
   uint32_t* colsum = off + len;
   uint32_t* bbase = colsum + (cells + 1);
-  const size_t head = layout_head_bytes(len, cells);
+  uint32_t* gcnt = bbase + (cells + 1);
+  uint32_t* goff = gcnt + glen;
+  uint64_t* stage = reinterpret_cast<uint64_t*>(
+      static_cast<char*>(temp) + (((2 * len + 2 * (cells + 1) + 2 * glen) * 4 + 15) & ~(size_t)15));
+  const size_t head = layout_head_bytes(len, cells, glen, total);
   if (temp_bytes < head) return hipErrorInvalidValue;
   void* scan_tmp = static_cast<char*>(temp) + head;
   size_t scan_bytes = temp_bytes - head;
   hipError_t e;
   // slots past `count` in the last block have no workgroup: zero counts
   if ((e = hipMemsetAsync(cnt, 0, len * 4, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(gcnt, 0, glen * 4, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_hb_count, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first, first,
-                     B, log_b, cnt);
+                     B, log_b, cnt, G, gcnt);
   hipLaunchKernelGGL(k_hb_colsum, dim3((unsigned)((cells + 1 + kB - 1) / kB)), dim3(kB), 0, s, cnt,
                      n_blk, B, colsum);
   if ((e = rocprim::exclusive_scan(scan_tmp, scan_bytes, colsum, bbase, 0u, (size_t)(cells + 1),
@@ -824,9 +887,11 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
     return e;
   const uint64_t bcells = (uint64_t)n_blk * (B + 1);
   hipLaunchKernelGGL(k_hb_offsets, dim3((unsigned)((bcells + kB - 1) / kB)), dim3(kB), 0, s, cnt,
-                     bbase, n_blk, B, off, out_boff, out_bstart, d_stat);
-  hipLaunchKernelGGL(k_hb_scatter, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first,
-                     first, B, log_b, off, out_data, out_ids);
+                     bbase, n_blk, B, off, out_boff, out_bstart, d_stat, G, gcnt, goff);
+  hipLaunchKernelGGL(k_hb_stage, dim3(count), dim3(kB), 0, s, data, starts, sizes, first, first,
+                     log_b, log_g, goff, stage);
+  hipLaunchKernelGGL(k_hb_place, dim3(n_blk * G), dim3(kB), 0, s, stage, off, goff, gcnt, B, log_b,
+                     log_g, out_data, out_ids);
   return hipGetLastError();
 }
 
@@ -932,7 +997,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   // the join's per-(block, bucket, slot) counting arrays take 8 B x 64 x B per
   // block; beyond a few GB of them (very many sketches) the merge tiles are used
   const bool join_fits = total < (1ull << 32) &&
-                         join_layout_temp_bytes(n, join_log_b(max_size)) < (8ull << 30);
+                         join_layout_temp_bytes(n, join_log_b(max_size), total) < (8ull << 30);
   if (algo != kIntersectMerge && join_fits) {
     // hash-bucketed block-major copy of the column sketches (and of the row
     // range when its blocks are not aligned with the column blocks), then k_join
@@ -944,8 +1009,8 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     uint32_t log_b = join_log_b(max_size);
     for (;;) {
       const uint32_t B = 1u << log_b;
-      const size_t tmp_c = join_layout_temp_bytes(n, log_b);
-      const size_t tmp_r = sep_rows ? join_layout_temp_bytes(rn, log_b) : 0;
+      const size_t tmp_c = join_layout_temp_bytes(n, log_b, total);
+      const size_t tmp_r = sep_rows ? join_layout_temp_bytes(rn, log_b, r_total) : 0;
       size_t o = 0;
       const size_t o_cdat = o; o = align16(o + total * 8);
       const size_t o_cids = o; o = align16(o + total);
@@ -964,14 +1029,14 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       JoinLayout rl = cl;
       uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
       if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
-      if ((e = join_layout_build(data, starts, sizes, 0, n, log_b, const_cast<uint64_t*>(cl.data),
+      if ((e = join_layout_build(data, starts, sizes, 0, n, total, log_b, const_cast<uint64_t*>(cl.data),
                                  const_cast<uint8_t*>(cl.ids), const_cast<uint32_t*>(cl.boff),
                                  const_cast<uint64_t*>(cl.bstart), stat, w + o_tmp, tmp_c, s)) != hipSuccess)
         return e;
       if (sep_rows) {
         rl = JoinLayout{reinterpret_cast<uint64_t*>(w + o_rdat), reinterpret_cast<uint8_t*>(w + o_rids),
                         reinterpret_cast<uint32_t*>(w + o_rbof), reinterpret_cast<uint64_t*>(w + o_rbst)};
-        if ((e = join_layout_build(data, starts, sizes, row_begin, rn, log_b,
+        if ((e = join_layout_build(data, starts, sizes, row_begin, rn, r_total, log_b,
                                    const_cast<uint64_t*>(rl.data), const_cast<uint8_t*>(rl.ids),
                                    const_cast<uint32_t*>(rl.boff), const_cast<uint64_t*>(rl.bstart),
                                    stat, w + o_tmp, tmp_r, s)) != hipSuccess)

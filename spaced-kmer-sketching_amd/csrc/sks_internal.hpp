@@ -146,14 +146,17 @@ struct JoinLayout {
 };
 uint32_t join_cap();                       // elements per join chunk (table capacity)
 uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch of max_size
-size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b);
-// Layout of sketches [first, first + count) into out_*; out_bstart gets
-// ceil(count/64) + 1 entries (the last = element total); *d_stat is raised to
-// the largest block-bucket population (the join needs it <= join_cap()).
+// total = elements of the `count` sketches (sizes the staging array)
+size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total);
+// Layout of sketches [first, first + count) (total elements) into out_*;
+// out_bstart gets ceil(count/64) + 1 entries (the last = element total);
+// *d_stat is raised to the largest block-bucket population (the join needs it
+// <= join_cap()).
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                             uint32_t first, uint32_t count, uint32_t log_b, uint64_t* out_data,
-                             uint8_t* out_ids, uint32_t* out_boff, uint64_t* out_bstart,
-                             uint32_t* d_stat, void* temp, size_t temp_bytes, hipStream_t s);
+                             uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
+                             uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
+                             uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
+                             hipStream_t s);
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t n,
                        uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, int32_t* out, hipStream_t s);
