@@ -596,7 +596,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cpu-sample-mb", type=int, default=60)
+    ap.add_argument("--cpu-sample-mb", type=int, default=125)  # ~10 s of 1-core work
     ap.add_argument("--cpu-crosscheck-mb", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pairs", action="store_true")
