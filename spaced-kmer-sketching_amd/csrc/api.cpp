@@ -535,10 +535,63 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
 
   MetaArena arena(c);
   size_t o_src = arena.add(src_off), o_csr = arena.add(csr), o_uniq = arena.add_zero(k);
+  // narrow bottom-s with every genome's candidates in one workgroup's registers:
+  // sort, unique and select per genome in one kernel (post.hip k_bottom_fused)
+  const bool fused = bottom && !S.wide && max_len <= sks::bottom_fused_capacity() &&
+                     getenv("SKS_NO_FUSED_BOTTOM") == nullptr;
+  std::vector<uint64_t> f_retry, f_pad(1, 0);
+  size_t o_cnt = 0, o_retry = 0, o_pad = 0, o_res = 0;
+  if (fused) {
+    for (uint32_t i = 0; i < k; ++i) {
+      f_retry.push_back(thresh[ok[i]] != ~0ull ? 1 : 0);
+      f_pad.push_back(f_pad.back() + std::min<uint64_t>(S.pol.param, cnt[i]));
+    }
+    o_cnt = arena.add(cnt);
+    o_retry = arena.add(f_retry);
+    o_pad = arena.add(f_pad);
+    o_res = arena.add_zero(k);
+  }
   SKS_TRY(arena.upload());
   uint64_t* d_src = arena.ptr(o_src);
   uint64_t* d_csr = arena.ptr(o_csr);
   uint64_t* d_uniq = arena.ptr(o_uniq);
+
+  if (fused) {
+    SKS_TRY(reserve_cols(c, {5}, f_pad[k] + 1));
+    const sks::BitRuns runs = sks::bit_runs(S.mask_lo);
+    const int kb = std::max(1, __builtin_popcountll(S.mask_lo));
+    SKS_HIP(sks::launch_bottom_fused(reinterpret_cast<uint64_t*>(c->rec[0].ptr), d_src,
+                                     arena.ptr(o_cnt), arena.ptr(o_retry), arena.ptr(o_pad), k,
+                                     S.pol.param, kb, runs, S.kconst, S.pol.flavour, col(c, 5),
+                                     arena.ptr(o_res), st));
+    std::vector<uint64_t> res(k);
+    SKS_HIP(sks::pinned_d2h(res.data(), arena.ptr(o_res), k * sizeof(uint64_t), st));
+    PassOut po;
+    std::vector<uint64_t> limit(k, 0), keep_off(1, 0);
+    uint64_t max_lim = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+      if (res[i] == ~0ull) {
+        retry_local.push_back(ok[i]);  // too few distinct candidates under the threshold
+        continue;
+      }
+      limit[i] = res[i];
+      max_lim = std::max(max_lim, res[i]);
+      final_size_local[ok[i]] = res[i];
+      po.segs.push_back(seg_ids[ok[i]]);
+      keep_off.push_back(keep_off.back() + res[i]);
+    }
+    std::vector<uint64_t> dense = prefix(limit);
+    MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
+    const size_t o_psrc = arena2.add(f_pad), o_pdst = arena2.add(dense);
+    SKS_TRY(arena2.upload());
+    SKS_TRY(alloc_u64(&po.d, dense[k], &po.bytes));
+    SKS_HIP(sks::compact_regions(col(c, 5), po.d, arena2.ptr(o_psrc), arena2.ptr(o_pdst), k,
+                                 max_lim, st));
+    po.off = keep_off;
+    SKS_HIP(hipStreamSynchronize(st));
+    passes.push_back(po);
+    return SKS_OK;
+  }
 
   SKS_TRY(reserve_cols(c, {0, 1, 2, 3, 4, 5, 6, 7, 8, 9}, T + 1));
   SKS_HIP(c->flag.reserve((T + 1) * sizeof(uint32_t)));

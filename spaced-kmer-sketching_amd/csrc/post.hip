@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
 
 #include "sks_hash.hpp"
 #include "sks_internal.hpp"
@@ -360,6 +361,159 @@ __global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restr
   }
 }
 
+// Bottom-s post-processing of one genome in one workgroup, straight from the
+// scan's record region: candidates packed to their mask bits, sorted in the
+// block (rocPRIM block radix sort, keys in registers), duplicates flagged, fmh
+// of the distinct ones into LDS, then k_bottom_select's radix select and an
+// in-order compaction. Replaces compaction + segmented sort + unique + scatter
+// + select (five kernels and a host sync) for genomes of <= kFuseCap candidates.
+// res[g] = sketch size, or ~0 when the genome has fewer than s distinct
+// candidates under a finite threshold (the build retries it). The sorted
+// packed keys are written back over the record region.
+constexpr uint32_t kFuseItems = 16;
+constexpr uint32_t kFuseCap = kSelB * kFuseItems;  // 16384 candidates
+#ifndef SKS_FUSE_RADIX_BITS
+#define SKS_FUSE_RADIX_BITS 0
+#endif
+#ifndef SKS_FUSE_RANK
+#define SKS_FUSE_RANK default_for_radix_sort
+#endif
+using FuseSort = rocprim::block_radix_sort<unsigned long long, kSelB, kFuseItems, rocprim::empty_type,
+                                           1, 1, SKS_FUSE_RADIX_BITS,
+                                           rocprim::block_radix_rank_algorithm::SKS_FUSE_RANK>;
+constexpr size_t kFuseLds = sizeof(FuseSort::storage_type) > kFuseCap * sizeof(uint64_t)
+                                ? sizeof(FuseSort::storage_type)
+                                : kFuseCap * sizeof(uint64_t);
+
+template <int FLAVOUR>
+__global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ rec,
+                                                        const uint64_t* __restrict__ src_off,
+                                                        const uint64_t* __restrict__ cnt,
+                                                        const uint64_t* __restrict__ retry_ok,
+                                                        const uint64_t* __restrict__ dst_off,
+                                                        uint64_t s_param, int key_bits,
+                                                        const BitRuns runs, uint64_t kconst,
+                                                        uint64_t* __restrict__ out,
+                                                        uint64_t* __restrict__ res) {
+  extern __shared__ unsigned char smem[];
+  auto& sort_storage = *reinterpret_cast<FuseSort::storage_type*>(smem);
+  uint64_t* f = reinterpret_cast<uint64_t*>(smem);  // reused after the sort
+  __shared__ uint32_t dup[kFuseCap / 32];            // 1 = not a distinct candidate
+  __shared__ unsigned long long s_last[kSelB];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t wsum[kSelWaves];
+  __shared__ uint32_t s_digit, s_below;
+  const uint32_t g = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint64_t base = src_off[g];
+  const uint32_t n = (uint32_t)cnt[g];  // <= kFuseCap (host-checked)
+
+  unsigned long long k[kFuseItems];
+#pragma unroll
+  for (uint32_t j = 0; j < kFuseItems; ++j) {
+    const uint32_t i = tid * kFuseItems + j;
+    k[j] = i < n ? runs_pack(rec[base + i], runs) : ~0ull;  // pads sort after equal keys
+  }
+  FuseSort().sort(k, sort_storage, 0, key_bits);
+  s_last[tid] = k[kFuseItems - 1];
+  __syncthreads();
+  const unsigned long long before = tid ? s_last[tid - 1] : 0ull;
+  uint64_t fv[kFuseItems];
+  uint32_t mine = 0, dmask = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kFuseItems; ++j) {
+    const uint32_t i = tid * kFuseItems + j;
+    const bool is_dup = i > 0 && k[j] == (j ? k[j - 1] : before);
+    const bool valid = i < n && !is_dup;
+    if (i < n) rec[base + i] = k[j];
+    fv[j] = valid ? hash_bitset128<FLAVOUR>(runs_expand(k[j], runs), 0) ^ kconst : 0ull;
+    mine += valid ? 1u : 0u;
+    dmask |= (valid ? 0u : 1u) << j;
+  }
+  __syncthreads();  // the sort storage becomes f[]
+#pragma unroll
+  for (uint32_t j = 0; j < kFuseItems; ++j) f[tid * kFuseItems + j] = fv[j];
+  // 16 flags per thread: half of a 32-bit word
+  if (tid < (int)(kFuseCap / 32)) dup[tid] = 0;
+  __syncthreads();
+  atomicOr(&dup[(tid * kFuseItems) >> 5], dmask << ((tid * kFuseItems) & 31));
+  uint32_t distinct;
+  {
+    uint32_t v = mine;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((tid & 63) == 0) wsum[tid >> 6] = v;
+    __syncthreads();
+    distinct = 0;
+#pragma unroll
+    for (int w = 0; w < kSelWaves; ++w) distinct += wsum[w];
+    __syncthreads();
+  }
+  if (distinct < s_param && retry_ok[g]) {
+    if (tid == 0) res[g] = ~0ull;
+    return;
+  }
+  const uint64_t lim = distinct < s_param ? distinct : s_param;
+  if (tid == 0) res[g] = lim;
+  uint64_t* dst = out + dst_off[g];
+  auto valid_at = [&](uint32_t i) { return i < n && !((dup[i >> 5] >> (i & 31)) & 1u); };
+  uint64_t prefix = 0;
+  uint32_t kk = (uint32_t)lim;
+  const bool all = distinct <= lim;
+  if (!all) {
+    uint64_t pmask = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += kSelB) hist[i] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < n; i += kSelB) {
+        const uint64_t v = f[i];
+        if (valid_at(i) && (v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid < 64) {  // wave 0: the digit where the running count reaches kk
+        uint32_t h4[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { h4[q] = hist[4 * tid + q]; sum += h4[q]; }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = __shfl_up(incl, o, 64);
+          if (tid >= o) incl += t;
+        }
+        const uint64_t bal = __ballot(incl >= kk);
+        const int L = __builtin_ctzll(bal);
+        if (tid == L) {
+          uint32_t c = incl - sum;
+          int q = 0;
+          while (c + h4[q] < kk) c += h4[q++];
+          s_digit = 4 * L + q;
+          s_below = c;
+        }
+      }
+      __syncthreads();
+      prefix |= (uint64_t)s_digit << shift;
+      pmask |= 255ull << shift;
+      kk -= s_below;
+      __syncthreads();
+    }
+  }
+  // keep (all distinct) or (fmh < F*, and the first kk with fmh == F*), in k-mer order
+  uint32_t eq_base = 0, out_base = 0;
+  for (uint32_t b0 = 0; b0 < n; b0 += kSelB) {
+    const uint32_t i = b0 + tid;
+    const bool ok = valid_at(i);
+    const uint64_t v = ok ? f[i] : ~0ull;
+    const bool eq = ok && !all && v == prefix;
+    uint32_t eq_tot, keep_tot;
+    const uint32_t eq_rank = eq_base + block_rank(eq, wsum, &eq_tot);
+    const bool keep = ok && (all || v < prefix || (eq && eq_rank < kk));
+    const uint32_t pos = out_base + block_rank(keep, wsum, &keep_tot);
+    if (keep) dst[pos] = runs_expand(rec[base + i], runs);
+    eq_base += eq_tot;
+    out_base += keep_tot;
+  }
+}
+
 template <int FLAVOUR>
 __global__ void k_fmh_narrow(uint64_t* __restrict__ keys, uint64_t n, uint64_t kconst) {
   const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
@@ -553,6 +707,31 @@ hipError_t launch_bottom_select(const uint64_t* uk, const uint64_t* d_uoff, cons
   else
     hipLaunchKernelGGL(k_bottom_select<1>, dim3(n_seg), dim3(kSelB), lds, s, uk, d_uoff, d_dst, d_lim,
                        kconst, out);
+  return hipGetLastError();
+}
+
+uint32_t bottom_fused_capacity() { return kFuseCap; }
+
+hipError_t launch_bottom_fused(uint64_t* rec, const uint64_t* d_src_off, const uint64_t* d_cnt,
+                               const uint64_t* d_retry_ok, const uint64_t* d_dst_off,
+                               uint32_t n_seg, uint64_t s_param, int key_bits, const BitRuns& runs,
+                               uint64_t kconst, int flavour, uint64_t* out, uint64_t* d_res,
+                               hipStream_t s) {
+  if (n_seg == 0) return hipSuccess;
+  static const hipError_t a0 = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_bottom_fused<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)kFuseLds);
+  static const hipError_t a1 = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(k_bottom_fused<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      (int)kFuseLds);
+  if (a0 != hipSuccess) return a0;
+  if (a1 != hipSuccess) return a1;
+  if (flavour == 0)
+    hipLaunchKernelGGL(k_bottom_fused<0>, dim3(n_seg), dim3(kSelB), kFuseLds, s, rec, d_src_off,
+                       d_cnt, d_retry_ok, d_dst_off, s_param, key_bits, runs, kconst, out, d_res);
+  else
+    hipLaunchKernelGGL(k_bottom_fused<1>, dim3(n_seg), dim3(kSelB), kFuseLds, s, rec, d_src_off,
+                       d_cnt, d_retry_ok, d_dst_off, s_param, key_bits, runs, kconst, out, d_res);
   return hipGetLastError();
 }
 

@@ -160,6 +160,20 @@ def test_bottom_s_many_genomes(torch_cuda, ctx):
             check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
 
 
+def test_bottom_s_unfused_paths(torch_cuda, ctx, monkeypatch):
+    """The per-genome fused post kernel is the default for genomes of <= 16384
+    candidates; SKS_NO_FUSED_BOTTOM routes them through compaction + segmented
+    sort + unique + k_bottom_select instead. Both must give the oracle's sets."""
+    genomes = [synth.bases(3000 + 997 * i, seed=1300 + i % 3, mut_seed=1400 + i,
+                           mut_rate=0.02 * (i % 4)).tobytes() for i in range(40)]
+    m = O.mask(31, 21, 5)
+    monkeypatch.setenv("SKS_NO_FUSED_BOTTOM", "1")
+    for flavour in (0, 1):
+        for s_ in (1, 300):
+            ss, _ = build(torch_cuda, ctx, genomes, 31, m, "bottom", s_, flavour)
+            check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
+
+
 def test_bottom_s_low_complexity_forces_threshold_retry(torch_cuda, ctx):
     # periodic genome: few distinct k-mers, so the first threshold pass finds
     # fewer than s candidates and the build must raise the threshold
