@@ -327,6 +327,35 @@ def test_concurrent_contexts_on_streams(torch_cuda, ctx):
     assert not bad, bad
 
 
+def test_block_cache_reuse_and_eviction(torch_cuda, ctx):
+    """Sketch arrays freed (plainly or stream-ordered) return to the block cache
+    and are handed to later builds; more than its 16 blocks evicts the oldest.
+    Sets built from recycled arrays equal fresh ones and the oracle."""
+    torch = torch_cuda
+    m = O.mask(31, 21, 1)
+    genomes = _genomes(77, [5000, 20000, 60000, 150000])
+    want = []
+    for i, g in enumerate(genomes):
+        ss, _ = build(torch, ctx, [g], 31, m, "frac", 7 + i)
+        want.append(ss.sketch(0))
+        del ss
+    st = torch.cuda.Stream()
+    for rnd in range(3):
+        held = []
+        for i, g in enumerate(genomes * 6):  # 24 sets alive: more blocks than the cache keeps
+            ss, _ = build(torch, ctx, [g], 31, m, "frac", 7 + i % 4)
+            assert np.array_equal(ss.sketch(0), want[i % 4]), (rnd, i)
+            held.append(ss)
+        for j, ss in enumerate(held):
+            if (j + rnd) % 2:
+                ss.free(stream=st.cuda_stream)
+            else:
+                ss.free()
+    torch.cuda.synchronize()
+    ss, _ = build(torch, ctx, genomes, 31, m, "frac", 7)
+    check_against_oracle(ss, genomes, 31, m, "frac", 7)
+
+
 def test_argument_errors(torch_cuda, ctx):
     torch = torch_cuda
     d = upload(torch, b"ACGTACGT\n")
