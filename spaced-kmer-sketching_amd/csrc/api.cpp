@@ -562,7 +562,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     const int kb = std::max(1, __builtin_popcountll(S.mask_lo));
     SKS_HIP(sks::launch_bottom_fused(reinterpret_cast<uint64_t*>(c->rec[0].ptr), d_src,
                                      arena.ptr(o_cnt), arena.ptr(o_retry), arena.ptr(o_pad), k,
-                                     S.pol.param, kb, runs, S.kconst, S.pol.flavour, col(c, 5),
+                                     max_len, S.pol.param, kb, runs, S.kconst, S.pol.flavour, col(c, 5),
                                      arena.ptr(o_res), st));
     std::vector<uint64_t> res(k);
     SKS_HIP(sks::pinned_d2h(res.data(), arena.ptr(o_res), k * sizeof(uint64_t), st));

@@ -370,22 +370,28 @@ __global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restr
 // res[g] = sketch size, or ~0 when the genome has fewer than s distinct
 // candidates under a finite threshold (the build retries it). The sorted
 // packed keys are written back over the record region.
-constexpr uint32_t kFuseItems = 16;
-constexpr uint32_t kFuseCap = kSelB * kFuseItems;  // 16384 candidates
+// ITEMS keys per thread (8, 12 or 16): the smallest that holds the pass's
+// largest genome, so that padding is not sorted (pads cost as much as keys).
+constexpr uint32_t kFuseMaxItems = 16;
+constexpr uint32_t kFuseCap = kSelB * kFuseMaxItems;  // 16384 candidates
 #ifndef SKS_FUSE_RADIX_BITS
 #define SKS_FUSE_RADIX_BITS 0
 #endif
 #ifndef SKS_FUSE_RANK
 #define SKS_FUSE_RANK default_for_radix_sort
 #endif
-using FuseSort = rocprim::block_radix_sort<unsigned long long, kSelB, kFuseItems, rocprim::empty_type,
-                                           1, 1, SKS_FUSE_RADIX_BITS,
+template <int ITEMS>
+using FuseSort = rocprim::block_radix_sort<unsigned long long, kSelB, ITEMS, rocprim::empty_type, 1, 1,
+                                           SKS_FUSE_RADIX_BITS,
                                            rocprim::block_radix_rank_algorithm::SKS_FUSE_RANK>;
-constexpr size_t kFuseLds = sizeof(FuseSort::storage_type) > kFuseCap * sizeof(uint64_t)
-                                ? sizeof(FuseSort::storage_type)
-                                : kFuseCap * sizeof(uint64_t);
+template <int ITEMS>
+constexpr size_t fuse_lds() {
+  return sizeof(typename FuseSort<ITEMS>::storage_type) > kSelB * ITEMS * sizeof(uint64_t)
+             ? sizeof(typename FuseSort<ITEMS>::storage_type)
+             : kSelB * ITEMS * sizeof(uint64_t);
+}
 
-template <int FLAVOUR>
+template <int FLAVOUR, int ITEMS>
 __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ rec,
                                                         const uint64_t* __restrict__ src_off,
                                                         const uint64_t* __restrict__ cnt,
@@ -395,10 +401,11 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
                                                         const BitRuns runs, uint64_t kconst,
                                                         uint64_t* __restrict__ out,
                                                         uint64_t* __restrict__ res) {
+  constexpr uint32_t kCap = kSelB * ITEMS;
   extern __shared__ unsigned char smem[];
-  auto& sort_storage = *reinterpret_cast<FuseSort::storage_type*>(smem);
+  auto& sort_storage = *reinterpret_cast<typename FuseSort<ITEMS>::storage_type*>(smem);
   uint64_t* f = reinterpret_cast<uint64_t*>(smem);  // reused after the sort
-  __shared__ uint32_t dup[kFuseCap / 32];            // 1 = not a distinct candidate
+  __shared__ uint32_t dup[kCap / 32];                // 1 = not a distinct candidate
   __shared__ unsigned long long s_last[kSelB];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t wsum[kSelWaves];
@@ -406,23 +413,23 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   const uint32_t g = blockIdx.x;
   const int tid = threadIdx.x;
   const uint64_t base = src_off[g];
-  const uint32_t n = (uint32_t)cnt[g];  // <= kFuseCap (host-checked)
+  const uint32_t n = (uint32_t)cnt[g];  // <= kCap (host-checked)
 
-  unsigned long long k[kFuseItems];
+  unsigned long long k[ITEMS];
 #pragma unroll
-  for (uint32_t j = 0; j < kFuseItems; ++j) {
-    const uint32_t i = tid * kFuseItems + j;
+  for (uint32_t j = 0; j < ITEMS; ++j) {
+    const uint32_t i = tid * ITEMS + j;
     k[j] = i < n ? runs_pack(rec[base + i], runs) : ~0ull;  // pads sort after equal keys
   }
-  FuseSort().sort(k, sort_storage, 0, key_bits);
-  s_last[tid] = k[kFuseItems - 1];
+  FuseSort<ITEMS>().sort(k, sort_storage, 0, key_bits);
+  s_last[tid] = k[ITEMS - 1];
   __syncthreads();
   const unsigned long long before = tid ? s_last[tid - 1] : 0ull;
-  uint64_t fv[kFuseItems];
+  uint64_t fv[ITEMS];
   uint32_t mine = 0, dmask = 0;
 #pragma unroll
-  for (uint32_t j = 0; j < kFuseItems; ++j) {
-    const uint32_t i = tid * kFuseItems + j;
+  for (uint32_t j = 0; j < ITEMS; ++j) {
+    const uint32_t i = tid * ITEMS + j;
     const bool is_dup = i > 0 && k[j] == (j ? k[j - 1] : before);
     const bool valid = i < n && !is_dup;
     if (i < n) rec[base + i] = k[j];
@@ -432,11 +439,15 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   }
   __syncthreads();  // the sort storage becomes f[]
 #pragma unroll
-  for (uint32_t j = 0; j < kFuseItems; ++j) f[tid * kFuseItems + j] = fv[j];
-  // 16 flags per thread: half of a 32-bit word
-  if (tid < (int)(kFuseCap / 32)) dup[tid] = 0;
+  for (uint32_t j = 0; j < ITEMS; ++j) f[tid * ITEMS + j] = fv[j];
+  if (tid < (int)(kCap / 32)) dup[tid] = 0;
   __syncthreads();
-  atomicOr(&dup[(tid * kFuseItems) >> 5], dmask << ((tid * kFuseItems) & 31));
+  // ITEMS flags per thread; a thread's run may straddle two 32-bit words
+  {
+    const uint32_t bit0 = tid * ITEMS, w0 = bit0 >> 5, sh = bit0 & 31;
+    atomicOr(&dup[w0], dmask << sh);
+    if (sh + ITEMS > 32) atomicOr(&dup[w0 + 1], dmask >> (32 - sh));
+  }
   uint32_t distinct;
   {
     uint32_t v = mine;
@@ -714,25 +725,24 @@ uint32_t bottom_fused_capacity() { return kFuseCap; }
 
 hipError_t launch_bottom_fused(uint64_t* rec, const uint64_t* d_src_off, const uint64_t* d_cnt,
                                const uint64_t* d_retry_ok, const uint64_t* d_dst_off,
-                               uint32_t n_seg, uint64_t s_param, int key_bits, const BitRuns& runs,
-                               uint64_t kconst, int flavour, uint64_t* out, uint64_t* d_res,
-                               hipStream_t s) {
+                               uint32_t n_seg, uint64_t max_cnt, uint64_t s_param, int key_bits,
+                               const BitRuns& runs, uint64_t kconst, int flavour, uint64_t* out,
+                               uint64_t* d_res, hipStream_t s) {
   if (n_seg == 0) return hipSuccess;
-  static const hipError_t a0 = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(k_bottom_fused<0>), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)kFuseLds);
-  static const hipError_t a1 = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(k_bottom_fused<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)kFuseLds);
-  if (a0 != hipSuccess) return a0;
-  if (a1 != hipSuccess) return a1;
-  if (flavour == 0)
-    hipLaunchKernelGGL(k_bottom_fused<0>, dim3(n_seg), dim3(kSelB), kFuseLds, s, rec, d_src_off,
-                       d_cnt, d_retry_ok, d_dst_off, s_param, key_bits, runs, kconst, out, d_res);
-  else
-    hipLaunchKernelGGL(k_bottom_fused<1>, dim3(n_seg), dim3(kSelB), kFuseLds, s, rec, d_src_off,
-                       d_cnt, d_retry_ok, d_dst_off, s_param, key_bits, runs, kconst, out, d_res);
-  return hipGetLastError();
+  auto go = [&](auto kernel, size_t lds) -> hipError_t {
+    const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (a != hipSuccess) return a;
+    hipLaunchKernelGGL(kernel, dim3(n_seg), dim3(kSelB), lds, s, rec, d_src_off, d_cnt, d_retry_ok,
+                       d_dst_off, s_param, key_bits, runs, kconst, out, d_res);
+    return hipGetLastError();
+  };
+  if (max_cnt <= kSelB * 8)
+    return flavour == 0 ? go(k_bottom_fused<0, 8>, fuse_lds<8>()) : go(k_bottom_fused<1, 8>, fuse_lds<8>());
+  if (max_cnt <= kSelB * 12)
+    return flavour == 0 ? go(k_bottom_fused<0, 12>, fuse_lds<12>())
+                        : go(k_bottom_fused<1, 12>, fuse_lds<12>());
+  return flavour == 0 ? go(k_bottom_fused<0, 16>, fuse_lds<16>()) : go(k_bottom_fused<1, 16>, fuse_lds<16>());
 }
 
 hipError_t launch_iota(uint64_t* out, uint64_t n, hipStream_t s) {

@@ -88,9 +88,9 @@ hipError_t launch_bits_expand(uint64_t* keys, uint64_t n, const BitRuns& runs, h
 uint32_t bottom_fused_capacity();
 hipError_t launch_bottom_fused(uint64_t* rec, const uint64_t* d_src_off, const uint64_t* d_cnt,
                                const uint64_t* d_retry_ok, const uint64_t* d_dst_off,
-                               uint32_t n_seg, uint64_t s_param, int key_bits, const BitRuns& runs,
-                               uint64_t kconst, int flavour, uint64_t* out, uint64_t* d_res,
-                               hipStream_t s);
+                               uint32_t n_seg, uint64_t max_cnt, uint64_t s_param, int key_bits,
+                               const BitRuns& runs, uint64_t kconst, int flavour, uint64_t* out,
+                               uint64_t* d_res, hipStream_t s);
 
 // Compact sparse survivor regions [off[g], off[g] + cnt[g]) into dense CSR,
 // packing each value's mask bits when `pack` is given.
