@@ -276,6 +276,43 @@ def test_frac_chunk_union_property(torch_cuda, ctx):
         assert sksffi.frac_min_hash(int(x), m, w, 1, 0) % 1000 == 0
 
 
+def test_genome_over_4gb_chunk_union(torch_cuda, ctx):
+    """Maximum sizes: one 4.6 GB genome (byte offsets, tile and window counts past
+    2^32) equals the union of the sketches of two halves with a (w-1)-base halo,
+    and its window count is exact; FracMinHash 1/1000 and bottom-s both ways."""
+    torch = torch_cuda
+    L, w = 4_600_000_000, 31
+    m = O.mask(31, 21, 0)
+    dev = torch.empty(L + 1, dtype=torch.uint8, device="cuda:0")
+    ctx.synth_bases(dev.data_ptr(), L, 4242)
+    dev[L] = ord("\n")
+    torch.cuda.synchronize()
+    whole = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, sksffi.SKS_FRAC_MOD, 1000)
+    assert int(whole.windows()[0]) == L - w + 1
+    cut = 2_300_000_017
+    a = ctx.sketch_build(dev.data_ptr(), cut + w - 1, [0, cut + w - 1], w, m, sksffi.SKS_FRAC_MOD,
+                         1000)
+    b = ctx.sketch_build(dev.data_ptr() + cut, L + 1 - cut, [0, L + 1 - cut], w, m,
+                         sksffi.SKS_FRAC_MOD, 1000)
+    union = np.union1d(a.sketch(0)[:, 0], b.sketch(0)[:, 0])
+    S = whole.sketch(0)[:, 0]
+    assert np.array_equal(union, S)
+    assert int(a.windows()[0]) + int(b.windows()[0]) == L - w + 1
+    for x in S[:: max(1, len(S) // 200)]:
+        assert sksffi.frac_min_hash(int(x), m, w, 1, 0) % 1000 == 0
+    # bottom-s over the whole genome: the s smallest fmh of the union of the halves' bottom-s
+    s_ = 10000
+    bw = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, sksffi.SKS_BOTTOM_S, s_).sketch(0)[:, 0]
+    ba = ctx.sketch_build(dev.data_ptr(), cut + w - 1, [0, cut + w - 1], w, m, sksffi.SKS_BOTTOM_S,
+                          s_).sketch(0)[:, 0]
+    bb = ctx.sketch_build(dev.data_ptr() + cut, L + 1 - cut, [0, L + 1 - cut], w, m,
+                          sksffi.SKS_BOTTOM_S, s_).sketch(0)[:, 0]
+    cand = np.union1d(ba, bb)
+    keyed = sorted((sksffi.frac_min_hash(int(x), m, w, 1, 0), int(x)) for x in cand)[:s_]
+    assert np.array_equal(np.array(sorted(x for _, x in keyed), dtype=np.uint64), bw)
+    del dev
+
+
 def test_concurrent_contexts_on_streams(torch_cuda, ctx):
     """bench.py's headline mode: builds from several host threads, one context
     per HIP stream, in flight together (and sets freed, both ways, while another
