@@ -237,12 +237,29 @@ std::vector<int> pair_counts(const std::vector<const kmer_set*>& a,
   check_hip(hipMemcpy(d_sizes.p, sizes.data(), sizes.size() * 4, hipMemcpyHostToDevice), "H2D");
   check_hip(hipMemcpy(d_a.p, ia.data(), ia.size() * 4, hipMemcpyHostToDevice), "H2D");
   check_hip(hipMemcpy(d_b.p, ib.data(), ib.size() * 4, hipMemcpyHostToDevice), "H2D");
-  check(sks_intersect_pairs(ctx(), d_words.as<uint64_t>(), d_starts.as<uint64_t>(),
-                            d_sizes.as<uint32_t>(), ew, d_a.as<int32_t>(), d_b.as<int32_t>(),
-                            a.size(), d_out.as<int32_t>()));
-  check(sks_ctx_synchronize(ctx()));
   std::vector<int32_t> res(a.size());
-  check_hip(hipMemcpy(res.data(), d_out.p, res.size() * 4, hipMemcpyDeviceToHost), "D2H");
+  const uint64_t n = uniq.size();
+  // Pair lists that cover a large part of the n x n matrix — the reference's
+  // main flow intersects generate_all_pairs_from_vector's list
+  // (kmer-sketching.cpp:195-200) — are counted as the whole symmetric matrix by
+  // the join kernel (sks_intersect_sym) and gathered; sparse lists go through
+  // one wavefront per pair (sks_intersect_pairs).
+  if (n >= 64 && n <= 16384 && a.size() * 4 >= n * n) {
+    DevMem d_mat(n * n * 4);
+    check(sks_intersect_sym(ctx(), d_words.as<uint64_t>(), d_starts.as<uint64_t>(),
+                            d_sizes.as<uint32_t>(), ew, (uint32_t)n, 0, sks_intersect_sym_tiles((uint32_t)n),
+                            d_mat.as<int32_t>()));
+    check(sks_ctx_synchronize(ctx()));
+    std::vector<int32_t> mat(n * n);
+    check_hip(hipMemcpy(mat.data(), d_mat.p, mat.size() * 4, hipMemcpyDeviceToHost), "D2H");
+    for (size_t i = 0; i < a.size(); ++i) res[i] = mat[(uint64_t)ia[i] * n + ib[i]];
+  } else {
+    check(sks_intersect_pairs(ctx(), d_words.as<uint64_t>(), d_starts.as<uint64_t>(),
+                              d_sizes.as<uint32_t>(), ew, d_a.as<int32_t>(), d_b.as<int32_t>(),
+                              a.size(), d_out.as<int32_t>()));
+    check(sks_ctx_synchronize(ctx()));
+    check_hip(hipMemcpy(res.data(), d_out.p, res.size() * 4, hipMemcpyDeviceToHost), "D2H");
+  }
   for (size_t i = 0; i < a.size(); ++i) {
     const bool same = a[i]->mask == b[i]->mask || a[i]->elements.empty() || b[i]->elements.empty();
     out[i] = same ? res[i] : 0;

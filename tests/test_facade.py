@@ -74,3 +74,27 @@ def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
     for p, (i, j) in enumerate([(i, j) for i in range(n) for j in range(n)]):
         c = O.containment(inter[p], len(sk[i]))
         assert float.fromhex(out["ani"][p]) == O.binomial_estimator(c, kk)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,k,param", [(31, 21, 10), (40, 30, 5)])
+def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param):
+    """70 sets: the all-pairs list of generate_all_pairs_from_vector covers the
+    whole matrix, so the facade counts it with the symmetric join
+    (sks_intersect_sym) and gathers; counts and ANI equal the oracle's."""
+    files = []
+    for i in range(70):
+        g = synth.bases(3000, seed=900 + i % 5, mut_seed=950 + i, mut_rate=0.02 * (i % 3))
+        p = tmp_path / f"h{i}.fa"
+        p.write_bytes(synth.fasta_text([(f"h{i}", g)], width=60))
+        files.append(str(p))
+    r = subprocess.run([facade_bin, "sketch", str(w), str(k), "0", str(param), "frac"] + files,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    m = O.mask(w, k, 0)
+    sk = [O.sketch(O.fasta_runs(f), w, m, "frac", param)[0] for f in files]
+    n = len(files)
+    inter = [O.intersect(sk[i], sk[j]) for i in range(n) for j in range(n)]
+    assert out["inter"] == inter
+    assert out["inter_serial_equal"]
