@@ -25,6 +25,8 @@
 // launch instead of one per survivor.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 #include <type_traits>
 
@@ -219,6 +221,20 @@ __device__ __forceinline__ uint64_t fmh_narrow(const ScanParams& p, uint64_t c) 
   return h ^ p.kconst;
 }
 
+// Flavour B up to the third hash_mix's second multiply: h = mix(mix(c+K)+K);
+// x = h + 128 + K; x ^= x >> 32; x *= M; x ^= x >> 32. The rest of the hash
+// is H = y ^ (y >> 28) with y = x * M, and fmh = H ^ kconst. The low 4 bits
+// of H need only the low 32 bits of y, i.e. one v_mul_lo_u32 (low-bits
+// pre-filter of the FracMinHash test, scan_kernel<..., PRE = 1>).
+__device__ __forceinline__ uint64_t mix3_head(uint64_t c) {
+  uint64_t h = hash_mix(c + kGolden32);
+  h = hash_mix(h + kGolden32);
+  uint64_t x = h + (128 + kGolden32);
+  x ^= x >> 32;
+  x = mul_const<kMixMul>(x);
+  return x ^ (x >> 32);
+}
+
 template <int MODE>
 __device__ __forceinline__ bool keep_fmh(const ScanParams& p, uint64_t f, uint64_t thresh) {
   if constexpr (MODE != kModeBottom) return div_test(f, p.low_mask, p.high_mask, p.dinv, p.dlim);
@@ -231,13 +247,17 @@ constexpr int kBeOff = 2;  // s_be[kBeOff + i] = word i; two zero words in front
 #define SKS_SCAN_MIN_WAVES 1
 #endif
 
-template <int MODE, int FLAVOUR>
+constexpr uint32_t kCandCap = 128;  // pre-filter candidates per wave (< 64 + 64)
+
+template <int MODE, int FLAVOUR, int PRE = 0>
 __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanParams p) {
   __shared__ uint32_t s_raw[kLoadVecs * 4];
   __shared__ uint32_t s_be[kWords + 2 + kBeOff];
   __shared__ uint32_t s_lc[kWords + 2];
   __shared__ uint32_t s_inv[kWords + 2];
   __shared__ Queue<MODE> q;
+  // (z, c) of windows past the low-bits pre-filter, per wave (PRE only)
+  __shared__ ulonglong2 s_cand[PRE ? (kBlock / 64) * kCandCap : 1];
 
   const int tid = threadIdx.x;
   const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
@@ -342,6 +362,60 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
     // Hot loop: no branches — one keep bit per window, so the compiler can
     // interleave the 16 independent hash chains.  Survivors (~1/c) are
     // re-derived and emitted afterwards.
+    if constexpr (PRE) {
+      // FracMinHash with an even c: a window survives only if the low
+      // min(s, 4) bits of its fmh are zero, and those follow from the low 32
+      // bits of the last multiply. Windows passing that test (1/8 for c = 1000)
+      // are queued per wave in LDS and finished 64 at a time, all lanes busy.
+      const int lane = tid & 63;
+      ulonglong2* cb = s_cand + (tid >> 6) * kCandCap;
+      const uint32_t pmask = p.low_mask & 0xFu;
+      const uint32_t klo = (uint32_t)p.kconst;
+      uint32_t cnt = 0;  // wave-uniform
+      auto finish = [&](uint32_t n) {  // candidates [0, n), n <= 64
+        __builtin_amdgcn_wave_barrier();
+        if ((uint32_t)lane < n) {
+          const ulonglong2 e = cb[lane];
+          uint64_t y = mul_const<kMixMul>(e.x);
+          y ^= y >> 28;
+          if (div_test(y ^ p.kconst, p.low_mask, p.high_mask, p.dinv, p.dlim))
+            emit<MODE>(p, q, g.seg, e.y, 0);
+        }
+        __builtin_amdgcn_wave_barrier();
+      };
+      auto windows_pre = [&](auto checked) {
+#pragma unroll
+        for (int j = 0; j < kWPT; ++j) {
+          const uint64_t c = canon(j);
+          const uint64_t z = mix3_head(c);
+          const uint32_t ylo = (uint32_t)z * (uint32_t)kMixMul;
+          bool pass = ((ylo ^ (ylo >> 28) ^ klo) & pmask) == 0;
+          if constexpr (decltype(checked)::value) {
+            const bool valid = ((inv64 >> j) & wmask_bits) == 0;
+            win_count += valid ? 1u : 0u;
+            pass = pass && valid;
+          }
+          const uint64_t bal = __ballot(pass);
+          const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (pass) cb[cnt + below] = make_ulonglong2(z, c);
+          cnt += (uint32_t)__popcll(bal);
+          if (cnt >= 64) {
+            finish(64);
+            const uint32_t rest = cnt - 64;  // < 64: move them to the front
+            ulonglong2 t = make_ulonglong2(0, 0);
+            if ((uint32_t)lane < rest) t = cb[64 + lane];
+            __builtin_amdgcn_wave_barrier();
+            if ((uint32_t)lane < rest) cb[lane] = t;
+            cnt = rest;
+          }
+        }
+        if constexpr (!decltype(checked)::value) win_count += kWPT;
+      };
+      if (__all(lane_clean)) windows_pre(std::false_type{});
+      else windows_pre(std::true_type{});
+      if (cnt) finish(cnt);
+    } else {
     uint32_t keepmask = 0;
     auto windows = [&](auto checked) {
 #pragma unroll
@@ -373,6 +447,7 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
         else emit<MODE>(p, q, g.seg, c, c);
       }
     }
+    }  // !PRE
 
     // 5) flush the queue once it is half full
     __syncthreads();
@@ -569,7 +644,11 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
     return hipGetLastError();
   };
   if (!wide) {
-    if (mode == kModeFrac) return flavour == 0 ? pick(scan_kernel<kModeFrac, 0>) : pick(scan_kernel<kModeFrac, 1>);
+    if (mode == kModeFrac) {
+      static const bool no_pre = getenv("SKS_NO_PREFILTER") != nullptr;
+      if (flavour == 0 && (p.low_mask & 0xFu) && !no_pre) return pick(scan_kernel<kModeFrac, 0, 1>);
+      return flavour == 0 ? pick(scan_kernel<kModeFrac, 0>) : pick(scan_kernel<kModeFrac, 1>);
+    }
     if (mode == kModeList) return flavour == 0 ? pick(scan_kernel<kModeList, 0>) : pick(scan_kernel<kModeList, 1>);
     return flavour == 0 ? pick(scan_kernel<kModeBottom, 0>) : pick(scan_kernel<kModeBottom, 1>);
   }
