@@ -383,9 +383,7 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
         }
         __builtin_amdgcn_wave_barrier();
       };
-      auto windows_pre = [&](auto checked) {
-#pragma unroll
-        for (int j = 0; j < kWPT; ++j) {
+      auto window_pre = [&](auto checked, int j) {
           const uint64_t c = canon(j);
           const uint64_t z = mix3_head(c);
           const uint32_t ylo = (uint32_t)z * (uint32_t)kMixMul;
@@ -409,11 +407,15 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
             if ((uint32_t)lane < rest) cb[lane] = t;
             cnt = rest;
           }
-        }
-        if constexpr (!decltype(checked)::value) win_count += kWPT;
       };
-      if (__all(lane_clean)) windows_pre(std::false_type{});
-      else windows_pre(std::true_type{});
+      if (__all(lane_clean)) {
+#pragma unroll
+        for (int j = 0; j < kWPT; ++j) window_pre(std::false_type{}, j);
+        win_count += kWPT;
+      } else {  // waves holding an invalid base: rare, kept out of the unrolled code
+#pragma unroll 1
+        for (int j = 0; j < kWPT; ++j) window_pre(std::true_type{}, j);
+      }
       if (cnt) finish(cnt);
     } else {
     uint32_t keepmask = 0;
