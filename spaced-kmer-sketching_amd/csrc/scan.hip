@@ -419,22 +419,22 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
       if (cnt) finish(cnt);
     } else {
     uint32_t keepmask = 0;
-    auto windows = [&](auto checked) {
+    if (__all(lane_clean)) {
 #pragma unroll
       for (int j = 0; j < kWPT; ++j) {
         const uint64_t f = fmh_narrow<FLAVOUR>(p, canon(j));
-        bool k = keep_fmh<MODE>(p, f, thresh);
-        if constexpr (decltype(checked)::value) {
-          const bool valid = ((inv64 >> j) & wmask_bits) == 0;
-          win_count += valid ? 1u : 0u;
-          k = k && valid;
-        }
-        keepmask |= (k ? 1u : 0u) << j;
+        keepmask |= (keep_fmh<MODE>(p, f, thresh) ? 1u : 0u) << j;
       }
-      if constexpr (!decltype(checked)::value) win_count += kWPT;
-    };
-    if (__all(lane_clean)) windows(std::false_type{});
-    else windows(std::true_type{});
+      win_count += kWPT;
+    } else {  // waves holding an invalid base: rare, kept out of the unrolled code
+#pragma unroll 1
+      for (int j = 0; j < kWPT; ++j) {
+        const uint64_t f = fmh_narrow<FLAVOUR>(p, canon(j));
+        const bool valid = ((inv64 >> j) & wmask_bits) == 0;
+        win_count += valid ? 1u : 0u;
+        keepmask |= (keep_fmh<MODE>(p, f, thresh) && valid ? 1u : 0u) << j;
+      }
+    }
     while (keepmask) {
       const uint32_t j = __builtin_ctz(keepmask);
       keepmask &= keepmask - 1;
