@@ -770,7 +770,7 @@ def main():
                        "sketch_size": sizes[0], "parallelism": f"genome-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "scan_kernel<frac, boost-mix>", "kernel_ms": scan_avg_ms,
+                         "kernel": "scan_kernel<frac, boost-mix, pre-filter>", "kernel_ms": scan_avg_ms,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "cpu_crosscheck": cpu_x,

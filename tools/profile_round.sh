@@ -12,8 +12,9 @@ OUT=$R/gpurun_out/round_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 # --inflight 1: every scan launch runs alone, so the trace average is the
-# kernel time bench.py reports for the roofline (its serial pass)
-ARGS="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --inflight 1"
+# kernel time bench.py reports for the roofline (its serial pass); the end-to-end
+# and one-genome-sharded sections (smaller launches of the same kernel) are off
+ARGS="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --inflight 1 --no-e2e --no-c3-sharded"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $ARGS > $OUT/bench_traced.json 2> $OUT/trace.log
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 $ARGS --no-pairs --no-sweep > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 $ARGS --no-pairs --no-sweep > $OUT/write.log 2>&1
