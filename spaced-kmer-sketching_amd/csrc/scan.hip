@@ -419,20 +419,31 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
       if (cnt) finish(cnt);
     } else {
     uint32_t keepmask = 0;
+    // bottom-s, flavour B: the candidate test only needs fmh's top 28 bits, which
+    // are the top bits of the last product y (H = y ^ (y >> 28) changes only
+    // bits < 36), so the xor-shift, the constant and the 64-bit compare go; a
+    // window whose top 28 bits equal the threshold's passes even if fmh > T (a
+    // superset of candidates: the post-processing selects exactly)
+    const uint32_t thr_top = (uint32_t)(thresh >> 36);
+    const uint32_t k_top = (uint32_t)(p.kconst >> 32);
+    auto keep_window = [&](uint64_t c) -> bool {
+      if constexpr (MODE == kModeBottom && FLAVOUR == 0) {
+        const uint64_t y = mul_const<kMixMul>(mix3_head(c));
+        return (((uint32_t)(y >> 32) ^ k_top) >> 4) <= thr_top;
+      } else {
+        return keep_fmh<MODE>(p, fmh_narrow<FLAVOUR>(p, c), thresh);
+      }
+    };
     if (__all(lane_clean)) {
 #pragma unroll
-      for (int j = 0; j < kWPT; ++j) {
-        const uint64_t f = fmh_narrow<FLAVOUR>(p, canon(j));
-        keepmask |= (keep_fmh<MODE>(p, f, thresh) ? 1u : 0u) << j;
-      }
+      for (int j = 0; j < kWPT; ++j) keepmask |= (keep_window(canon(j)) ? 1u : 0u) << j;
       win_count += kWPT;
     } else {  // waves holding an invalid base: rare, kept out of the unrolled code
 #pragma unroll 1
       for (int j = 0; j < kWPT; ++j) {
-        const uint64_t f = fmh_narrow<FLAVOUR>(p, canon(j));
         const bool valid = ((inv64 >> j) & wmask_bits) == 0;
         win_count += valid ? 1u : 0u;
-        keepmask |= (keep_fmh<MODE>(p, f, thresh) && valid ? 1u : 0u) << j;
+        keepmask |= (keep_window(canon(j)) && valid ? 1u : 0u) << j;
       }
     }
     while (keepmask) {
