@@ -646,11 +646,13 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
                        hipStream_t stream, int grid_override) {
   if (p.n_tiles == 0) return hipSuccess;
   auto pick = [&](auto kernel) -> hipError_t {
-    // Oversubscribe the resident slots 16x (config 3: 16384 workgroups of ~45
-    // tiles): the workgroup dispatcher then refills CUs as ranges finish, which
-    // evens out per-CU speed differences and keeps every SIMD at its wave limit
-    // (the occupancy query reports 4 workgroups per CU; LDS allows 6). Measured
-    // on config 3 (tools/scan_grid_sweep.py): 5.95 ms at 1x, 5.19 ms at 8x-16x.
+    // Oversubscribe the resident slots 16x (config 3, pre-filter kernel: 20480
+    // workgroups of ~36 tiles): the workgroup dispatcher then refills CUs as
+    // ranges finish, which evens out per-CU speed differences and keeps every
+    // SIMD at its wave limit. Measured on config 3 (tools/scan_grid_sweep.py):
+    // 5.95 ms at 1x, 5.19 ms at 8x-16x before the pre-filter; with it 4.7 ms at
+    // 8x and 16x (equal within noise in full benches), 5.6 ms at 32x and 9.2 at
+    // 64x (per-workgroup start-up and flush costs).
     int grid = grid_override > 0 ? grid_override : kGridOversubscribe * occupancy_grid(kernel, device);
     if ((uint64_t)grid > p.n_tiles) grid = (int)p.n_tiles;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, p);

@@ -19,7 +19,7 @@ def main():
     buf[n] = ord("\n")
     mask = sksffi.mask_generate(31, 21, 0)
     ref = None
-    for grid in [0, 1024, 1280, 1536, 1792, 2048, 3072, 4096, 8192, 16384]:
+    for grid in [0, 5120, 10240, 20480, 40960, 81920]:
         ctx.set_scan_grid(grid)
         for kind, param in ((sksffi.SKS_FRAC_MOD, 1000), (sksffi.SKS_BOTTOM_S, 10000)):
             ms = []
