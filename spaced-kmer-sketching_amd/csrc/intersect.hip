@@ -586,7 +586,11 @@ __device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cdata,
 
 __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
   // slot h = {key, mask of columns}: one ds_read_b128 per probe step
-  __shared__ ulonglong2 s_tab[kJSlots];
+  // slot h: key s_key[h], mask of the columns holding it s_msk[h]. Probes read
+  // the 8-byte key only (half the LDS banks of a 16-byte slot under random
+  // access) and fetch the mask on a hit.
+  __shared__ unsigned long long s_key[kJSlots];
+  __shared__ unsigned long long s_msk[kJSlots];
   __shared__ uint32_t s_cnt[kTile * kCntLd];
   __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
   __shared__ uint16_t s_next[kJWin];       // greedy chunk end of a chunk starting at bucket b
@@ -614,9 +618,11 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
   const uint32_t* roff = a.r.boff + (uint64_t)rblk * (a.B + 1);
   const uint32_t* coff = a.c.boff + (uint64_t)J * (a.B + 1);
   const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);  // slots < r_valid are rows
-  unsigned long long* tab = reinterpret_cast<unsigned long long*>(s_tab);  // [2h] key, [2h+1] mask
 
-  for (int i = tid; i < kJSlots; i += kB) s_tab[i] = make_ulonglong2(kEmpty, 0ull);
+  for (int i = tid; i < kJSlots; i += kB) {
+    s_key[i] = kEmpty;
+    s_msk[i] = 0ull;
+  }
   for (int i = tid; i < kTile * kCntLd; i += kB) s_cnt[i] = 0;
   if (tid == 0) s_special = 0;
 
@@ -684,7 +690,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
             atomicOr(&s_special, 1ull << cur.cid[u]);
           } else {
             hs[u] = join_hash(v);
-            prev[u] = atomicCAS(&tab[2 * hs[u]], (unsigned long long)kEmpty, (unsigned long long)v);
+            prev[u] = atomicCAS(&s_key[hs[u]], (unsigned long long)kEmpty, (unsigned long long)v);
           }
         }
       }
@@ -698,20 +704,20 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
           unsigned long long p = prev[u];
           while (p != kEmpty && p != v) {
             h = (h + 1) & (kJSlots - 1);
-            p = atomicCAS(&tab[2 * h], (unsigned long long)kEmpty, (unsigned long long)v);
+            p = atomicCAS(&s_key[h], (unsigned long long)kEmpty, (unsigned long long)v);
           }
           if (p == kEmpty) made[u] = h;
-          atomicOr(&tab[2 * h + 1], 1ull << cur.cid[u]);
+          atomicOr(&s_msk[h], 1ull << cur.cid[u]);
         }
       }
       __syncthreads();
       // 2) probe with the row elements: first slots read together
       const unsigned long long special = s_special;
-      ulonglong2 sl[kJRowPf];
+      unsigned long long sl[kJRowPf];
 #pragma unroll
       for (int u = 0; u < kJRowPf; ++u) {
-        sl[u] = make_ulonglong2(kEmpty, 0ull);
-        if (cur.rid[u] < r_valid && cur.rv[u] != kEmpty) sl[u] = s_tab[join_hash(cur.rv[u])];
+        sl[u] = kEmpty;
+        if (cur.rid[u] < r_valid && cur.rv[u] != kEmpty) sl[u] = s_key[join_hash(cur.rv[u])];
       }
 #pragma unroll
       for (int u = 0; u < kJRowPf; ++u) {
@@ -722,13 +728,13 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
         if (v == kEmpty) {
           m = special;
         } else {
-          ulonglong2 x = sl[u];
+          unsigned long long x = sl[u];
           uint32_t h = join_hash(v);
-          while (x.x != v && x.x != kEmpty) {
+          while (x != v && x != kEmpty) {
             h = (h + 1) & (kJSlots - 1);
-            x = s_tab[h];
+            x = s_key[h];
           }
-          m = x.x == v ? x.y : 0ull;
+          m = x == v ? s_msk[h] : 0ull;
         }
         if (m) add_hits(r, m);
       }
@@ -741,12 +747,12 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
           m = special;
         } else {
           uint32_t h = join_hash(v);
-          ulonglong2 x = s_tab[h];
-          while (x.x != v && x.x != kEmpty) {
+          unsigned long long x = s_key[h];
+          while (x != v && x != kEmpty) {
             h = (h + 1) & (kJSlots - 1);
-            x = s_tab[h];
+            x = s_key[h];
           }
-          m = x.x == v ? x.y : 0ull;
+          m = x == v ? s_msk[h] : 0ull;
         }
         if (m) add_hits(r, m);
       }
@@ -754,7 +760,10 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
       // 3) reset the slots this thread created (and the ~0 mask)
 #pragma unroll
       for (int u = 0; u < kJMade; ++u)
-        if (made[u] != kNoSlot) s_tab[made[u]] = make_ulonglong2(kEmpty, 0ull);
+        if (made[u] != kNoSlot) {
+          s_key[made[u]] = kEmpty;
+          s_msk[made[u]] = 0ull;
+        }
       if (tid == 0) s_special = 0;
       __syncthreads();
       cur = nxt;
