@@ -821,9 +821,10 @@ hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* sta
 
 namespace sks {
 
-uint32_t join_cap() {
-  static const uint32_t cap = std::min<uint32_t>(
-      kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP")) : kJCap);
+uint32_t join_cap() {  // SKS_JOIN_CAP (diagnostics) is clamped to [64, kJCap]
+  static const uint32_t cap = std::max<uint32_t>(
+      64, std::min<uint32_t>(kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP"))
+                                                           : kJCap));
   return cap;
 }
 
