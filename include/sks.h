@@ -60,6 +60,9 @@ typedef struct sks_policy {
 /* ---- library ---------------------------------------------------------------- */
 int sks_abi_version(void);
 const char* sks_last_error(void);
+/* "src:<16 hex digits>": hash of the sources this library was linked from
+ * (spaced-kmer-sketching_amd/srchash.py); no reference counterpart. */
+const char* sks_build_info(void);
 
 /* ---- host helpers (no device needed) ---------------------------------------------- */
 /* generate_random_spaced_seed_mask(w, k, seed) — kmer_bitset.cpp:132-152.

@@ -29,6 +29,9 @@ namespace {
 
 constexpr int kB = 256;
 constexpr int kWavesPerBlock = kB / 64;
+// workgroups per launch at most (HIP caps a grid at 2^32 - 1 work-items);
+// larger grids are cut into slices
+constexpr uint64_t kMaxGrid = 1ull << 22;
 
 struct U128 {
   uint64_t lo, hi;
@@ -96,9 +99,9 @@ __global__ __launch_bounds__(kB) void k_pairs(const uint64_t* __restrict__ data,
                                               const uint64_t* __restrict__ starts,
                                               const uint32_t* __restrict__ sizes,
                                               const int32_t* __restrict__ a,
-                                              const int32_t* __restrict__ b, uint64_t n_pairs,
-                                              int32_t* __restrict__ out) {
-  const uint64_t p = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+                                              const int32_t* __restrict__ b, uint64_t p0,
+                                              uint64_t n_pairs, int32_t* __restrict__ out) {
+  const uint64_t p = p0 + (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (p >= n_pairs) return;
   const int32_t ia = a[p], ib = b[p];
   int32_t c = wave_pair_count<EW>(data, starts[ia], sizes[ia], starts[ib], sizes[ib]);
@@ -109,9 +112,9 @@ template <int EW>
 __global__ __launch_bounds__(kB) void k_all(const uint64_t* __restrict__ data,
                                             const uint64_t* __restrict__ starts,
                                             const uint32_t* __restrict__ sizes, uint32_t n,
-                                            uint32_t row_begin, uint64_t n_pairs,
+                                            uint32_t row_begin, uint64_t p0, uint64_t n_pairs,
                                             int32_t* __restrict__ out) {
-  const uint64_t p = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const uint64_t p = p0 + (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (p >= n_pairs) return;
   const uint32_t i = row_begin + (uint32_t)(p / n), j = (uint32_t)(p % n);
   int32_t c = wave_pair_count<EW>(data, starts[i], sizes[i], starts[j], sizes[j]);
@@ -375,8 +378,8 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 // bucket, sketch by sketch, with the sketch's slot in the block in a u8 id
 // array.  A run of buckets of one block is one contiguous range, so a
 // workgroup streams the column block in coalesced chunks of whole buckets
-// that fit the table (<= kJCap elements) and the row block's same buckets
-// with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
+// that fit the table (<= kJCap elements; a larger bucket is cut into
+// sub-chunks) and the row block's same buckets with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
 #ifndef SKS_JOIN_LOG_SLOTS
 #define SKS_JOIN_LOG_SLOTS 11
 #endif
@@ -661,21 +664,34 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
       s_next[i] = (uint16_t)lo;
     }
     __syncthreads();
+    // A chunk is buckets [bs, be) with column elements [cs, ce).  A single
+    // bucket holding more than cap column elements (sketches far larger than the
+    // bucket count was sized for, or hash skew) is cut into sub-chunks of cap
+    // column elements, each joined against ALL of the bucket's row elements: a
+    // value's columns may then sit in two sub-chunks, and each contributes its
+    // own columns' hits, so the counts stay exact for any population.
     auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
     uint32_t bs = wb, be = chunk_end(wb);
+    uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
     JoinChunk cur;
-    join_fetch(cdata, cids, rdata, rids, s_coff[0], s_coff[be - wb], s_roff[0], s_roff[be - wb],
-               tid, cur);
+    join_fetch(cdata, cids, rdata, rids, cs, ce, s_roff[0], s_roff[be - wb], tid, cur);
     while (bs < we) {
-      const uint32_t cs = s_coff[bs - wb], ce = s_coff[be - wb];
       const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
       // prefetch the next chunk's elements while this one is joined
-      const uint32_t nbs = be;
-      const uint32_t nbe = nbs < we ? chunk_end(nbs) : nbs;
+      uint32_t nbs, nbe, ncs, nce;
+      if (ce < s_coff[be - wb]) {  // rest of an oversized bucket
+        nbs = bs;
+        nbe = be;
+        ncs = ce;
+      } else {
+        nbs = be;
+        nbe = nbs < we ? chunk_end(nbs) : nbs;
+        ncs = s_coff[nbs - wb];
+      }
+      nce = min(s_coff[nbe - wb], ncs + a.cap);
       JoinChunk nxt;
       if (nbs < we)
-        join_fetch(cdata, cids, rdata, rids, s_coff[nbs - wb], s_coff[nbe - wb], s_roff[nbs - wb],
-                   s_roff[nbe - wb], tid, nxt);
+        join_fetch(cdata, cids, rdata, rids, ncs, nce, s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
 
       // 1) insert the column elements: every first CAS in flight together,
       //    then the collisions walk on
@@ -769,6 +785,8 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
       cur = nxt;
       bs = nbs;
       be = nbe;
+      cs = ncs;
+      ce = nce;
     }
   }
   __syncthreads();
@@ -790,31 +808,39 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
                                   const uint32_t* sizes, int elem_words, const int32_t* a,
                                   const int32_t* b, uint64_t n_pairs, int32_t* out, hipStream_t s) {
-  if (n_pairs == 0) return hipSuccess;
-  uint64_t blocks = (n_pairs + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (elem_words == 1)
-    hipLaunchKernelGGL(k_pairs<1>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, a, b,
-                       n_pairs, out);
-  else
-    hipLaunchKernelGGL(k_pairs<2>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, a, b,
-                       n_pairs, out);
-  return hipGetLastError();
+  const uint64_t per = kMaxGrid * kWavesPerBlock;  // pairs per launch slice
+  for (uint64_t p0 = 0; p0 < n_pairs; p0 += per) {
+    const uint64_t blocks = (std::min(per, n_pairs - p0) + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (elem_words == 1)
+      hipLaunchKernelGGL(k_pairs<1>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, a,
+                         b, p0, n_pairs, out);
+    else
+      hipLaunchKernelGGL(k_pairs<2>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, a,
+                         b, p0, n_pairs, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* starts,
                                        const uint32_t* sizes, int elem_words, uint32_t n,
                                        uint32_t row_begin, uint32_t row_end, int32_t* out,
                                        hipStream_t s) {
-  uint64_t n_pairs = (uint64_t)(row_end - row_begin) * n;
-  if (n_pairs == 0) return hipSuccess;
-  uint64_t blocks = (n_pairs + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (elem_words == 1)
-    hipLaunchKernelGGL(k_all<1>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, n,
-                       row_begin, n_pairs, out);
-  else
-    hipLaunchKernelGGL(k_all<2>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, n,
-                       row_begin, n_pairs, out);
-  return hipGetLastError();
+  const uint64_t n_pairs = (uint64_t)(row_end - row_begin) * n;
+  const uint64_t per = kMaxGrid * kWavesPerBlock;
+  for (uint64_t p0 = 0; p0 < n_pairs; p0 += per) {
+    const uint64_t blocks = (std::min(per, n_pairs - p0) + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (elem_words == 1)
+      hipLaunchKernelGGL(k_all<1>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, n,
+                         row_begin, p0, n_pairs, out);
+    else
+      hipLaunchKernelGGL(k_all<2>, dim3((unsigned)blocks), dim3(kB), 0, s, data, starts, sizes, n,
+                         row_begin, p0, n_pairs, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace sks
@@ -936,15 +962,27 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   // each. Config 4 (136 tiles, B = 4096): 8704 workgroups, 1.17 ms; config 5
   // (10 tiles): 1030, 0.31 ms — against 1.32 / 0.36 ms with 2048 in all.
   // SKS_JOIN_WGS (diagnostics) sets the total instead.
+  // The ~64-buckets floor only applies while the grid is small (<= 64K
+  // workgroups); with very many tiles a tile gets fewer, larger groups (down to
+  // one), and the launch is cut into tile slices of at most kMaxGrid workgroups
+  // (HIP caps a grid at 2^32 - 1 work-items).
   static const uint64_t wgs_env = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 0;
   uint64_t want = wgs_env ? (wgs_env + tiles - 1) / tiles
-                          : std::max<uint64_t>((B + 63) / 64, (1024 + tiles - 1) / tiles);
+                          : std::max<uint64_t>(std::min<uint64_t>((B + 63) / 64, (65536 + tiles - 1) / tiles),
+                                               (1024 + tiles - 1) / tiles);
   if (!wgs_env) want = std::min<uint64_t>(want, std::max<uint32_t>(1, B / 16));
   const uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, want));
   ja.buckets_per_group = (B + groups - 1) / groups;
   ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
-  hipLaunchKernelGGL(k_join, dim3((unsigned)(tiles * ja.n_groups)), dim3(kB), 0, s, ja);
-  return hipGetLastError();
+  const uint64_t tiles_per_launch = std::max<uint64_t>(1, kMaxGrid / ja.n_groups);
+  for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
+    const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
+    ja.tile_begin = t0;
+    hipLaunchKernelGGL(k_join, dim3((unsigned)(nt * ja.n_groups)), dim3(kB), 0, s, ja);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // Tiled all-pairs for u64 sketches.  Host-synchronous (reads sizes and bucket
@@ -1003,10 +1041,16 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
         reinterpret_cast<const void*>(k_tiles), hipFuncAttributeMaxDynamicSharedMemorySize,
         (int)(kMaxPart * kSlots * sizeof(uint64_t) + kSlots * sizeof(uint32_t)));
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_tiles, dim3((unsigned)(tiles * a.n_groups)), dim3(kB), lds_bytes, s, a);
-    hipError_t le = hipGetLastError();
-    if (le == hipSuccess) *used_tiles = true;
-    return le;
+    const uint64_t per = std::max<uint64_t>(1, kMaxGrid / a.n_groups);  // tiles per slice
+    for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += per) {
+      a.tile_begin = t0;
+      hipLaunchKernelGGL(k_tiles, dim3((unsigned)(std::min(per, tile_end - t0) * a.n_groups)), dim3(kB),
+                         lds_bytes, s, a);
+      hipError_t le = hipGetLastError();
+      if (le != hipSuccess) return le;
+    }
+    *used_tiles = true;
+    return hipSuccess;
   };
   auto align16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
 
@@ -1065,7 +1109,10 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       if (dbg)
         fprintf(stderr, "[sks intersect] join n=%u B=%u max block bucket %u tiles=%llu\n", n, B,
                 h_stat, (unsigned long long)tiles);
-      if (h_stat <= join_cap()) {
+      // buckets above the table's capacity are joined in sub-chunks (exact, but
+      // the bucket's row elements are probed once per sub-chunk), so more
+      // buckets are tried first while the count matrix allows
+      if (h_stat <= join_cap() || log_b >= kJMaxLogB) {
         const uint32_t r_blk0 = sep_rows ? 0 : (sym ? 0 : row_begin / kTile);
         if ((e = join_launch(rl, r_blk0, cl, n, log_b, sym, row_begin, row_end, tile_begin, tile_end,
                              out, s)) != hipSuccess)
@@ -1073,8 +1120,6 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
         *used_tiles = true;
         return hipSuccess;
       }
-      // a block-bucket larger than the table: only hash-adversarial inputs
-      if (log_b >= kJMaxLogB) break;
       ++log_b;
     }
   }

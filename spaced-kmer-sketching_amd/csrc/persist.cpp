@@ -155,12 +155,18 @@ int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_
   if (h.window < 1 || h.window > 64 || h.elem_words != (h.window > 32 ? 2u : 1u))
     return fail(SKS_E_IO, where + "bad window / element width");
   if (h.n > (1ull << 32) || h.total > (1ull << 40)) return fail(SKS_E_IO, where + "bad counts");
+  // every region must fit in the file before any offset past it is formed: the
+  // counts are bounded above, so o_names cannot wrap; names_bytes is checked
+  // against the bytes left rather than added first
   const size_t o_sizes = sizeof(Header);
   const size_t o_win = o_sizes + pad8(h.n * 4);
   const size_t o_data = o_win + h.n * 8;
   const size_t o_names = o_data + h.total * h.elem_words * 8;
+  const size_t body = buf.size() - 8;  // bytes before the checksum
+  if (o_names > body || h.names_bytes > body - o_names)
+    return fail(SKS_E_IO, where + "length does not match the header");
   const size_t o_sum = o_names + h.names_bytes;
-  if (buf.size() != o_sum + 8) return fail(SKS_E_IO, where + "length does not match the header");
+  if (o_sum != body) return fail(SKS_E_IO, where + "length does not match the header");
   Fnv fnv;
   fnv.add(buf.data(), o_sum);
   uint64_t sum;

@@ -156,21 +156,27 @@ def _gather_flat(t, world):
 
 
 def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity, build, count,
-                    device="cpu", out=None):
+                    device="cpu", out=None, max_log_b=14):
     """Full n x n int32 intersection matrix on every rank.
 
     build(log_b) -> (data u64[tot], ids u8[tot], boff u32[nb*(B+1)], bstart u64[nb+1],
                      max_block_bucket) for this rank's block-aligned genomes (block_shard);
     count(n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out) fills `out`
     (zeroed first) with the counts of upper-triangle tiles [tile_begin, tile_end), both halves
-    — the contract of sks_intersect_sym_layout."""
+    — the contract of sks_intersect_sym_layout.
+
+    The bucket count is raised while the largest block-bucket (over all ranks)
+    exceeds the join table's `capacity`, up to 2^max_log_b buckets.  That is a
+    speed choice, not a correctness one: k_join cuts a bucket above capacity into
+    table-sized sub-chunks and probes the bucket's row elements once per
+    sub-chunk, so the counts at max_log_b are exact for any sketch size."""
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
     log_b = log_b_for(_max_over(local_max_size, world, device))
     nb_local = (g1 - g0 + TILE - 1) // TILE
     while True:
         data, ids, boff, bstart, mb = build(log_b)
         if world == 1:
-            if mb <= capacity or log_b >= 14:
+            if mb <= capacity or log_b >= max_log_b:
                 break
         else:
             # one all-reduce for the capacity check and the padded layout size
@@ -179,7 +185,7 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
             both = torch.cat([torch.tensor([int(mb)], dtype=torch.int64, device=device), tot])
             dist.all_reduce(both, op=dist.ReduceOp.MAX)
             mb_all, cap_e = (int(v) for v in both.cpu())
-            if mb_all <= capacity or log_b >= 14:
+            if mb_all <= capacity or log_b >= max_log_b:
                 break
         log_b += 1
     B1 = (1 << log_b) + 1

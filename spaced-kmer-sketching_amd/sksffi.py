@@ -43,7 +43,7 @@ class Timings(C.Structure):
 
 
 EXPORTED = [
-    "sks_abi_version", "sks_last_error", "sks_mask_generate", "sks_mask_contiguous",
+    "sks_abi_version", "sks_last_error", "sks_build_info", "sks_mask_generate", "sks_mask_contiguous",
     "sks_frac_min_hash", "sks_containment", "sks_binomial_estimator", "sks_ani_from_counts",
     "sks_fasta_open", "sks_fasta_close", "sks_fasta_num_records", "sks_fasta_record",
     "sks_fasta_stream", "sks_fasta_stream_bytes", "sks_fasta_runs", "sks_ctx_create",
@@ -74,6 +74,7 @@ def lib():
     u64p = C.POINTER(C.c_uint64)
     vp = C.c_void_p
     L.sks_last_error.restype = C.c_char_p
+    L.sks_build_info.restype = C.c_char_p
     L.sks_mask_generate.argtypes = [C.c_int, C.c_int, C.c_uint64, u64p]
     L.sks_mask_contiguous.argtypes = [C.c_int, u64p]
     L.sks_frac_min_hash.argtypes = [u64p, u64p, C.c_int, C.c_int64, C.c_int]
@@ -498,3 +499,8 @@ class SketchSet:
     def export(self, d_dst_ptr, stride, d_sizes_ptr):
         check(lib().sks_sketch_set_export(self.h, C.c_void_p(d_dst_ptr), stride,
                                           C.c_void_p(d_sizes_ptr)))
+
+
+def build_info():
+    """'src:<hash>' of the sources libsks.so was linked from (srchash.py)."""
+    return lib().sks_build_info().decode()

@@ -215,32 +215,41 @@ def _np_count_layout(n, log_b, data, ids, boff, bstart, t0, t1, out):
                     out[j, i] = c
 
 
-def _join_worker(rank, world, port, q):
+def _join_worker(rank, world, port, q, capacity, max_log_b):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sk = [s.astype(np.uint64) for s in _sketches()]
     _, g0, g1 = sks_dist.block_shard(N_GENOMES, world, rank)
     mine = sk[g0:g1]
+    built = []
+
+    def build(lb):
+        built.append(lb)
+        return _np_layout(mine, lb)
     mat = sks_dist.all_vs_all_join(
         N_GENOMES, world, rank, max((len(s) for s in mine), default=0),
-        lambda m: 3, capacity=10**9, build=lambda lb: _np_layout(mine, lb),
-        count=_np_count_layout)
-    q.put((rank, mat.numpy()))
+        lambda m: 1 if capacity < 100 else 3, capacity=capacity, build=build,
+        count=_np_count_layout, max_log_b=max_log_b)
+    q.put((rank, mat.numpy(), built))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_all_vs_all_join_layout_gather_gloo(world):
+# (capacity, max_log_b): a table that holds everything (no bucket search), and
+# a tiny one that walks log_b 1 -> max_log_b and then counts with block-buckets
+# still above capacity (the kernel's sub-chunk case; counts must stay exact)
+@pytest.mark.parametrize("world,capacity,max_log_b", [(2, 10**9, 14), (3, 10**9, 14), (2, 20, 4)])
+def test_all_vs_all_join_layout_gather_gloo(world, capacity, max_log_b):
     """Ranks build layouts of their own block-aligned genomes, all-gather them and
     count their tile share: every rank ends with the single-process matrix."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, capacity, max_log_b))
+             for r in range(world)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=240) for _ in range(world))
+    results = {r: (m, b) for r, m, b in (q.get(timeout=240) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -248,7 +257,13 @@ def test_all_vs_all_join_layout_gather_gloo(world):
     want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(N_GENOMES)]
                      for i in range(N_GENOMES)])
     for r in range(world):
-        assert np.array_equal(results[r], want)
+        assert np.array_equal(results[r][0], want)
+        # every rank walks the same log_b sequence (the check is all-reduced)
+        assert results[r][1] == results[0][1]
+    if capacity < 100:
+        assert results[0][1] == list(range(1, max_log_b + 1))
+    else:
+        assert results[0][1] == [3]
 
 
 def test_block_shard_covers_whole_blocks():

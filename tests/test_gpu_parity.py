@@ -580,3 +580,111 @@ def test_join_layout_build_and_concat(torch_cuda, ctx):
             torch.cuda.synchronize()
             acc += out.cpu().numpy().reshape(n, n)
         assert np.array_equal(acc, want)
+
+
+def _family_arrays(rng, n, base_n, fams, lo, hi, extra):
+    base = [np.unique(rng.integers(0, 2**63, size=base_n, dtype=np.uint64)) for _ in range(fams)]
+    sk = []
+    for i in range(n):
+        b = base[i % fams]
+        keep = b[rng.random(b.size) < lo + (hi - lo) * ((i * 7) % 10) / 10]
+        sk.append(np.unique(np.concatenate(
+            [keep, rng.integers(0, 2**64 - 1, size=extra, dtype=np.uint64)])))
+    return sk
+
+
+def _count_rows(sk, rows):
+    """|S_r ∩ S_j| for the given rows and every column (searchsorted merge)."""
+    out = np.zeros((len(rows), len(sk)), dtype=np.int64)
+    for a, r in enumerate(rows):
+        A = sk[r]
+        for j, Bv in enumerate(sk):
+            if A.size == 0 or Bv.size == 0:
+                continue
+            p = np.searchsorted(Bv, A)
+            p[p == Bv.size] = 0
+            out[a, j] = int(np.count_nonzero(Bv[p] == A))
+    return out
+
+
+def _layout(torch, ctx, d, st, sz, sk, log_b):
+    n = len(sk)
+    tot = int(sum(len(s) for s in sk))
+    nb = (n + 63) // 64
+    out = (torch.empty(max(tot, 1), dtype=torch.int64, device="cuda:0"),
+           torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda:0"),
+           torch.empty(nb * ((1 << log_b) + 1), dtype=torch.int32, device="cuda:0"),
+           torch.empty(nb + 1, dtype=torch.int64, device="cuda:0"))
+    mx = ctx.join_layout_build(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, log_b,
+                               *(t.data_ptr() for t in out))
+    return out, mx
+
+
+@pytest.mark.parametrize("log_b", [0, 1, 3])
+def test_join_buckets_above_table_capacity(torch_cuda, ctx, log_b):
+    """A layout with far fewer buckets than its sketches need: every block-bucket
+    holds many times the join table's capacity (up to 64 x 2.8k elements in one
+    bucket at log_b = 0), so k_join cuts each bucket into sub-chunks.  Counts
+    through sks_intersect_sym_layout equal numpy for every tile range split."""
+    torch = torch_cuda
+    rng = np.random.default_rng(23)
+    n = 150
+    sk = _family_arrays(rng, n, 2500, 3, 0.2, 0.9, 300)
+    sk[5] = np.zeros(0, np.uint64)
+    sk[40] = np.union1d(sk[40], np.array([0, 2**64 - 1], np.uint64))
+    sk[100] = np.union1d(sk[100], np.array([2**64 - 1], np.uint64))
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)]
+                     for i in range(n)])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    lay, mx = _layout(torch, ctx, d, st, sz, sk, log_b)
+    assert mx > 4 * sksffi.join_layout_capacity()
+    T = sksffi.intersect_sym_tiles(n)
+    acc = np.zeros((n, n), dtype=np.int64)
+    for (t0, t1) in [(0, 2), (2, T)]:
+        out = torch.full((n * n,), 7, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in lay), t0, t1, out.data_ptr())
+        torch.cuda.synchronize()
+        acc += out.cpu().numpy().reshape(n, n)
+    assert np.array_equal(acc, want)
+
+
+def test_join_large_sketches_300k(torch_cuda, ctx):
+    """128 sketches of 300k-390k elements (FracMinHash of 100-300 Mb genomes at
+    c = 1000 is this size): the bucket count saturates at 2^14 with the largest
+    block-bucket above the table.  Both entry points —
+    sks_intersect_sym / sks_intersect_all (host-sized layout) and
+    sks_join_layout_build + sks_intersect_sym_layout (the multi-GPU path) — give
+    exact counts: diagonal = sizes, symmetric, and rows 0, 1, 77, 127 equal a
+    numpy merge against all 128 columns."""
+    torch = torch_cuda
+    rng = np.random.default_rng(29)
+    n = 128
+    sk = _family_arrays(rng, n, 420_000, 4, 0.74, 0.92, 4000)
+    assert min(len(s) for s in sk) >= 300_000
+    rows = [0, 1, 77, 127]
+    want_rows = _count_rows(sk, rows)
+    sizes = np.array([len(s) for s in sk])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    log_b = sksffi.join_layout_log_b(int(sizes.max()))
+    assert log_b == 14
+    lay, mx = _layout(torch, ctx, d, st, sz, sk, log_b)
+    assert mx > sksffi.join_layout_capacity()  # the sub-chunk case
+    T = sksffi.intersect_sym_tiles(n)
+
+    def check(m):
+        assert np.array_equal(np.diag(m), sizes)
+        assert np.array_equal(m, m.T)
+        assert np.array_equal(m[rows], want_rows)
+
+    out = torch.full((n * n,), 3, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in lay), 0, T, out.data_ptr())
+    torch.cuda.synchronize()
+    check(out.cpu().numpy().reshape(n, n).astype(np.int64))
+    out.fill_(-1)
+    ctx.intersect_sym(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, T, out.data_ptr())
+    torch.cuda.synchronize()
+    check(out.cpu().numpy().reshape(n, n).astype(np.int64))
+    out.fill_(-1)
+    ctx.intersect_all(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, n, out.data_ptr())
+    torch.cuda.synchronize()
+    check(out.cpu().numpy().reshape(n, n).astype(np.int64))

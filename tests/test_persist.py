@@ -98,7 +98,19 @@ def test_host_load_rejects_damage(facade_bin, tmp_path):
         "not a sketch file": b"XX" + good[2:],
         "unsupported version": good[:8] + b"\x07" + good[9:],
     }
-    for msg, data in cases.items():
+    # a crafted header whose data region runs past the file while names_bytes
+    # wraps the end offset back onto the file length, checksum forged: must be
+    # rejected before any region is read (no over-read)
+    n, total = struct.unpack_from("<QQ", good, 64)
+    o_names = 96 + ((n * 4 + 7) & ~7) + 8 * n + 8 * total
+    big_total = total + 4096
+    o_names_big = o_names + 8 * 4096
+    nb_wrap = (len(good) - 8 - o_names_big) % (1 << 64)
+    forged = bytearray(good)
+    struct.pack_into("<QQ", forged, 72, big_total, nb_wrap)
+    struct.pack_into("<Q", forged, len(forged) - 8, fnv1a64(bytes(forged[:-8])))
+    cases["length"] = bytes(forged)
+    for msg, data in list(cases.items()) + [("length", good[:-9])]:
         bad = tmp_path / "bad.sks"
         bad.write_bytes(data)
         r = subprocess.run([facade_bin, "load", str(bad)], capture_output=True, text=True, timeout=60)
