@@ -418,7 +418,9 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n == 0)
-    return sks::fail(SKS_E_HIP, "sks_ctx_create: no HIP device available (the engine has no CPU path)");
+    return sks::fail(SKS_E_HIP, std::string("sks_ctx_create: no HIP device available (the engine has "
+                                            "no CPU path): hipGetDeviceCount -> ") +
+                                    hipGetErrorString(e) + ", " + std::to_string(n) + " devices");
   if (device < 0 || device >= n) return sks::fail(SKS_E_ARG, "sks_ctx_create: bad device index");
   DeviceGuard g(device);
   sks_ctx* c = new (std::nothrow) sks_ctx();

@@ -383,10 +383,20 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 #ifndef SKS_JOIN_LOG_SLOTS
 #define SKS_JOIN_LOG_SLOTS 11
 #endif
+#ifndef SKS_JOIN_DIAG  // diagnostics only (wrong counts): 1 no probes / hit adds,
+#define SKS_JOIN_DIAG 0  // 2 no count flush
+#endif
+// 512 threads (8 waves): with the table's LDS allowing 3 workgroups per CU,
+// 24 waves per CU instead of 12 hide the LDS round trips of the insert and
+// probe chains (config 4: k_join 0.86 -> 0.69 ms; 1024 threads 0.72)
+#ifndef SKS_JOIN_THREADS
+#define SKS_JOIN_THREADS 512
+#endif
+constexpr int kJB = SKS_JOIN_THREADS;       // threads per k_join workgroup
 constexpr int kJLog = SKS_JOIN_LOG_SLOTS;
 constexpr int kJSlots = 1 << kJLog;          // hash slots
 constexpr int kJCap = kJSlots / 2;          // column elements per chunk (load <= 1/2)
-constexpr int kJMade = kJCap / kB;          // column elements per thread per chunk (4)
+constexpr int kJMade = kJCap / kJB;         // column elements per thread per chunk
 constexpr int kJWin = 256;                  // bucket offsets staged per window
 constexpr uint32_t kJMaxLogB = 14;          // B <= 16384 (LDS histogram of k_hb_count)
 constexpr int kCntLd = kTile + 1;
@@ -559,7 +569,10 @@ struct JoinArgs {
 // Elements of one chunk held in registers: column elements k = cs + tid + 256u
 // (u < kJMade: a chunk holds <= kJCap) and the first kJRowPf * 256 row elements;
 // the rest of a (rare) larger row range is read in the probe loop.
-constexpr int kJRowPf = 6;
+constexpr int kJRowPf = 1536 / kJB;
+// s_waitcnt immediate for gfx9 "vmcnt(0)" with expcnt / lgkmcnt left at their
+// maxima: vmcnt = imm[3:0] | imm[15:14] << 4, expcnt = imm[6:4], lgkmcnt = imm[11:8]
+constexpr int kWaitVmcnt0 = 0x0F70;
 struct JoinChunk {
   uint64_t cv[kJMade];
   uint32_t cid[kJMade];
@@ -575,19 +588,35 @@ __device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cdata,
                                            JoinChunk& c) {
 #pragma unroll
   for (int u = 0; u < kJMade; ++u) {
-    const uint32_t k = cs + tid + kB * u;
+    const uint32_t k = cs + tid + kJB * u;
     c.cv[u] = k < ce ? cdata[k] : 0;
     c.cid[u] = k < ce ? cids[k] : 0xFFu;
   }
 #pragma unroll
   for (int u = 0; u < kJRowPf; ++u) {
-    const uint32_t k = rs + tid + kB * u;
+    const uint32_t k = rs + tid + kJB * u;
     c.rv[u] = k < re ? rdata[k] : 0;
     c.rid[u] = k < re ? rids[k] : 0xFFu;
   }
 }
 
-__global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
+#ifdef SKS_JOIN_STAMPS  // diagnostic build: cycles per k_join phase, wave 0 of each workgroup
+__device__ unsigned long long g_join_stamps[8];
+#define JSTAMP(i)                                              \
+  do {                                                         \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+    st_acc[i] += t_ - st_last;                                 \
+    st_last = t_;                                              \
+  } while (0)
+#else
+#define JSTAMP(i) do {} while (0)
+#endif
+
+__global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
+#ifdef SKS_JOIN_STAMPS
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
   // slot h = {key, mask of columns}: one ds_read_b128 per probe step
   // slot h: key s_key[h], mask of the columns holding it s_msk[h]. Probes read
   // the 8-byte key only (half the LDS banks of a 16-byte slot under random
@@ -622,11 +651,11 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
   const uint32_t* coff = a.c.boff + (uint64_t)J * (a.B + 1);
   const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);  // slots < r_valid are rows
 
-  for (int i = tid; i < kJSlots; i += kB) {
+  for (int i = tid; i < kJSlots; i += kJB) {
     s_key[i] = kEmpty;
     s_msk[i] = 0ull;
   }
-  for (int i = tid; i < kTile * kCntLd; i += kB) s_cnt[i] = 0;
+  for (int i = tid; i < kTile * kCntLd; i += kJB) s_cnt[i] = 0;
   if (tid == 0) s_special = 0;
 
   // a row element's bit loop starts at column `lane`: lanes holding the same
@@ -646,7 +675,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
   for (uint32_t wb = b0; wb < b1; wb += kJWin) {
     const uint32_t we = min(b1, wb + kJWin);
     __syncthreads();  // previous window fully consumed
-    for (uint32_t i = tid; i <= we - wb; i += kB) {
+    for (uint32_t i = tid; i <= we - wb; i += kJB) {
       s_roff[i] = roff[wb + i];
       s_coff[i] = coff[wb + i];
     }
@@ -654,7 +683,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     // chunk = whole buckets [bs, be) whose column elements fit the table: the
     // largest be with coff[be] - coff[bs] <= cap (at least bs + 1), found
     // for every start bucket at once by binary search
-    for (uint32_t i = tid; i < we - wb; i += kB) {
+    for (uint32_t i = tid; i < we - wb; i += kJB) {
       const uint32_t cs = s_coff[i];
       uint32_t lo = i + 1, hi = we - wb;  // answer in [lo, hi]
       while (lo < hi) {
@@ -670,6 +699,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     // column elements, each joined against ALL of the bucket's row elements: a
     // value's columns may then sit in two sub-chunks, and each contributes its
     // own columns' hits, so the counts stay exact for any population.
+    JSTAMP(0);
     auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
     uint32_t bs = wb, be = chunk_end(wb);
     uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
@@ -677,6 +707,13 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     join_fetch(cdata, cids, rdata, rids, cs, ce, s_roff[0], s_roff[be - wb], tid, cur);
     while (bs < we) {
       const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
+      // This chunk's elements (prefetched during the previous chunk) have
+      // landed: say so before the next prefetch is issued.  Without it the
+      // compiler's wait for `cur` (merged with the first chunk's loads at the
+      // loop head) was a vmcnt(1) placed after the new prefetch, i.e. every
+      // chunk waited for the NEXT chunk's loads before its first insert
+      // (config 4: 53k of 117k cycles per workgroup in the insert phase).
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
       // prefetch the next chunk's elements while this one is joined
       uint32_t nbs, nbe, ncs, nce;
       if (ce < s_coff[be - wb]) {  // rest of an oversized bucket
@@ -700,7 +737,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
 #pragma unroll
       for (int u = 0; u < kJMade; ++u) {
         hs[u] = kNoSlot;
-        if (cs + tid + kB * u < ce) {
+        if (cs + tid + kJB * u < ce) {
           const uint64_t v = cur.cv[u];
           if (v == kEmpty) {
             atomicOr(&s_special, 1ull << cur.cid[u]);
@@ -727,6 +764,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
         }
       }
       __syncthreads();
+      JSTAMP(1);
       // 2) probe with the row elements: first slots read together
       const unsigned long long special = s_special;
       unsigned long long sl[kJRowPf];
@@ -752,9 +790,10 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
           }
           m = x == v ? s_msk[h] : 0ull;
         }
+        if (SKS_JOIN_DIAG & 1) continue;
         if (m) add_hits(r, m);
       }
-      for (uint32_t k = rs + tid + kB * kJRowPf; k < re; k += kB) {
+      for (uint32_t k = rs + tid + kJB * kJRowPf; k < re; k += kJB) {
         const uint32_t r = rids[k];
         if (r >= r_valid) continue;
         const uint64_t v = rdata[k];
@@ -773,6 +812,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
         if (m) add_hits(r, m);
       }
       __syncthreads();
+      JSTAMP(2);
       // 3) reset the slots this thread created (and the ~0 mask)
 #pragma unroll
       for (int u = 0; u < kJMade; ++u)
@@ -782,6 +822,7 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
         }
       if (tid == 0) s_special = 0;
       __syncthreads();
+      JSTAMP(3);
       cur = nxt;
       bs = nbs;
       be = nbe;
@@ -790,8 +831,10 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     }
   }
   __syncthreads();
+  JSTAMP(5);
+  if (SKS_JOIN_DIAG & 2) return;
   // counts -> global (one atomic per nonzero pair; both halves for sym off-diagonal)
-  for (int i = tid; i < kTile * kTile; i += kB) {
+  for (int i = tid; i < kTile * kTile; i += kJB) {
     const uint32_t r = i >> 6, c = i & 63;
     const uint32_t cnt = s_cnt[r * kCntLd + c];
     if (!cnt) continue;
@@ -801,6 +844,11 @@ __global__ __launch_bounds__(kB) void k_join(JoinArgs a) {
     atomicAdd(&a.out[orow * a.ld + gc], (int32_t)cnt);
     if (a.sym && I != J) atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
   }
+#ifdef SKS_JOIN_STAMPS
+  JSTAMP(4);
+  if (tid == 0)
+    for (int i = 0; i < 6; ++i) atomicAdd(&g_join_stamps[i], (unsigned long long)st_acc[i]);
+#endif
 }
 
 }  // namespace
@@ -978,10 +1026,23 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
     const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
     ja.tile_begin = t0;
-    hipLaunchKernelGGL(k_join, dim3((unsigned)(nt * ja.n_groups)), dim3(kB), 0, s, ja);
+    hipLaunchKernelGGL(k_join, dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+#ifdef SKS_JOIN_STAMPS
+  {
+    unsigned long long h[8] = {0};
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_join_stamps), sizeof h);
+    const unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_join_stamps), z, sizeof z);
+    const double wgs = (double)(tile_end - tile_begin) * ja.n_groups;
+    fprintf(stderr, "[k_join stamps] cycles per workgroup: setup %.0f insert %.0f probe %.0f reset %.0f "
+            "flush %.0f tail-barrier %.0f (%.0f workgroups)\n", h[0] / wgs, h[1] / wgs, h[2] / wgs,
+            h[3] / wgs, h[4] / wgs, h[5] / wgs, wgs);
+  }
+#endif
   return hipSuccess;
 }
 

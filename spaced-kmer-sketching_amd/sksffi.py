@@ -70,6 +70,15 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libsks.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    # PyTorch-ROCm ships its own libamdhip64 with the same SONAME as /opt/rocm's
+    # (libamdhip64.so.7): whichever loads first serves both.  Load torch first
+    # when it is installed, so a process that also uses torch device memory and
+    # streams runs ONE HIP runtime — the order every GPU test and bench.py use.
+    # (libsks loaded first, then torch, left sks_ctx_create without devices.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     u64p = C.POINTER(C.c_uint64)
     vp = C.c_void_p

@@ -8,7 +8,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
 mkdir -p "$T/pkg"
 cp -r "$R/include" "$T/"
-cp -r "$R/spaced-kmer-sketching_amd/csrc" "$R/spaced-kmer-sketching_amd/cpp" "$R/spaced-kmer-sketching_amd/Makefile" "$T/pkg/"
+cp -r "$R/spaced-kmer-sketching_amd/csrc" "$R/spaced-kmer-sketching_amd/cpp" "$R/spaced-kmer-sketching_amd/Makefile" "$R/spaced-kmer-sketching_amd/srchash.py" "$T/pkg/"
 make -s -C "$T/pkg" -j8 CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wno-unused-result $*" lib/libsks.so
 mkdir -p "$R/variants"
 cp "$T/pkg/lib/libsks.so" "$R/variants/libsks_$TAG.so"
