@@ -240,6 +240,11 @@ int sks_intersect_sym(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_st
  * d_out holds n values; *n_out (host) = distinct values.  Narrow (w <= 32) only. */
 int sks_sketch_union(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64_t* d_out,
                      uint64_t* n_out);
+/* The same for 32 < w <= 64: n 128-bit k-mers as (lo, hi) word pairs (2n words),
+ * ordered by the 128-bit value like the reference's operator< on kmer_bitset.
+ * d_in / d_out 16-byte aligned (SKS_E_ARG otherwise). */
+int sks_sketch_union_wide(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64_t* d_out,
+                          uint64_t* n_out);
 
 /* ---- join layout: all-vs-all across GPUs ------------------------------------------------
  * The all-pairs join kernel (sks_intersect_all / _sym, SKS_INTERSECT_JOIN) reads

@@ -9,6 +9,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <exception>
 #include <iostream>
 #include <mutex>
 #include <string>
@@ -195,8 +196,66 @@ namespace {
 
 // Pair counts on the GPU for sets sharing a mask; pairs with different masks
 // have no common k-mer (identity includes the mask, kmer.hpp:82-85).
+std::vector<int> pair_counts_single_mask(const std::vector<const kmer_set*>& a,
+                                         const std::vector<const kmer_set*>& b);
+
+// Sets holding k-mers under several masks: identity is (masked_bits, mask)
+// (kmer.hpp:82-85), so |A ∩ B| = Σ over masks m held by both of |A_m ∩ B_m|.
+// Each (set, mask) part becomes one sketch; the parts sharing a mask are counted
+// on the GPU (sks_intersect_pairs) and summed per pair.
+std::vector<int> pair_counts_mixed(const std::vector<const kmer_set*>& a,
+                                   const std::vector<const kmer_set*>& b) {
+  std::vector<kmer_set> parts;  // single-mask views of every (set, mask) part
+  std::vector<const kmer_set*> pa, pb;
+  std::vector<size_t> owner;
+  std::unordered_map<const void*, size_t> part_of;  // &elements -> index in parts
+  auto part = [&](const kmer_set* s, size_t g) {
+    const std::vector<kmer_bitset>* e = g == 0 ? &s->elements : &s->other_masks[g - 1].elements;
+    auto it = part_of.find(e);
+    if (it != part_of.end()) return it->second;
+    kmer_set p;
+    p.has_mask = true;
+    p.mask = g == 0 ? s->mask : s->other_masks[g - 1].mask;
+    p.window_length = g == 0 ? s->window_length : s->other_masks[g - 1].window_length;
+    p.elements = *e;
+    parts.push_back(std::move(p));
+    part_of.emplace(e, parts.size() - 1);
+    return parts.size() - 1;
+  };
+  std::vector<std::pair<size_t, size_t>> sub;
+  for (size_t i = 0; i < a.size(); ++i) {
+    for (size_t ga = 0; ga <= a[i]->other_masks.size(); ++ga) {
+      const kmer_bitset& m = ga == 0 ? a[i]->mask : a[i]->other_masks[ga - 1].mask;
+      if (ga == 0 && !a[i]->has_mask) continue;
+      for (size_t gb = 0; gb <= b[i]->other_masks.size(); ++gb) {
+        if (gb == 0 && !b[i]->has_mask) continue;
+        const kmer_bitset& mb = gb == 0 ? b[i]->mask : b[i]->other_masks[gb - 1].mask;
+        if (!(m == mb)) continue;
+        sub.emplace_back(part(a[i], ga), part(b[i], gb));
+        owner.push_back(i);
+      }
+    }
+  }
+  std::vector<int> out(a.size(), 0);
+  if (sub.empty()) return out;
+  for (auto& [x, y] : sub) {  // parts is final now
+    pa.push_back(&parts[x]);
+    pb.push_back(&parts[y]);
+  }
+  const std::vector<int> c = pair_counts_single_mask(pa, pb);
+  for (size_t k = 0; k < sub.size(); ++k) out[owner[k]] += c[k];
+  return out;
+}
+
 std::vector<int> pair_counts(const std::vector<const kmer_set*>& a,
                              const std::vector<const kmer_set*>& b) {
+  for (size_t i = 0; i < a.size(); ++i)
+    if (!a[i]->other_masks.empty() || !b[i]->other_masks.empty()) return pair_counts_mixed(a, b);
+  return pair_counts_single_mask(a, b);
+}
+
+std::vector<int> pair_counts_single_mask(const std::vector<const kmer_set*>& a,
+                                         const std::vector<const kmer_set*>& b) {
   std::unordered_map<const kmer_set*, int32_t> index;
   std::vector<const kmer_set*> uniq;
   auto id = [&](const kmer_set* s) {
@@ -335,31 +394,104 @@ size_t frac_min_hash::operator()(const kmer& k) const {
 }
 
 // ---- kmer_set -------------------------------------------------------------------------------------
+namespace {
+// insert sorted masked bits into a sorted unique array
+void merge_into(std::vector<kmer_bitset>& dst, std::vector<kmer_bitset>& add) {
+  std::sort(add.begin(), add.end());
+  std::vector<kmer_bitset> merged;
+  merged.reserve(dst.size() + add.size());
+  std::merge(dst.begin(), dst.end(), add.begin(), add.end(), std::back_inserter(merged));
+  merged.erase(std::unique(merged.begin(), merged.end()), merged.end());
+  dst.swap(merged);
+}
+}  // namespace
+
 void kmer_set::insert_kmers(const std::vector<kmer>& kmers) {
   if (kmers.empty()) return;
   std::vector<kmer_bitset> add;
+  std::vector<std::vector<kmer_bitset>> add_other(other_masks.size());
   add.reserve(kmers.size());
   for (const kmer& k : kmers) {
     if (!has_mask) {
       mask = k.mask;
       window_length = k.window_length;
       has_mask = true;
-    } else if (!(k.mask == mask)) {
-      throw std::runtime_error("kmer_set: k-mers with different masks cannot share a GPU sketch");
     }
-    add.push_back(k.masked_bits);
+    if (k.mask == mask) {
+      add.push_back(k.masked_bits);
+      continue;
+    }
+    size_t g = 0;
+    while (g < other_masks.size() && !(other_masks[g].mask == k.mask)) ++g;
+    if (g == other_masks.size()) {
+      other_masks.push_back(mask_group{k.window_length, k.mask, {}});
+      add_other.emplace_back();
+    }
+    add_other[g].push_back(k.masked_bits);
   }
-  std::sort(add.begin(), add.end());
-  std::vector<kmer_bitset> merged;
-  merged.reserve(elements.size() + add.size());
-  std::merge(elements.begin(), elements.end(), add.begin(), add.end(), std::back_inserter(merged));
-  merged.erase(std::unique(merged.begin(), merged.end()), merged.end());
-  elements.swap(merged);
+  merge_into(elements, add);
+  for (size_t g = 0; g < other_masks.size(); ++g)
+    if (!add_other[g].empty()) merge_into(other_masks[g].elements, add_other[g]);
+}
+
+int kmer_set::kmer_set_size() const {
+  size_t n = elements.size();
+  for (const auto& g : other_masks) n += g.elements.size();
+  return (int)n;
+}
+
+const std::vector<kmer_bitset>* kmer_set::elements_for(const kmer_bitset& m) const {
+  if (has_mask && m == mask) return &elements;
+  for (const auto& g : other_masks)
+    if (g.mask == m) return &g.elements;
+  return nullptr;
 }
 
 bool kmer_set::contains(const kmer& k) const {
-  if (!has_mask || !(k.mask == mask)) return false;
-  return std::binary_search(elements.begin(), elements.end(), k.masked_bits);
+  const std::vector<kmer_bitset>* e = elements_for(k.mask);
+  return e && std::binary_search(e->begin(), e->end(), k.masked_bits);
+}
+
+// ---- kmer_hashes view --------------------------------------------------------------------------------
+namespace {
+size_t n_groups(const kmer_set* s) { return 1 + s->other_masks.size(); }
+const std::vector<kmer_bitset>& group_elems(const kmer_set* s, size_t g) {
+  return g == 0 ? s->elements : s->other_masks[g - 1].elements;
+}
+kmer group_kmer(const kmer_set* s, size_t g, size_t e) {
+  const kmer_bitset& b = group_elems(s, g)[e];
+  if (g == 0) return kmer{s->window_length, b, s->mask, b};
+  const auto& grp = s->other_masks[g - 1];
+  return kmer{grp.window_length, b, grp.mask, b};
+}
+}  // namespace
+
+void kmer_hash_view::const_iterator::settle() {
+  while (g_ < n_groups(s_) && e_ >= group_elems(s_, g_).size()) {
+    ++g_;
+    e_ = 0;
+  }
+  if (g_ < n_groups(s_)) cur_.emplace(group_kmer(s_, g_, e_), 1);
+  else cur_.reset();
+}
+
+std::size_t kmer_hash_view::size() const { return (std::size_t)s_->kmer_set_size(); }
+std::size_t kmer_hash_view::count(const kmer& k) const { return s_->contains(k) ? 1 : 0; }
+int kmer_hash_view::at(const kmer& k) const {
+  if (!s_->contains(k)) throw std::out_of_range("kmer_set::kmer_hashes::at: k-mer not in the set");
+  return 1;
+}
+kmer_hash_view::const_iterator kmer_hash_view::begin() const { return const_iterator(s_, 0, 0); }
+kmer_hash_view::const_iterator kmer_hash_view::end() const { return const_iterator(s_, n_groups(s_), 0); }
+kmer_hash_view::const_iterator kmer_hash_view::find(const kmer& k) const {
+  for (size_t g = 0; g < n_groups(s_); ++g) {
+    const bool same = g == 0 ? (s_->has_mask && s_->mask == k.mask) : s_->other_masks[g - 1].mask == k.mask;
+    if (!same) continue;
+    const auto& e = group_elems(s_, g);
+    auto it = std::lower_bound(e.begin(), e.end(), k.masked_bits);
+    if (it != e.end() && *it == k.masked_bits) return const_iterator(s_, g, (size_t)(it - e.begin()));
+  }
+  return end();
 }
 
 int kmer_set_intersection(const kmer_set& ks1, const kmer_set& ks2) {
@@ -440,6 +572,137 @@ void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& kmer_list,
 std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
                                                   const kmer_bitset& mask, const int window_length,
                                                   const sketch_policy& sketching_cond) {
+  std::vector<kmer> out;
+  nucleotide_string_list_to_kmers_by_reference(out, nucleotide_strings, mask, window_length,
+                                               sketching_cond);
+  return out;
+}
+
+// ---- the std::function plug-in point (kmer.hpp:93-103, :195-212) ----------------------------------------
+namespace sks {
+namespace {
+
+std::mutex g_gpu_mu;  // the facade's context serves one build at a time
+
+// Every window of a record stream, in order (kmer_sliding.cpp:144-185 over
+// each run), as the reference's kmer objects, handed to `fn`.  The windows
+// come from the GPU list build at c = 1 (every valid window, canonical masked
+// bits and the unmasked kmer_bits); the stream is cut into pieces of kPiece
+// bytes plus a (w - 1)-byte halo, keeping the windows that start inside each
+// piece's own range, so host buffers stay bounded for any genome size.
+void for_each_window(const std::vector<uint8_t>& stream, const kmer_bitset& mask, int w,
+                     const std::function<void(const kmer&)>& fn) {
+  constexpr uint64_t kPiece = 2u << 20;
+  const uint64_t n = stream.size();
+  const sks_policy every{SKS_FRAC_MOD, hash_flavour(), 1, 1};
+  const uint64_t m[2] = {mask.lo(), mask.hi()};
+  std::vector<uint64_t> pos, bits;
+  for (uint64_t a = 0; a < n; a += kPiece) {
+    const uint64_t own = std::min(kPiece, n - a);
+    const uint64_t len = std::min(n - a, own + (uint64_t)(w > 0 ? w - 1 : 0));
+    uint64_t cnt = 0;
+    {
+      std::lock_guard<std::mutex> lock(g_gpu_mu);
+      DevMem d(len);
+      check_hip(hipMemcpy(d.p, stream.data() + a, len, hipMemcpyHostToDevice), "hipMemcpy H2D");
+      const uint64_t seg[2] = {0, len};
+      sks_kmer_list* kl = nullptr;
+      check(sks_kmer_list_build(ctx(), d.as<uint8_t>(), len, seg, 1, w, m, &every, &kl));
+      cnt = sks_kmer_list_total(kl);
+      pos.resize(cnt);
+      bits.resize(4 * cnt);
+      const int rc = sks_kmer_list_copy(kl, pos.data(), bits.data());
+      sks_kmer_list_free(kl);
+      check(rc);
+    }
+    for (uint64_t i = 0; i < cnt && pos[i] < own; ++i)
+      fn(kmer{w, kmer_bitset(bits[4 * i], bits[4 * i + 1]), mask,
+              kmer_bitset(bits[4 * i + 2], bits[4 * i + 3])});
+  }
+}
+
+std::vector<uint8_t> file_stream(const char* path) {
+  FastaHandle f(path);  // strings_from_fasta's quirks; unreadable -> exit(1) like the reference
+  const uint8_t* p = sks_fasta_stream(f.f);
+  return std::vector<uint8_t>(p, p + sks_fasta_stream_bytes(f.f));
+}
+
+kmer_set set_from_stream(const std::vector<uint8_t>& stream, const kmer_bitset& mask, int w,
+                         const sketching_condition_t& cond) {
+  std::vector<kmer> kept;
+  for_each_window(stream, mask, w, [&](const kmer& k) {
+    if (cond(k)) kept.push_back(k);
+  });
+  kmer_set ks;  // kmer_set_from_fasta_file: insert_kmers of the selected list (kmer_set.cpp:54-68)
+  ks.insert_kmers(kept);
+  if (!ks.has_mask) {
+    ks.mask = mask;
+    ks.window_length = w;
+    ks.has_mask = true;
+  }
+  return ks;
+}
+
+}  // namespace
+}  // namespace sks
+
+kmer_set kmer_set_from_fasta_file(const char fasta_filename[], const kmer_bitset& mask,
+                                  const int window_length, const sketching_condition_t& sketching_cond) {
+  return sks::set_from_stream(sks::file_stream(fasta_filename), mask, window_length, sketching_cond);
+}
+
+std::vector<kmer_set> kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
+                                                 const kmer_bitset& mask, const int window_length,
+                                                 const sketching_condition_t& sketching_cond) {
+  std::vector<kmer_set> out;
+  for (int i = 0; i < num_files; ++i)
+    out.push_back(kmer_set_from_fasta_file(fasta_filenames[i], mask, window_length, sketching_cond));
+  return out;
+}
+
+std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
+                                                          const kmer_bitset& mask, const int window_length,
+                                                          const sketching_condition_t& sketching_cond) {
+  const int n = num_files > 0 ? num_files : 0;
+  // open serially first so that the reference's exit(1) / error order holds
+  for (int i = 0; i < n; ++i) {
+    FILE* fp = fopen(fasta_filenames[i], "rb");
+    if (!fp) sks::report_unreadable(fasta_filenames[i]);
+    else fclose(fp);
+  }
+  std::vector<kmer_set> out(n);
+  std::vector<std::exception_ptr> err(n);
+  std::vector<std::thread> ts;
+  std::atomic<int> next{0};
+  const int workers = std::max(1, std::min<int>(n, (int)std::thread::hardware_concurrency()));
+  for (int t = 0; t < workers; ++t)
+    ts.emplace_back([&]() {
+      for (int i; (i = next.fetch_add(1)) < n;) {
+        try {
+          out[i] = kmer_set_from_fasta_file(fasta_filenames[i], mask, window_length, sketching_cond);
+        } catch (...) {
+          err[i] = std::current_exception();
+        }
+      }
+    });
+  for (auto& t : ts) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+  return out;
+}
+
+void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& kmer_list,
+                                                  const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketching_condition_t& sketching_cond) {
+  sks::for_each_window(runs_stream(nucleotide_strings), mask, window_length, [&](const kmer& k) {
+    if (sketching_cond(k)) kmer_list.push_back(k);
+  });
+}
+
+std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketching_condition_t& sketching_cond) {
   std::vector<kmer> out;
   nucleotide_string_list_to_kmers_by_reference(out, nucleotide_strings, mask, window_length,
                                                sketching_cond);

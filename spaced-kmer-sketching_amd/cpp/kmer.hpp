@@ -1,19 +1,23 @@
 // kmer.hpp — drop-in replacement for the reference's src/kmer.hpp
 // (bensonlzl/spaced-kmer-sketching) on top of libsks.so (include/sks.h).
 //
-// Same names, argument meanings and error behaviour as the reference, with one
-// deliberate change at the plug-in point: the reference passes the sketch
-// predicate as std::function<bool(const kmer)> (kmer.hpp:93-103, :195-212),
-// a host callback that cannot run inside a GPU kernel.  Here the predicate is a
-// `sketch_policy` descriptor; `frac_mod_condition{frac_min_hash(1), 200}` is
-// the reference's `sketching_condition` (kmer-sketching.cpp:29-34) and
-// converts to it implicitly.  There is no CPU fallback: sketching and
-// intersection always run on the GPU and fail loudly without one.
+// Same names, argument meanings and error behaviour as the reference.  The
+// plug-in point keeps the reference's signature: every builder takes
+// std::function<bool(const kmer)> sketching_cond (kmer.hpp:93-103, :195-212),
+// called once per window in window order like kmer_sliding.cpp:183.  The GPU
+// extracts every window (canonical masked k-mer, kmer_bits) and the host
+// predicate filters them.  For the FracMinHash predicate the selection itself
+// runs on the GPU: pass `frac_mod_condition{frac_min_hash(1), 200}` (the
+// reference's `sketching_condition`, kmer-sketching.cpp:29-34) or a
+// `sketch_policy` (FracMinHash or bottom-s descriptor) instead of a callback.
+// There is no CPU fallback: without a GPU every builder throws.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <iterator>
+#include <optional>
 #include <ostream>
 #include <stdexcept>
 #include <string>
@@ -183,24 +187,137 @@ struct frac_mod_condition {
 };
 
 // ---- kmer_set (kmer.hpp:152-190) ---------------------------------------------------------------
-// Sorted unique masked canonical k-mers sharing one mask (the reference's
-// hash map keyed by (masked_bits, mask)).
+// The reference keys its set by (masked_bits, mask) in an unordered_map
+// (kmer.hpp:152, :170-178).  Here a set is one sorted array of masked bits per
+// mask: `elements` under `mask` (every set the builders make has one mask),
+// plus `other_masks` when k-mers with further masks were inserted.
+struct kmer_set;
+
+// Read-only view with the reference's kmer_set::kmer_hashes interface (an
+// unordered_map<kmer, int, kmer_hash> whose values are all 1): size(), empty(),
+// count(), contains(), at(), find(), and iteration over std::pair<const kmer, int>.
+// The kmer a view yields has kmer_bits = masked_bits (the reference keeps the
+// unmasked window of the first insertion there, which no result depends on).
+class kmer_hash_view {
+ public:
+  using key_type = kmer;
+  using mapped_type = int;
+  using value_type = std::pair<const kmer, int>;
+  using size_type = std::size_t;
+
+  class const_iterator {
+   public:
+    using iterator_category = std::forward_iterator_tag;
+    using value_type = kmer_hash_view::value_type;
+    using difference_type = std::ptrdiff_t;
+    using pointer = const value_type*;
+    using reference = const value_type&;
+    const_iterator() = default;
+    reference operator*() const { return *cur_; }
+    pointer operator->() const { return &*cur_; }
+    const_iterator& operator++() { ++e_; settle(); return *this; }
+    const_iterator operator++(int) { const_iterator t = *this; ++*this; return t; }
+    friend bool operator==(const const_iterator& a, const const_iterator& b) {
+      return a.s_ == b.s_ && a.g_ == b.g_ && a.e_ == b.e_;
+    }
+    friend bool operator!=(const const_iterator& a, const const_iterator& b) { return !(a == b); }
+
+   private:
+    friend class kmer_hash_view;
+    const_iterator(const kmer_set* s, std::size_t g, std::size_t e) : s_(s), g_(g), e_(e) { settle(); }
+    void settle();  // skip empty groups; materialise the current pair
+    const kmer_set* s_ = nullptr;
+    std::size_t g_ = 0, e_ = 0;  // group (0 = elements, i = other_masks[i - 1]), element
+    std::optional<value_type> cur_;
+  };
+  using iterator = const_iterator;
+
+  std::size_t size() const;
+  bool empty() const { return size() == 0; }
+  std::size_t count(const kmer& k) const;
+  bool contains(const kmer& k) const { return count(k) != 0; }
+  int at(const kmer& k) const;  // 1, or std::out_of_range like unordered_map::at
+  const_iterator find(const kmer& k) const;
+  const_iterator begin() const;
+  const_iterator end() const;
+  const_iterator cbegin() const { return begin(); }
+  const_iterator cend() const { return end(); }
+
+ private:
+  friend struct kmer_set;
+  explicit kmer_hash_view(const kmer_set* s) : s_(s) {}
+  const kmer_set* s_;
+};
+
 struct kmer_set {
   int window_length = 0;
   kmer_bitset mask;
   bool has_mask = false;
-  std::vector<kmer_bitset> elements;  // ascending
+  std::vector<kmer_bitset> elements;  // masked bits under `mask`, ascending, unique
+  struct mask_group {
+    int window_length;
+    kmer_bitset mask;
+    std::vector<kmer_bitset> elements;  // ascending, unique
+  };
+  std::vector<mask_group> other_masks;  // further masks, in first-insertion order
+  kmer_hash_view kmer_hashes{this};     // kmer.hpp:162
 
-  // kmer.hpp:170-178 — set insert (duplicates collapse)
+  kmer_set() = default;
+  kmer_set(const kmer_set& o)
+      : window_length(o.window_length), mask(o.mask), has_mask(o.has_mask), elements(o.elements),
+        other_masks(o.other_masks) {}
+  kmer_set(kmer_set&& o) noexcept
+      : window_length(o.window_length), mask(o.mask), has_mask(o.has_mask),
+        elements(std::move(o.elements)), other_masks(std::move(o.other_masks)) {}
+  kmer_set& operator=(const kmer_set& o) {
+    window_length = o.window_length; mask = o.mask; has_mask = o.has_mask;
+    elements = o.elements; other_masks = o.other_masks;
+    return *this;
+  }
+  kmer_set& operator=(kmer_set&& o) noexcept {
+    window_length = o.window_length; mask = o.mask; has_mask = o.has_mask;
+    elements = std::move(o.elements); other_masks = std::move(o.other_masks);
+    return *this;
+  }
+
+  // kmer.hpp:170-178 — set insert (duplicates collapse; any mix of masks)
   void insert_kmers(const std::vector<kmer>& kmers);
   // kmer.hpp:186-189
-  inline int kmer_set_size() const { return (int)elements.size(); }
+  int kmer_set_size() const;
   bool contains(const kmer& k) const;
+  // the sorted masked bits held under mask m (nullptr if none)
+  const std::vector<kmer_bitset>* elements_for(const kmer_bitset& m) const;
 };
 
 int kmer_set_intersection(const kmer_set& ks1, const kmer_set& ks2);
 
 // ---- sketch builders (kmer_set.cpp:54-133, kmer_sliding.cpp:199-238) ------------------------
+// The reference's plug-in point: any std::function<bool(const kmer)> predicate,
+// called for every window of every run in order (kmer_sliding.cpp:144-185),
+// with the reference's kmer (window_length, kmer_bits, mask, masked_bits).
+using sketching_condition_t = std::function<bool(const kmer)>;
+
+kmer_set kmer_set_from_fasta_file(const char fasta_filename[], const kmer_bitset& mask,
+                                  const int window_length, const sketching_condition_t& sketching_cond);
+std::vector<kmer_set> kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
+                                                 const kmer_bitset& mask, const int window_length,
+                                                 const sketching_condition_t& sketching_cond);
+// One host thread per file (the reference's cilk_for, kmer_set.cpp:124): the
+// predicate is called concurrently for different files and must be thread-safe,
+// as in the reference.
+std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
+                                                          const kmer_bitset& mask, const int window_length,
+                                                          const sketching_condition_t& sketching_cond);
+std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketching_condition_t& sketching_cond);
+void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& kmer_list,
+                                                  const std::vector<std::vector<uint8_t>>& nucleotide_strings,
+                                                  const kmer_bitset& mask, const int window_length,
+                                                  const sketching_condition_t& sketching_cond);
+
+// GPU-selected forms: a sketch_policy descriptor (FracMinHash or bottom-s), or
+// frac_mod_condition (converted to its FracMinHash descriptor).
 kmer_set kmer_set_from_fasta_file(const char fasta_filename[], const kmer_bitset& mask,
                                   const int window_length, const sketch_policy& policy);
 std::vector<kmer_set> kmer_sets_from_fasta_files(const int num_files, char* fasta_filenames[],
@@ -215,10 +332,9 @@ std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files,
                                                           const sketch_policy& policy);
 // nucleotide_string_list_to_kmers[_by_reference] (kmer_sliding.cpp:199-238):
 // every selected window of every run, in order, duplicates kept, each with
-// the reference's kmer_bits / masked_bits.  The predicate must be a
-// per-k-mer FracMinHash condition (frac_mod_condition, or sketch_policy::frac;
-// c = 1 keeps every window); a bottom-s policy throws std::invalid_argument.
-// Codes are used as the reference uses them (low two bits, kmer_sliding.cpp:26-47).
+// the reference's kmer_bits / masked_bits.  The policy must be a per-k-mer
+// FracMinHash condition (c = 1 keeps every window); a bottom-s policy throws
+// std::invalid_argument.  Codes act through their low two bits (kmer_sliding.cpp:26-47).
 std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
                                                   const kmer_bitset& mask, const int window_length,
                                                   const sketch_policy& sketching_cond);
@@ -231,6 +347,32 @@ void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& kmer_list,
 kmer_set nucleotide_string_list_to_kmer_set(const std::vector<std::vector<uint8_t>>& nucleotide_strings,
                                             const kmer_bitset& mask, const int window_length,
                                             const sketch_policy& policy);
+
+// frac_mod_condition is both callable and a descriptor; these exact overloads
+// pick the GPU-selected form.
+inline kmer_set kmer_set_from_fasta_file(const char f[], const kmer_bitset& m, const int w,
+                                         const frac_mod_condition& c) {
+  return kmer_set_from_fasta_file(f, m, w, sketch_policy(c));
+}
+inline std::vector<kmer_set> kmer_sets_from_fasta_files(const int n, char* f[], const kmer_bitset& m,
+                                                        const int w, const frac_mod_condition& c) {
+  return kmer_sets_from_fasta_files(n, f, m, w, sketch_policy(c));
+}
+inline std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int n, char* f[], const kmer_bitset& m,
+                                                                 const int w, const frac_mod_condition& c) {
+  return parallel_kmer_sets_from_fasta_files(n, f, m, w, sketch_policy(c));
+}
+inline std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<uint8_t>>& r,
+                                                         const kmer_bitset& m, const int w,
+                                                         const frac_mod_condition& c) {
+  return nucleotide_string_list_to_kmers(r, m, w, sketch_policy(c));
+}
+inline void nucleotide_string_list_to_kmers_by_reference(std::vector<kmer>& out,
+                                                         const std::vector<std::vector<uint8_t>>& r,
+                                                         const kmer_bitset& m, const int w,
+                                                         const frac_mod_condition& c) {
+  nucleotide_string_list_to_kmers_by_reference(out, r, m, w, sketch_policy(c));
+}
 
 // ---- pairwise intersections (kmer_set.cpp:143-184) ------------------------------------------------
 std::vector<int> compute_pairwise_kmer_set_intersections(const std::vector<kmer_set*>& kmer_sets_1,

@@ -1320,6 +1320,18 @@ int sks_sketch_union(sks_ctx* c, const uint64_t* d_in, uint64_t n, uint64_t* d_o
   return SKS_OK;
 }
 
+int sks_sketch_union_wide(sks_ctx* c, const uint64_t* d_in, uint64_t n, uint64_t* d_out,
+                          uint64_t* n_out) {
+  if (!c || !n_out) return sks::fail(SKS_E_ARG, "sks_sketch_union_wide: null argument");
+  if (n && (!d_in || !d_out)) return sks::fail(SKS_E_ARG, "sks_sketch_union_wide: null argument");
+  if (n >= (1ull << 32)) return sks::fail(SKS_E_UNSUPPORTED, "sks_sketch_union_wide: n >= 2^32");
+  if ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15)
+    return sks::fail(SKS_E_ARG, "sks_sketch_union_wide: buffers must be 16-byte aligned");
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::sort_unique_u128(d_in, n, d_out, n_out, c->iwork, c->stream));
+  return SKS_OK;
+}
+
 uint32_t sks_join_layout_log_b(uint32_t max_sketch_size) { return sks::join_log_b(max_sketch_size); }
 uint32_t sks_join_layout_capacity(void) { return sks::join_cap(); }
 

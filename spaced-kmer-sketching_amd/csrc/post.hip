@@ -660,6 +660,41 @@ hipError_t sort_unique_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64
   return pinned_d2h(n_out, d_cnt, 8, s);
 }
 
+// The same for 128-bit k-mers (w > 32) stored as (lo, hi) word pairs: on a
+// little-endian device the pair IS the __uint128_t hi * 2^64 + lo, so one radix
+// sort over 128 bits orders them like the reference's operator< on 128-bit
+// dynamic_bitsets (most significant block first).  in/out 16-byte aligned.
+hipError_t sort_unique_u128(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* n_out,
+                            Scratch& tmp, hipStream_t s) {
+  using u128 = rocprim::uint128_t;
+  *n_out = 0;
+  if (n == 0) return hipSuccess;
+  if (n >= (1ull << 32)) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) return hipErrorInvalidValue;
+  const u128* kin = reinterpret_cast<const u128*>(in);
+  u128* kout = reinterpret_cast<u128*>(out);
+  size_t sort_bytes = 0, uniq_bytes = 0;
+  hipError_t e;
+  if ((e = rocprim::radix_sort_keys(nullptr, sort_bytes, kin, kout, (size_t)n, 0, 128, s)) != hipSuccess)
+    return e;
+  if ((e = rocprim::unique(nullptr, uniq_bytes, kout, kout, (uint64_t*)nullptr, (size_t)n,
+                           rocprim::equal_to<u128>(), s)) != hipSuccess)
+    return e;
+  const size_t o_sorted = 0, o_cnt = (n * 16 + 15) & ~(size_t)15, o_tmp = o_cnt + 16;
+  if ((e = tmp.reserve(o_tmp + std::max(sort_bytes, uniq_bytes))) != hipSuccess) return e;
+  char* w = static_cast<char*>(tmp.ptr);
+  u128* sorted = reinterpret_cast<u128*>(w + o_sorted);
+  uint64_t* d_cnt = reinterpret_cast<uint64_t*>(w + o_cnt);
+  void* t = w + o_tmp;
+  size_t tb = tmp.bytes - o_tmp;
+  if ((e = rocprim::radix_sort_keys(t, tb, kin, sorted, (size_t)n, 0, 128, s)) != hipSuccess) return e;
+  tb = tmp.bytes - o_tmp;
+  if ((e = rocprim::unique(t, tb, sorted, kout, d_cnt, (size_t)n, rocprim::equal_to<u128>(), s)) !=
+      hipSuccess)
+    return e;
+  return pinned_d2h(n_out, d_cnt, 8, s);
+}
+
 hipError_t launch_synth(uint8_t* out, uint64_t n, uint64_t seed, uint64_t mut_seed,
                         uint64_t mut_thresh, uint64_t pos_offset, hipStream_t s) {
   if (n == 0) return hipSuccess;

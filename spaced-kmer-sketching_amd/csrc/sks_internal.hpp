@@ -112,6 +112,8 @@ hipError_t seg_unique_scan(const uint64_t* keys, const uint64_t* keys2, uint64_t
 // segment g at pos[off[g]] (the global unique rank, i.e. dense CSR output).
 hipError_t sort_unique_u64(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* n_out,
                            Scratch& tmp, hipStream_t s);
+hipError_t sort_unique_u128(const uint64_t* in, uint64_t n, uint64_t* out, uint64_t* n_out,
+                            Scratch& tmp, hipStream_t s);
 hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint64_t total,
                               uint64_t max_len, const uint64_t* d_off, uint32_t n_seg,
                               const uint32_t* d_flag,

@@ -235,18 +235,20 @@ def genome_chunk(n_bytes, w, world, rank):
 
 
 def sketch_genome_sharded(n_bytes, w, world, rank, build_chunk, union, device="cpu"):
-    """build_chunk(a, b) -> (int64 tensor of the chunk's sorted k-mers, windows);
-    union(t) -> sorted distinct values of t.  Returns (sketch, total windows) on
+    """build_chunk(a, b) -> (int64 tensor of the chunk's sorted k-mers, windows):
+    shape [k] for w <= 32, [k, 2] (lo, hi) for w > 32; union(t) -> sorted distinct
+    k-mers of t (same shape convention).  Returns (sketch, total windows) on
     every rank."""
     a, b = genome_chunk(n_bytes, w, world, rank)
     vals, nw = build_chunk(a, b)
     if world == 1:
         return vals, nw
-    k = vals.numel()
+    k = vals.shape[0]
+    rest = tuple(vals.shape[1:])
     kmax = max(1, _max_over(k, world, device))
-    pad = torch.zeros(kmax, dtype=torch.int64, device=device)
+    pad = torch.zeros((kmax,) + rest, dtype=torch.int64, device=device)
     pad[:k] = vals
-    g = _gather_flat(pad, world).view(world, kmax)
+    g = _gather_flat(pad.reshape(-1), world).view((world, kmax) + rest)
     sizes = _gather_flat(torch.tensor([k], dtype=torch.int64, device=device), world)
     keep = torch.arange(kmax, device=device).view(1, kmax) < sizes.view(world, 1)
     t = torch.tensor([nw], dtype=torch.int64, device=device)

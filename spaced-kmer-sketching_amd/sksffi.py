@@ -53,7 +53,7 @@ EXPORTED = [
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
     "sks_synth_bases", "sks_intersect_sym", "sks_intersect_sym_tiles",
-    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_ctx_set_intersect_kernel", "sks_join_layout_log_b", "sks_sketch_union",
+    "sks_ctx_last_intersect_ms", "sks_ctx_set_scan_grid", "sks_ctx_set_intersect_kernel", "sks_join_layout_log_b", "sks_sketch_union", "sks_sketch_union_wide",
     "sks_join_layout_capacity", "sks_join_layout_build", "sks_intersect_sym_layout", "sks_fasta_parse_device",
     "sks_ctx_last_ingress_ms", "sks_kmer_list_build", "sks_kmer_list_free", "sks_kmer_list_total",
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
@@ -112,6 +112,7 @@ def lib():
     L.sks_ctx_set_scan_grid.argtypes = [vp, C.c_int]
     L.sks_ctx_set_intersect_kernel.argtypes = [vp, C.c_int]
     L.sks_sketch_union.argtypes = [vp, vp, C.c_uint64, vp, u64p]
+    L.sks_sketch_union_wide.argtypes = [vp, vp, C.c_uint64, vp, u64p]
     L.sks_join_layout_log_b.argtypes = [C.c_uint32]
     L.sks_join_layout_log_b.restype = C.c_uint32
     L.sks_join_layout_capacity.argtypes = []
@@ -294,10 +295,13 @@ class Context:
     def set_scan_grid(self, grid):
         check(lib().sks_ctx_set_scan_grid(self.h, grid))
 
-    def sketch_union(self, d_in, n, d_out):
-        """sks_sketch_union: sorted distinct values of d_in[0, n) into d_out; returns the count."""
+    def sketch_union(self, d_in, n, d_out, elem_words=1):
+        """sks_sketch_union (elem_words 1: u64 values) or sks_sketch_union_wide
+        (elem_words 2: n (lo, hi) pairs): sorted distinct k-mers of d_in into d_out;
+        returns the count."""
         k = C.c_uint64(0)
-        check(lib().sks_sketch_union(self.h, C.c_void_p(d_in), n, C.c_void_p(d_out), C.byref(k)))
+        fn = lib().sks_sketch_union if elem_words == 1 else lib().sks_sketch_union_wide
+        check(fn(self.h, C.c_void_p(d_in), n, C.c_void_p(d_out), C.byref(k)))
         return int(k.value)
 
     def join_layout_build(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_data, out_ids,

@@ -287,36 +287,49 @@ def _genome():
     return g.tobytes()
 
 
-def _shard_worker(rank, world, port, q):
+def _union128(t):
+    """Sorted distinct (lo, hi) rows as 128-bit values (the contract of
+    sks_sketch_union_wide), via numpy on the host."""
+    a = t.numpy().view(np.uint64).reshape(-1, 2)
+    a = np.unique(a, axis=0)
+    order = np.lexsort((a[:, 0], a[:, 1]))  # hi major, lo minor
+    return torch.from_numpy(a[order].view(np.int64).copy())
+
+
+def _shard_worker(rank, world, port, q, w, k):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = _genome()
-    m = O.mask(GW, 21, 0)
+    m = O.mask(w, k, 0)
 
     def build_chunk(a, b):
-        sk, nw = O.sketch(O.cut_runs(g[a:b]), GW, m, "frac", 50)
+        sk, nw = O.sketch(O.cut_runs(g[a:b]), w, m, "frac", 50)
+        if w > 32:
+            return torch.from_numpy(sk.view(np.int64).copy()), nw  # [k, 2] (lo, hi)
         return torch.from_numpy(sk[:, 0].view(np.int64).copy()), nw
-    union = lambda t: torch.unique(t, sorted=True)
-    sk, nw = sks_dist.sketch_genome_sharded(len(g), GW, world, rank, build_chunk, union)
+    union = _union128 if w > 32 else (lambda t: torch.unique(t, sorted=True))
+    sk, nw = sks_dist.sketch_genome_sharded(len(g), w, world, rank, build_chunk, union)
     q.put((rank, sk.numpy(), nw))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_one_genome_sharded_gloo(world):
+@pytest.mark.parametrize("world,w,k", [(2, GW, 21), (3, GW, 21), (3, 45, 30)])
+def test_one_genome_sharded_gloo(world, w, k):
     """Every rank's union of the chunk sketches equals the whole genome's sketch,
-    and the windows add up (no window counted twice across a halo)."""
+    and the windows add up (no window counted twice across a halo); w = 45 moves
+    (lo, hi) k-mer pairs through the same gather."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q, w, k)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want, nw = O.sketch(O.cut_runs(_genome()), GW, O.mask(GW, 21, 0), "frac", 50)
+    want, nw = O.sketch(O.cut_runs(_genome()), w, O.mask(w, k, 0), "frac", 50)
     for _, sk, n in res:
-        assert np.array_equal(sk.view(np.uint64), want[:, 0]) and n == nw
+        got = sk.view(np.uint64).reshape(-1, 2) if w > 32 else sk.view(np.uint64)
+        assert np.array_equal(got, want if w > 32 else want[:, 0]) and n == nw

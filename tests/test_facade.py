@@ -98,3 +98,71 @@ def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param):
     inter = [O.intersect(sk[i], sk[j]) for i in range(n) for j in range(n)]
     assert out["inter"] == inter
     assert out["inter_serial_equal"]
+
+
+REF_CALLER = os.path.join(ROOT, "tests", "cpp", "build", "ref_caller")
+
+
+def _odd_rule(lo):
+    return bin(int(lo)).count("1") % 2 == 0 and (int(lo) & 0xffffffff) % 3 == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,k,c", [(31, 21, 200), (21, 21, 50), (40, 30, 20)])
+def test_reference_shaped_caller_std_function(tmp_path, w, k, c):
+    """tests/cpp/ref_caller.cpp uses only the reference's API names and passes
+    std::function predicates (a free function like kmer-sketching.cpp:29-34 and
+    lambdas) to the builders, as kmer-sketching.cpp:151-212 does.  Sets, pair
+    counts and ANI equal the oracle's; the predicate runs once per window; a
+    rule no sketch descriptor can express selects exactly the oracle's windows;
+    kmer_hashes iterates the set; k-mers of two masks in one set count per mask."""
+    build_facade_test()
+    files = []
+    for i in range(3):
+        g = synth.bases(25000, seed=81, mut_seed=600 + i, mut_rate=0.02 * i)
+        g[3000:3020] = ord("N")
+        p = tmp_path / f"r{i}.fa"
+        p.write_bytes(synth.fasta_text([(f"r{i}_a", g[:11000]), (f"r{i}_b", g[11000:])], width=61))
+        files.append(str(p))
+    r = subprocess.run([REF_CALLER, str(w), str(k), str(c)] + files, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    m = O.mask(w, k, 0)
+    assert int(out["mask"], 16) == m
+    kk = bin(m).count("1") // 2
+    assert out["k"] == kk
+    runs = [O.fasta_runs(f) for f in files]
+    sk, nws = [], []
+    for i in range(3):
+        want, nw = O.sketch(runs[i], w, m, "frac", c)
+        assert [int(h, 16) for h in out["sets"][i]] == [int(lo) | int(hi) << 64 for lo, hi in want]
+        sk.append(want)
+        nws.append(nw)
+    n = 3
+    order = [(i, j) for i in range(n) for j in range(n)]
+    inter = [O.intersect(sk[i], sk[j]) for i, j in order]
+    assert out["inter"] == inter
+    assert out["pairs"] == [[files[i], files[j]] for i, j in order]
+    for p, (i, j) in enumerate(order):
+        assert float.fromhex(out["ani"][p]) == O.binomial_estimator(O.containment(inter[p], len(sk[i])), kk)
+    assert out["lambda_equal"]
+    assert out["calls0"] == nws[0] and out["one_size"] == len(sk[0])
+    every = O.kmer_list(runs[0], w, m, c=1)  # every window in order: kmer_bits lo, hi, masked lo, hi
+    keep = np.array([_odd_rule(lo) and True for lo in every[:, 2]], dtype=bool) if len(every) else \
+        np.zeros(0, bool)
+    sel = every[keep]
+    assert [[int(a, 16) for a in row] for row in out["list"]] == \
+        [[int(r_[0]) | int(r_[1]) << 64, int(r_[2]) | int(r_[3]) << 64] for r_ in sel]
+    custom = sorted({int(r_[2]) | int(r_[3]) << 64 for r_ in sel})
+    assert [int(h, 16) for h in out["custom"]] == custom and len(custom) > 0
+    m2 = O.mask(w, k, 5)
+    assert int(out["mask2"], 16) == m2
+    # w = k: both masks are all ones, so the second insert adds nothing new
+    s2 = [O.sketch(runs[i], w, m2, "frac", c)[0] for i in range(2)] if m2 != m else \
+        [np.zeros((0, 2), np.uint64)] * 2
+    assert out["mixed_sizes"] == [len(sk[0]) + len(s2[0]), len(sk[1]) + len(s2[1])]
+    both = O.intersect(sk[0], sk[1]) + O.intersect(s2[0], s2[1])
+    assert out["mixed_inter"] == both
+    # (mixed0, mixed1), (mixed1, data[1]): only the mask-m part is shared, (mixed0, mixed0)
+    assert out["mixed_pairs"] == [both, len(sk[1]), len(sk[0]) + len(s2[0])]

@@ -276,6 +276,42 @@ def test_frac_chunk_union_property(torch_cuda, ctx):
         assert sksffi.frac_min_hash(int(x), m, w, 1, 0) % 1000 == 0
 
 
+def test_wide_chunk_union_w45(torch_cuda, ctx):
+    """The sharded-genome union for 32 < w <= 64 (sks_sketch_union_wide): the
+    union of w = 45 chunk sketches ((w-1)-base halos) equals the whole-genome
+    sketch and the oracle's, ordered as 128-bit values (hi word first)."""
+    torch = torch_cuda
+    L, w, k, c = 3_000_000, 45, 30, 20
+    m = O.mask(w, k, 1)
+    assert m >> 64  # the mask reaches the high word
+    dev = torch.empty(L + 1, dtype=torch.uint8, device="cuda:0")
+    ctx.synth_bases(dev.data_ptr(), L, 57)
+    dev[L] = ord("\n")
+    dev[50_000:50_030] = ord("N")
+    whole = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, m, sksffi.SKS_FRAC_MOD, c)
+    S = whole.sketch(0)
+    want, _ = O.sketch(O.cut_runs(dev.cpu().numpy().tobytes()), w, m, "frac", c)
+    assert np.array_equal(S, want)
+    cuts = [0, 1_000_001, 2_222_222, L + 1]
+    parts = []
+    for i in range(len(cuts) - 1):
+        a, b = cuts[i], min(L + 1, cuts[i + 1] + w - 1)
+        ss = ctx.sketch_build(dev.data_ptr() + a, b - a, [0, b - a], w, m, sksffi.SKS_FRAC_MOD, c)
+        parts.append(ss.sketch(0))
+    cat = np.concatenate(parts)
+    rng = np.random.default_rng(4)
+    cat = cat[rng.permutation(len(cat))]  # any order in
+    d_in = torch.from_numpy(np.ascontiguousarray(cat).view(np.int64)).to("cuda:0")
+    d_out = torch.empty_like(d_in)
+    n = ctx.sketch_union(d_in.data_ptr(), len(cat), d_out.data_ptr(), elem_words=2)
+    torch.cuda.synchronize()
+    assert n == len(S)
+    assert np.array_equal(d_out[:n].cpu().numpy().view(np.uint64), S)
+    assert ctx.sketch_union(d_in.data_ptr(), 0, d_out.data_ptr(), elem_words=2) == 0
+    with pytest.raises(sksffi.SksError):  # 16-byte alignment is required
+        ctx.sketch_union(d_in.data_ptr() + 8, 4, d_out.data_ptr(), elem_words=2)
+
+
 def test_genome_over_4gb_chunk_union(torch_cuda, ctx):
     """Maximum sizes: one 4.6 GB genome (byte offsets, tile and window counts past
     2^32) equals the union of the sketches of two halves with a (w-1)-base halo,

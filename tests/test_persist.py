@@ -5,7 +5,7 @@ is read here by an independent Python parser, so the layout is pinned by the
 documentation rather than by the C++ code alone.  CPU tests drive the host
 facade (sks::save_kmer_sets / load_kmer_sets) through tests/cpp/test_facade;
 GPU tests round-trip device sets (sks_sketch_set_save / _load / _concat) and
-check that loaded sketches intersect exactly like freshly built ones."""
+check that loaded sketches equal the oracle's and intersect like freshly built ones."""
 import os
 import struct
 import subprocess
@@ -173,6 +173,10 @@ def test_device_save_load_concat(gpu, tmp_path, w, k, kind, param):
     assert back.names() == names
     assert back.info() == ss.info()
     for i in range(6):
+        # loaded sets equal the oracle's sketches, not only the in-process build
+        want, nw = O.sketch(O.cut_runs(genomes[i]), w, m, kind, param)
+        assert np.array_equal(back.sketch(i), want), i
+        assert f["windows"][i] == nw
         assert np.array_equal(back.sketch(i), ss.sketch(i))
     assert np.array_equal(_all_pairs(torch, ctx, back), _all_pairs(torch, ctx, ss))
     # shards built separately and concatenated == one build over all genomes
