@@ -430,6 +430,123 @@ def cpu_crosscheck_c3(ctx, buf, mask, sample_bytes):
                       f"{dt:.1f} s; set equal to the GPU's"}
 
 
+# ---- config 2 ------------------------------------------------------------------------
+C2_LEN, C2_SEED, C2_S, C2_BATCH = 5_000_000, 2, 10000, 64
+
+
+def run_c2(ctx, mask, steps, warmup, inflight=2):
+    """Config 2 of BASELINE.json: one 5 Mb bacterial-scale genome (synthetic,
+    seed 2), w=31/k=21 spaced seed, bottom-s s=10000.  One such build is
+    launch/latency-bound (a few hundred microseconds of GPU work spread over a
+    dozen launches and two host syncs), so three numbers are reported, each
+    named for what it is:
+      * single: K builds one at a time — wall time per build (k-mers/s of a
+        complete sks_sketch_build) and the scan kernel's own time (hipEvents)
+        with its HBM roofline fraction;
+      * inflight: the same single-genome build with `inflight` contexts on their
+        own HIP streams and host threads (builds overlap);
+      * batched: C2_BATCH distinct 5 Mb genomes (genome 0 = the config-2
+        genome) in ONE sks_sketch_build call (the reference's per-file sets,
+        kmer_set.cpp:112-133, in one launch sequence).
+    Every sketch is checked against the first build (and batch genome 0 equal to
+    it); the oracle comparison at this size is tests/test_gpu_parity.py::
+    test_config2_5mb_bottom_s."""
+    import threading
+    seg_len = C2_LEN + 1
+    buf = torch.empty(seg_len * C2_BATCH, dtype=torch.uint8, device="cuda")
+    for i in range(C2_BATCH):
+        ctx.synth_bases(buf.data_ptr() + i * seg_len, C2_LEN, C2_SEED if i == 0 else 2000 + i)
+        buf[i * seg_len + C2_LEN] = ord("\n")
+    torch.cuda.synchronize()
+    windows = C2_LEN - W + 1
+
+    def one(c):
+        return c.sketch_build(buf.data_ptr(), seg_len, [0, seg_len], W, mask, sksffi.SKS_BOTTOM_S, C2_S)
+
+    ref = one(ctx).sketch(0)
+    for _ in range(warmup):
+        del_ = one(ctx)
+        del del_
+    scan_ms, surv = [], []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ss = one(ctx)
+        t = ctx.timings()
+        scan_ms.append(t["scan_ms"])
+        surv.append(t["survivors"])
+        assert int(ss.windows()[0]) == windows
+        del ss
+    torch.cuda.synchronize()
+    t_single = (time.perf_counter() - t0) / steps
+    scan = float(np.median(scan_ms))
+    # bottom-s candidates are written as (k-mer, k-mer) record pairs: 16 B each
+    alg = seg_len + 16 * float(np.mean(surv))
+    achieved = alg / (scan * 1e-3) / 1e9
+
+    # in flight: one context + stream + host thread per build in flight
+    streams = [torch.cuda.Stream() for _ in range(max(1, inflight))]
+    ctxs = [sksffi.Context(torch.cuda.current_device(), st.cuda_stream) for st in streams]
+    for c in ctxs:
+        assert np.array_equal(one(c).sketch(0), ref)
+    errors = []
+
+    def worker(i):
+        try:
+            for _ in range(i, steps, len(ctxs)):
+                ss = one(ctxs[i])
+                ss.free(stream=streams[i].cuda_stream)
+        except Exception as e:  # surfaced after the join
+            errors.append(e)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(ctxs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    t_inflight = (time.perf_counter() - t0) / steps
+    if errors:
+        raise errors[0]
+
+    # batched: C2_BATCH genomes in one build
+    seg = [i * seg_len for i in range(C2_BATCH + 1)]
+    bs = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, C2_S)
+    assert np.array_equal(bs.sketch(0), ref) and (bs.sizes() == C2_S).all()
+    del bs
+    reps = max(2, steps // 4)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        bs = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, C2_S)
+        bt = ctx.timings()
+        del bs
+    torch.cuda.synchronize()
+    t_batch = (time.perf_counter() - t0) / reps
+    bscan = bt["scan_ms"]
+    balg = seg[-1] + 16 * bt["survivors"]
+    del buf
+    return {
+        "metric": "k-mers hashed/s, config 2", "unit": "k-mers/s", "steps": steps,
+        "config": {"workload": "config2: 1x5 Mb genome, spaced seed w=31/k=21 (mask seed 0), "
+                               "bottom-s s=10000", "genome_len": C2_LEN, "s": C2_S,
+                   "windows_per_genome": windows},
+        "single": {"kmers_per_s_build": windows / t_single, "ms_per_build": t_single * 1e3,
+                   "scan_kernel_ms": scan, "kmers_per_s_scan": windows / (scan * 1e-3),
+                   "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                                "algorithmic_bytes_per_launch": alg},
+                   "note": "one complete build at a time, wall clock incl. host syncs; the "
+                           "scan kernel alone by hipEvents"},
+        "inflight": {"builds_in_flight": len(ctxs), "kmers_per_s": windows / t_inflight,
+                     "ms_per_build": t_inflight * 1e3},
+        "batched": {"genomes_per_build": C2_BATCH, "kmers_per_s": C2_BATCH * windows / t_batch,
+                    "ms_per_build": t_batch * 1e3, "scan_kernel_ms": bscan,
+                    "scan_roofline_frac": balg / (bscan * 1e-3) / 1e9 / HBM_PEAK_GBS},
+    }
+
+
 # ---- config 4 ------------------------------------------------------------------------
 def c4_genome_seeds(g):
     anc = g // (C4_GENOMES // C4_ANCESTORS)
@@ -473,37 +590,9 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         buf[seg[i] + C4_LEN] = ord("\n")
     torch.cuda.synchronize()
     mat = torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32, device="cuda")
-    nb_local = (n_local + 63) // 64
     dev = "cuda" if os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
 
-    lay_bufs = {}
-
-    def layout_fns(ss, sizes_h):
-        data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
-        tot = int(sizes_h.astype(np.int64).sum())
-
-        def build(log_b):
-            B1 = (1 << log_b) + 1
-            key = (tot, log_b)
-            if key not in lay_bufs:  # layout buffers persist across steps
-                lay_bufs.clear()
-                lay_bufs[key] = (torch.empty(max(tot, 1), dtype=torch.int64, device="cuda"),
-                                 torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda"),
-                                 torch.empty(max(nb_local * B1, 1), dtype=torch.int32, device="cuda"),
-                                 torch.empty(nb_local + 1, dtype=torch.int64, device="cuda"))
-            out = lay_bufs[key]
-            mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b,
-                                       *(t.data_ptr() for t in out))
-            return tuple(t.to(dev) for t in out) + (mx,)
-
-        def count(n, log_b, d, i, b, s, t0, t1, out):
-            lay = [t.to("cuda") for t in (d, i, b, s)]
-            tgt = out if out.is_cuda else torch.empty(out.shape, dtype=out.dtype, device="cuda")
-            ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in lay), t0, t1,
-                                     tgt.data_ptr())
-            if tgt is not out:
-                out.copy_(tgt.cpu())
-        return build, count
+    lay_bufs = {}  # join layout buffers, reused across steps
 
     t_sketch = t_pairs = 0.0
     timed = 0
@@ -521,7 +610,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         t1 = time.perf_counter()
         # layouts of this rank's blocks, all-gathered; symmetric join tiles of
         # this rank; all-reduce of the counts
-        build, count = layout_fns(ss, local_sizes)
+        build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs)
         out = mat if dev == "cuda" else torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32)
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max, sksffi.join_layout_log_b,
                                        sksffi.join_layout_capacity(), build, count, device=dev,
@@ -661,6 +750,20 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
     }
 
 
+def latest_traffic_json():
+    """profiles/rNN/traffic.json of the newest round that has one: written by
+    tools/profile_round.sh from rocprofv3 PMC passes over this same bench command
+    (FETCH_SIZE and WRITE_SIZE cannot share a pass), per timed launch."""
+    import glob
+    import re
+    found = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")):
+        m = re.search(r"[/\\]r(\d+)[/\\]traffic\.json$", f)
+        if m:
+            found.append((int(m.group(1)), f))
+    return max(found)[1] if found else ""
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -673,10 +776,13 @@ def main():
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-c3-sharded", action="store_true")
+    ap.add_argument("--no-c2", action="store_true")
     ap.add_argument("--inflight", type=int, default=2,
                     help="config-3 builds in flight (one context + HIP stream each)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"))
+    ap.add_argument("--traffic-json", default=latest_traffic_json(),
+                    help="PMC HBM traffic of the scan launches this command times "
+                         "(tools/profile_round.sh; default: the newest profiles/rNN)")
     args = ap.parse_args()
 
     world, rank, local = dist_setup(args.gpus, args.dist_backend)
@@ -726,10 +832,15 @@ def main():
     scan_avg_ms = float(np.mean(scan_ms))
     alg_bytes = n_bytes + 8 * float(np.mean(survivors))
     achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
+    traffic = traffic_src = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f).get("scan_hbm_bytes_per_launch")
+        traffic_src = os.path.relpath(args.traffic_json, ROOT)
+
+    c2 = None
+    if not args.no_c2:
+        c2 = run_c2(ctx, mask, steps=max(4, args.steps), warmup=2, inflight=args.inflight)
 
     pairs = None
     if not args.no_pairs:
@@ -771,9 +882,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "scan_kernel<frac, boost-mix, pre-filter>", "kernel_ms": scan_avg_ms,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "kernel_ms_median": float(np.median(scan_ms)),
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "traffic_source": traffic_src,
+                         "timing": "hipEvents around each scan launch of the serial pass "
+                                   "(the --steps builds after --warmup)"},
             "cpu_baseline": cpu,
             "cpu_crosscheck": cpu_x,
+            "config2": c2,
             "pairs": pairs,
             "seed_sweep": sweep,
             "end_to_end": e2e,

@@ -157,6 +157,7 @@ struct Queue {
   uint64_t val[MODE == kModeBottom ? kQCap : 1];
   uint32_t n;
   unsigned long long base;
+  unsigned long long wins;  // windows of the current segment not yet published
 };
 
 template <int MODE>
@@ -180,6 +181,11 @@ __device__ __forceinline__ void emit(const ScanParams& p, Queue<MODE>& q, uint32
 template <int MODE>
 __device__ __forceinline__ void flush(const ScanParams& p, Queue<MODE>& q, uint32_t seg) {
   __syncthreads();
+  // the workgroup's window count: one global atomic per flush, not one per
+  // wave — when a small input gives every workgroup one tile, all of them
+  // finish together and the segment's counter word serialises the atomics
+  // (one word takes ~88 per microsecond, MI355X_MICROARCH.md "dequeue")
+  if (threadIdx.x == 0 && q.wins) atomicAdd(&p.seg_windows[seg], q.wins);
   uint32_t n = q.n < kQCap ? q.n : kQCap;
   if (n) {
     if (threadIdx.x == 0) q.base = atomicAdd(&p.seg_count[seg], (unsigned long long)n);
@@ -195,16 +201,20 @@ __device__ __forceinline__ void flush(const ScanParams& p, Queue<MODE>& q, uint3
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) q.n = 0;
+  if (threadIdx.x == 0) {
+    q.n = 0;
+    q.wins = 0;
+  }
   __syncthreads();
 }
 
-__device__ __forceinline__ void add_windows(const ScanParams& p, uint32_t seg, uint32_t cnt) {
-  // wave reduction, one atomic per wave
+// Windows hashed by this thread for the current segment -> the workgroup's
+// LDS total (published by the next flush of that segment).
+__device__ __forceinline__ void add_windows(unsigned long long& wins, uint32_t cnt) {
   uint32_t v = cnt;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&p.seg_windows[seg], (unsigned long long)v);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(&wins, (unsigned long long)v);
 }
 
 // frac_min_hash of a canonical k-mer (w <= 32, so the high block is 0).
@@ -262,7 +272,10 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
   const int tid = threadIdx.x;
   const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
   const uint64_t t_end = (uint64_t)(blockIdx.x + 1) * p.n_tiles / gridDim.x;
-  if (tid == 0) q.n = 0;
+  if (tid == 0) {
+    q.n = 0;
+    q.wins = 0;
+  }
   if (t_begin >= t_end) return;
 
   const int w = p.w;
@@ -297,7 +310,7 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
   for (uint64_t tile = t_begin; tile < t_end; ++tile) {
     Geom g = tile_geom(p, tile, cur_seg);
     if (g.seg != count_seg) {  // segment change: publish the previous segment
-      add_windows(p, count_seg, win_count);
+      add_windows(q.wins, win_count);
       win_count = 0;
       flush<MODE>(p, q, count_seg);
       count_seg = g.seg;
@@ -368,9 +381,11 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
       // bits of the last multiply. Windows passing that test (1/8 for c = 1000)
       // are queued per wave in LDS and finished 64 at a time, all lanes busy.
       const int lane = tid & 63;
-      ulonglong2* cb = s_cand + (tid >> 6) * kCandCap;
+      // the wave's candidate buffer, wave-uniform: readfirstlane keeps it in an
+      // SGPR so a candidate's LDS address is one v_lshl_add_u32 of its rank
+      ulonglong2* cb = s_cand + __builtin_amdgcn_readfirstlane(tid >> 6) * kCandCap;
       const uint32_t pmask = p.low_mask & 0xFu;
-      const uint32_t klo = (uint32_t)p.kconst;
+      const uint32_t kbits = (uint32_t)p.kconst & pmask;
       uint32_t cnt = 0;  // wave-uniform
       auto finish = [&](uint32_t n) {  // candidates [0, n), n <= 64
         __builtin_amdgcn_wave_barrier();
@@ -387,7 +402,7 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
           const uint64_t c = canon(j);
           const uint64_t z = mix3_head(c);
           const uint32_t ylo = (uint32_t)z * (uint32_t)kMixMul;
-          bool pass = ((ylo ^ (ylo >> 28) ^ klo) & pmask) == 0;
+          bool pass = ((ylo ^ (ylo >> 28)) & pmask) == kbits;
           if constexpr (decltype(checked)::value) {
             const bool valid = ((inv64 >> j) & wmask_bits) == 0;
             win_count += valid ? 1u : 0u;
@@ -464,9 +479,13 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
 
     // 5) flush the queue once it is half full
     __syncthreads();
-    if (q.n >= kQCap / 2) flush<MODE>(p, q, g.seg);
+    if (q.n >= kQCap / 2) {
+      add_windows(q.wins, win_count);
+      win_count = 0;
+      flush<MODE>(p, q, g.seg);
+    }
   }
-  add_windows(p, count_seg, win_count);
+  add_windows(q.wins, win_count);
   flush<MODE>(p, q, count_seg);
 }
 
@@ -481,12 +500,15 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
   __shared__ uint32_t s_inv[kWords + 2];
   __shared__ uint64_t q_a[kQCap / 2], q_b[kQCap / 2], q_c[kQCap / 2];
   __shared__ uint32_t q_n;
-  __shared__ unsigned long long q_base;
+  __shared__ unsigned long long q_base, q_wins;
 
   const int tid = threadIdx.x;
   const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
   const uint64_t t_end = (uint64_t)(blockIdx.x + 1) * p.n_tiles / gridDim.x;
-  if (tid == 0) q_n = 0;
+  if (tid == 0) {
+    q_n = 0;
+    q_wins = 0;
+  }
   if (t_begin >= t_end) return;
   constexpr uint32_t cap = kQCap / 2;
 
@@ -510,6 +532,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
 
   auto wflush = [&](uint32_t seg) {
     __syncthreads();
+    if (tid == 0 && q_wins) atomicAdd(&p.seg_windows[seg], q_wins);
     uint32_t n = q_n < cap ? q_n : cap;
     if (n) {
       if (tid == 0) q_base = atomicAdd(&p.seg_count[seg], (unsigned long long)n);
@@ -523,14 +546,17 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
         }
     }
     __syncthreads();
-    if (tid == 0) q_n = 0;
+    if (tid == 0) {
+      q_n = 0;
+      q_wins = 0;
+    }
     __syncthreads();
   };
 
   for (uint64_t tile = t_begin; tile < t_end; ++tile) {
     Geom g = tile_geom(p, tile, cur_seg);
     if (g.seg != count_seg) {
-      add_windows(p, count_seg, win_count);
+      add_windows(q_wins, win_count);
       win_count = 0;
       wflush(count_seg);
       count_seg = g.seg;
@@ -619,9 +645,13 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
       }
     }
     __syncthreads();
-    if (q_n >= cap / 2) wflush(g.seg);
+    if (q_n >= cap / 2) {
+      add_windows(q_wins, win_count);
+      win_count = 0;
+      wflush(g.seg);
+    }
   }
-  add_windows(p, count_seg, win_count);
+  add_windows(q_wins, win_count);
   wflush(count_seg);
 }
 

@@ -222,6 +222,41 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     return out
 
 
+def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
+    """The build / count callables of all_vs_all_join for this rank's sketches
+    on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
+    `local_sizes` its sizes (numpy).  build(log_b) runs sks_join_layout_build
+    into device buffers (kept in `cache` across calls of the same shape) and
+    returns them on `device`; count(...) runs sks_intersect_sym_layout (on the
+    GPU, staging through `device` tensors when that is the CPU, as with gloo)."""
+    n_local = len(local_sizes)
+    nb_local = (n_local + TILE - 1) // TILE
+    data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
+    tot = int(local_sizes.astype("int64").sum()) if n_local else 0
+    cache = {} if cache is None else cache
+
+    def build(log_b):
+        B1 = (1 << log_b) + 1
+        key = (tot, log_b, nb_local)
+        if key not in cache:  # layout buffers persist across steps
+            cache.clear()
+            cache[key] = (torch.empty(max(tot, 1), dtype=torch.int64, device="cuda"),
+                          torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda"),
+                          torch.empty(max(nb_local * B1, 1), dtype=torch.int32, device="cuda"),
+                          torch.empty(nb_local + 1, dtype=torch.int64, device="cuda"))
+        out = cache[key]
+        mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out))
+        return tuple(t.to(device) for t in out) + (mx,)
+
+    def count(n, log_b, d, i, b, s, t0, t1, out):
+        lay = [t.to("cuda") for t in (d, i, b, s)]
+        tgt = out if out.is_cuda else torch.empty(out.shape, dtype=out.dtype, device="cuda")
+        ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in lay), t0, t1, tgt.data_ptr())
+        if tgt is not out:
+            out.copy_(tgt.cpu())
+    return build, count
+
+
 # ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------
 # FracMinHash keeps a k-mer on its own hash, so the sketch of a genome is the
 # union of the sketches of chunks cut with (w-1)-base halos: rank r scans the

@@ -1,0 +1,147 @@
+"""GPU parity at the benchmark's own sizes (BASELINE.json configs 4 and 5).
+
+Config 4: 1000 synthetic 5 Mb genomes (10 ancestors x 100 mutated
+descendants, bench.c4_genome_seeds), spaced seed w=31/k=21, bottom-s
+s=10000, counted all-vs-all through exactly the path bench.py times
+(sks_dist.all_vs_all_join over sks_join_layout_build +
+sks_intersect_sym_layout, world 1).  Checked: 8 genomes' sketches against the
+oracle (oracle/sks_oracle.cpp) on the same 5 Mb bytes; the whole 1000 x 1000
+count matrix against an independent host count of the exported sketches
+(sparse 0/1 membership product); symmetry and diagonal = sizes.
+
+Config 5: mask seeds 0..7 over the first 200 genomes, per seed all-vs-all and
+ANI (kmer-sketching.cpp:185-200), consensus = mean over seeds through
+sks_dist.seed_sweep like bench.py.  Checked: 2 genomes per seed against the
+oracle, each seed's matrix against the host count, and the consensus against a
+host recomputation of containment / ANI from the exported sketches (<= 1e-12).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+import sksffi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    import bench
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    ctx = sksffi.Context(0)
+    yield torch, bench, ctx
+    ctx.close()
+
+
+def _genomes(torch, bench, ctx, n):
+    L = bench.C4_LEN
+    seg = [0]
+    for _ in range(n):
+        seg.append(seg[-1] + L + 1)
+    buf = torch.empty(seg[-1], dtype=torch.uint8, device="cuda")
+    for g in range(n):
+        a, ms, r = bench.c4_genome_seeds(g)
+        ctx.synth_bases(buf.data_ptr() + seg[g], L, a, ms, r)
+        buf[seg[g] + L] = ord("\n")
+    torch.cuda.synchronize()
+    return buf, seg
+
+
+def _host_counts(sketches):
+    """|S_i ∩ S_j| for all pairs from sorted u64 arrays: 0/1 membership rows over
+    the union of values, multiplied (independent of every GPU kernel)."""
+    import scipy.sparse as sp
+    n = len(sketches)
+    allv = np.concatenate(sketches)
+    rows = np.repeat(np.arange(n), [len(s) for s in sketches])
+    _, inv = np.unique(allv, return_inverse=True)
+    M = sp.csr_matrix((np.ones(len(allv), np.int32), (rows, inv)), shape=(n, int(inv.max()) + 1))
+    return (M @ M.T).toarray().astype(np.int64)
+
+
+def _exported(ss, n):
+    return [ss.sketch(i)[:, 0].copy() for i in range(n)]
+
+
+def test_config4_all_vs_all_1000x5mb(env):
+    torch, bench, ctx = env
+    import sks_dist
+    n, s = bench.C4_GENOMES, bench.C4_S
+    buf, seg = _genomes(torch, bench, ctx, n)
+    mask = sksffi.mask_generate(bench.W, bench.K, bench.MASK_SEED)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, bench.W, mask, sksffi.SKS_BOTTOM_S, s)
+    sizes = ss.sizes().copy()
+    assert (sizes == s).all()  # every 5 Mb genome has > 10000 distinct k-mers
+    # sketches against the oracle on the same bytes: both ends of the family
+    # structure (rates 0 and 9.9 %) in several families
+    for g in (0, 1, 99, 100, 457, 501, 998, 999):
+        raw = buf[seg[g]:seg[g + 1]].cpu().numpy().tobytes()
+        want, nw = O.sketch(O.cut_runs(raw), bench.W, mask, "bottom", s)
+        assert np.array_equal(ss.sketch(g), want), g
+        assert int(ss.windows()[g]) == nw
+    # the bench's pair path, world 1
+    build, count = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda")
+    out = torch.full((n, n), -1, dtype=torch.int32, device="cuda")
+    mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), sksffi.join_layout_log_b,
+                                   sksffi.join_layout_capacity(), build, count, device="cuda", out=out)
+    torch.cuda.synchronize()
+    got = mat.cpu().numpy().astype(np.int64)
+    want = _host_counts(_exported(ss, n))
+    assert np.array_equal(got, got.T)
+    assert np.array_equal(np.diag(got), sizes.astype(np.int64))
+    assert np.array_equal(got, want)
+    # the family structure is real: related pairs share k-mers, unrelated ones do not
+    assert got[0, 1] > 0 and got[0, 50] > 0 and got[0, 999] < 50
+
+
+def test_config5_seed_sweep_8x200x5mb(env):
+    torch, bench, ctx = env
+    import sks_dist
+    n, s, seeds = bench.C5_GENOMES, bench.C4_S, bench.C5_SEEDS
+    buf, seg = _genomes(torch, bench, ctx, n)
+    padded = torch.full((n, s), -1, dtype=torch.int64, device="cuda")
+    psizes = torch.zeros(n, dtype=torch.int32, device="cuda")
+    starts = torch.arange(n, dtype=torch.int64, device="cuda") * s
+    T = sksffi.intersect_sym_tiles(n)
+    host_ani = []
+    checked = {0: (3, 150), 1: (0, 199), 2: (42, 77), 3: (100, 101), 4: (5, 6), 5: (120, 180),
+               6: (7, 190), 7: (60, 61)}
+
+    def ani_for_seed(k):
+        m = sksffi.mask_generate(bench.W, bench.K, k)
+        ones = bin(m).count("1") // 2
+        ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, bench.W, m, sksffi.SKS_BOTTOM_S, s)
+        for g in checked[k]:
+            raw = buf[seg[g]:seg[g + 1]].cpu().numpy().tobytes()
+            want, _ = O.sketch(O.cut_runs(raw), bench.W, m, "bottom", s)
+            assert np.array_equal(ss.sketch(g), want), (k, g)
+        ss.export(padded.data_ptr(), s, psizes.data_ptr())
+        mat = torch.empty((n, n), dtype=torch.int32, device="cuda")
+        ctx.intersect_sym(padded.data_ptr(), starts.data_ptr(), psizes.data_ptr(), 1, n, 0, T,
+                          mat.data_ptr())
+        torch.cuda.synchronize()
+        counts = mat.cpu().numpy()
+        sk = _exported(ss, n)
+        hc = _host_counts(sk)
+        assert np.array_equal(counts.astype(np.int64), hc), k
+        size_first = np.repeat(np.diag(counts).astype(np.int32), n)
+        _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones)
+        # host recomputation (kmer-sketching.cpp:195-200, ani_estimation.cpp:24-42)
+        sz = np.array([len(x) for x in sk], dtype=np.float64)
+        cont = hc / sz[:, None]
+        host_ani.append(np.where(cont > 0, np.power(cont, 1.0 / ones), 0.0))
+        return torch.from_numpy(ani.reshape(n, n))
+
+    cons, mine = sks_dist.seed_sweep(seeds, 1, 0, ani_for_seed, n, device="cpu")
+    assert mine == list(range(seeds))
+    want = sum(host_ani) / seeds
+    assert np.allclose(cons.numpy(), want, rtol=0, atol=1e-12)
+    c = cons.numpy()
+    assert np.allclose(np.diag(c), 1.0) and 0 < c[0, 1] < 1 and c[0, 150] < c[0, 1]

@@ -1,0 +1,96 @@
+"""Summaries of a round profile (tools/profile_round.sh) for profiles/<tag>/:
+  kernel_stats.csv          rocprofv3 --stats of the default bench command (trimmed)
+  scan_timed_launches.json  the config-3 scan dispatches bench.py times (its serial
+                            pass: dispatches [warmup, warmup + steps) of the kernel)
+                            from the kernel trace: durations, median, mean, and the
+                            bench line's own hipEvent kernel time of the same run
+  traffic.json              HBM bytes per timed launch from PMC: FETCH_SIZE x 2 (the
+                            gfx950 correction, MI355X_MICROARCH.md HBM) + WRITE_SIZE,
+                            KiB units, median over the same dispatch indices
+  scan_counters.txt / pair_counters.txt   SQ counter averages per kernel
+    python tools/summarize_round.py <round_dir> <dst> <warmup> <steps>"""
+import csv
+import glob
+import io
+import json
+import os
+import statistics
+import sys
+from contextlib import redirect_stdout
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pmc_by_kernel  # noqa: E402
+
+SCAN = "scan_kernel<0, 0, 1>"  # FracMinHash, flavour B, low-bits pre-filter (config 3)
+
+
+def _one(d, pattern):
+    f = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    return f[0] if f else None
+
+
+def _scan_dispatches(rows, key="Dispatch_Id"):
+    out = [r for r in rows if SCAN in r["Kernel_Name"]]
+    out.sort(key=lambda r: int(r[key]))
+    return out
+
+
+def _pmc_per_dispatch(path, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter and SCAN in r["Kernel_Name"]:
+            vals[int(r["Dispatch_Id"])] = vals.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def main(src, dst, warmup, steps):
+    os.makedirs(dst, exist_ok=True)
+    stats = _one(os.path.join(src, "trace"), "*kernel_stats.csv")
+    rows = list(csv.DictReader(open(stats)))
+    with open(os.path.join(dst, "kernel_stats.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+        for r in rows:
+            w.writerow([r["Name"][:160], r["Calls"], r["TotalDurationNs"], r["AverageNs"],
+                        r["Percentage"], r["MinNs"], r["MaxNs"]])
+    trace = list(csv.DictReader(open(_one(os.path.join(src, "trace"), "*kernel_trace.csv"))))
+    scans = _scan_dispatches(trace)
+    timed = scans[warmup:warmup + steps]
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
+    bench_ms = None
+    try:
+        line = [l for l in open(os.path.join(src, "bench_traced.json")) if l.startswith("{")][-1]
+        bench_ms = json.loads(line)["roofline"]["kernel_ms"]
+    except (OSError, IndexError, KeyError, ValueError):
+        pass
+    launches = {"kernel": SCAN, "dispatches_of_kernel": len(scans), "timed_indices": [warmup, warmup + steps],
+                "timed_ms": dur, "median_ms": statistics.median(dur), "mean_ms": statistics.mean(dur),
+                "bench_line_hipevent_kernel_ms": bench_ms,
+                "note": "rocprofv3 --kernel-trace of the default bench command; the timed launches "
+                        "are the serial pass (after --warmup), the ones bench.py's roofline uses"}
+    with open(os.path.join(dst, "scan_timed_launches.json"), "w") as f:
+        json.dump(launches, f, indent=1)
+    fetch = _pmc_per_dispatch(_one(os.path.join(src, "fetch"), "*counter_collection.csv"), "FETCH_SIZE")
+    write = _pmc_per_dispatch(_one(os.path.join(src, "write"), "*counter_collection.csv"), "WRITE_SIZE")
+    fetch_t, write_t = fetch[warmup:warmup + steps], write[warmup:warmup + steps]
+    fk, wk = statistics.median(fetch_t), statistics.median(write_t)
+    traffic = {"kernel": SCAN + " (config 3 step)", "timed_indices": [warmup, warmup + steps],
+               "fetch_size_kib_median": fk, "write_size_kib_median": wk,
+               "scan_hbm_bytes_per_launch": (2 * fk + wk) * 1024,
+               "correction": "FETCH_SIZE x 2 (gfx950 counts 128-B requests at 64 B, MI355X_MICROARCH.md HBM)",
+               "dispatches_seen": [len(fetch), len(write)]}
+    with open(os.path.join(dst, "traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
+    for sub, name, kernels in (("sq", "scan_counters.txt", ["scan_kernel"]),
+                               ("pairs", "pair_counters.txt", ["k_join", "k_bottom_fused", "k_hb_"])):
+        if os.path.isdir(os.path.join(src, sub)):
+            buf = io.StringIO()
+            with redirect_stdout(buf):
+                pmc_by_kernel.main(os.path.join(src, sub), kernels)
+            open(os.path.join(dst, name), "w").write(buf.getvalue())
+    print(json.dumps({"launches": {k: launches[k] for k in ("median_ms", "mean_ms", "bench_line_hipevent_kernel_ms")},
+                      "traffic": traffic["scan_hbm_bytes_per_launch"]}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
