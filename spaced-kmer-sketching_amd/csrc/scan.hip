@@ -43,7 +43,15 @@ constexpr int kTile = kBlock * kWPT;      // 4096 window starts per tile
 constexpr int kHaloWords = 4;             // 64 extra bases (>= w - 1 for w <= 64)
 constexpr int kWords = kBlock + kHaloWords;            // 2-bit words per tile (16 bases each)
 constexpr int kLoadVecs = (kWords * 16 + 16) / 16;      // 16-B loads per tile (+1 for alignment)
-constexpr int kQCap = 2048;               // LDS survivor queue entries
+constexpr int kQCap = 2048;               // LDS survivor queue entries (list mode, wide path)
+#ifndef SKS_SCAN_QCAP
+#define SKS_SCAN_QCAP 512
+#endif
+// FracMinHash keeps ~1/c of the windows and bottom-s ~s/L (a few per tile), so a
+// small queue suffices there and leaves LDS for more workgroups per CU; list
+// mode (every selected window, c = 1 keeps all) keeps the large one.
+template <int MODE>
+constexpr int qcap() { return MODE == kModeList ? kQCap : SKS_SCAN_QCAP; }
 constexpr unsigned char kSep = '\n';      // any non-ACGT byte
 
 struct Geom {
@@ -153,8 +161,8 @@ __device__ __forceinline__ uint32_t rev_pairs(uint32_t x) {
 
 template <int MODE>
 struct Queue {
-  uint64_t key[kQCap];
-  uint64_t val[MODE == kModeBottom ? kQCap : 1];
+  uint64_t key[qcap<MODE>()];
+  uint64_t val[MODE == kModeBottom ? qcap<MODE>() : 1];
   uint32_t n;
   unsigned long long base;
   unsigned long long wins;  // windows of the current segment not yet published
@@ -164,7 +172,7 @@ template <int MODE>
 __device__ __forceinline__ void emit(const ScanParams& p, Queue<MODE>& q, uint32_t seg,
                                      uint64_t key, uint64_t val) {
   uint32_t slot = atomicAdd(&q.n, 1u);
-  if (slot < kQCap) {
+  if (slot < (uint32_t)qcap<MODE>()) {
     q.key[slot] = key;
     if constexpr (MODE == kModeBottom) q.val[slot] = val;
   } else {  // queue full: rare direct path
@@ -186,7 +194,8 @@ __device__ __forceinline__ void flush(const ScanParams& p, Queue<MODE>& q, uint3
   // finish together and the segment's counter word serialises the atomics
   // (one word takes ~88 per microsecond, MI355X_MICROARCH.md "dequeue")
   if (threadIdx.x == 0 && q.wins) atomicAdd(&p.seg_windows[seg], q.wins);
-  uint32_t n = q.n < kQCap ? q.n : kQCap;
+  constexpr uint32_t cap = qcap<MODE>();
+  uint32_t n = q.n < cap ? q.n : cap;
   if (n) {
     if (threadIdx.x == 0) q.base = atomicAdd(&p.seg_count[seg], (unsigned long long)n);
     __syncthreads();
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
 
     // 5) flush the queue once it is half full
     __syncthreads();
-    if (q.n >= kQCap / 2) {
+    if (q.n >= (uint32_t)qcap<MODE>() / 2) {
       add_windows(q.wins, win_count);
       win_count = 0;
       flush<MODE>(p, q, g.seg);
