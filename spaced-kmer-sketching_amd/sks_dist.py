@@ -88,6 +88,32 @@ def all_vs_all(local, local_sizes, n_genomes, world, rank, count_sym, out=None):
     return out
 
 
+def row_shard(n, world, rank):
+    return rank * n // world, (rank + 1) * n // world
+
+
+def all_vs_all_rows(local, local_sizes, n_genomes, world, rank, count_rows):
+    """Row-block form of all_vs_all for sketches of any element width — (lo, hi)
+    k-mers for 32 < w <= 64, which the join / merge tiles do not take: the padded
+    sketches are all-gathered as in all_vs_all, rank r counts rows [r0, r1) against
+    every column with count_rows(sketches, sizes, n, r0, r1, out_rows) (the contract
+    of sks_intersect_all: out_rows[(i - r0) * n + j] = |S_i ∩ S_j|), and the row
+    blocks are all-gathered.  Returns the full n x n int32 matrix on every rank."""
+    src, src_sz = gather_sketches(local, local_sizes, world)
+    r0, r1 = row_shard(n_genomes, world, rank)
+    rows = torch.zeros((r1 - r0, n_genomes), dtype=torch.int32, device=local.device)
+    if r1 > r0:
+        count_rows(src, src_sz, n_genomes, r0, r1, rows)
+    if world == 1:
+        return rows
+    per = (n_genomes + world - 1) // world
+    pad = torch.zeros((per, n_genomes), dtype=torch.int32, device=local.device)
+    pad[: r1 - r0] = rows
+    g = _gather_flat(pad.reshape(-1), world).view(world, per, n_genomes)
+    return torch.cat([g[r, : row_shard(n_genomes, world, r)[1] - row_shard(n_genomes, world, r)[0]]
+                      for r in range(world)])
+
+
 # ---- seed sweep (BASELINE config 5) ----------------------------------------------------
 # The reference sweeps (w, k) configurations serially, re-sketching every file
 # per configuration (kmer-sketching.cpp:214-239 around :151-212).  Config 5 runs

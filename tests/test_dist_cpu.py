@@ -83,6 +83,67 @@ def test_all_vs_all_gloo_matches_single_process(world):
         assert np.array_equal(results[r], want)
 
 
+# ---- all-vs-all in row blocks, (lo, hi) k-mers (w > 32): sks_dist.all_vs_all_rows ------
+WIDE_N, WIDE_W, WIDE_K, WIDE_STRIDE = 45, 40, 30, 160
+
+
+def _wide_sketches():
+    m = O.mask(WIDE_W, WIDE_K, 0)
+    out = []
+    for g in range(WIDE_N):
+        seq = synth.bases(2500, seed=60 + g % 3, mut_seed=700 + g, mut_rate=0.004 * (g % 6))
+        sk, _ = O.sketch(O.cut_runs(seq.tobytes()), WIDE_W, m, "frac", 20)
+        out.append(sk)  # (k, 2) uint64 (lo, hi)
+    return out
+
+
+def _oracle_count_rows(src, sizes, n, r0, r1, out):
+    """count_rows contract (sks_intersect_all row blocks) on padded (lo, hi) rows."""
+    a = src.numpy().view(np.uint64).reshape(src.shape[0], -1, 2)
+    sz = sizes.numpy()
+    for i in range(r0, r1):
+        for j in range(n):
+            out[i - r0, j] = O.intersect(a[i, : sz[i]], a[j, : sz[j]])
+
+
+def _rows_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sk = _wide_sketches()
+    per, g0, g1 = sks_dist.genome_shard(WIDE_N, world, rank)
+    local = torch.full((per, 2 * WIDE_STRIDE), -1, dtype=torch.int64)
+    local_sz = torch.zeros(per, dtype=torch.int32)
+    for i, g in enumerate(range(g0, g1)):
+        assert len(sk[g]) <= WIDE_STRIDE
+        local[i, : 2 * len(sk[g])] = torch.from_numpy(sk[g].reshape(-1).view(np.int64))
+        local_sz[i] = len(sk[g])
+    mat = sks_dist.all_vs_all_rows(local, local_sz, WIDE_N, world, rank, _oracle_count_rows)
+    q.put((rank, mat.numpy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_vs_all_rows_wide_gloo(world):
+    """w = 40 (128-bit k-mers): padded (lo, hi) sketches gathered, each rank counts its
+    row block, row blocks gathered; every rank ends with the single-process matrix."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sk = _wide_sketches()
+    want = np.array([[O.intersect(sk[i], sk[j]) for j in range(WIDE_N)] for i in range(WIDE_N)])
+    assert want[0, 3] > 0  # related genomes share 128-bit k-mers
+    for r in range(world):
+        assert np.array_equal(results[r], want)
+
+
 def test_shard_arithmetic():
     for n in (1, 63, 64, 65, 1000):
         T = sks_dist.sym_tiles(n)

@@ -724,3 +724,34 @@ def test_join_large_sketches_300k(torch_cuda, ctx):
     ctx.intersect_all(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, n, out.data_ptr())
     torch.cuda.synchronize()
     check(out.cpu().numpy().reshape(n, n).astype(np.int64))
+
+
+def test_wide_all_vs_all_rows_path(torch_cuda, ctx):
+    """The multi-GPU row-block path for 128-bit k-mers (sks_dist.all_vs_all_rows at
+    world 1): exported fixed-stride (lo, hi) sketches, rows counted by
+    sks_intersect_all (one wavefront per pair), equal to the oracle's counts."""
+    torch = torch_cuda
+    import sks_dist
+    w, k, c, n = 45, 30, 15, 70
+    m = O.mask(w, k, 2)
+    genomes = [synth.bases(4000, seed=90 + i % 4, mut_seed=800 + i, mut_rate=0.003 * (i % 5)).tobytes()
+               for i in range(n)]
+    ss, _ = build(torch, ctx, genomes, w, m, "frac", c)
+    assert ss.elem_words == 2
+    sk = [O.sketch(O.cut_runs(g), w, m, "frac", c)[0] for g in genomes]
+    stride = max(len(x) for x in sk) + 3
+    padded = torch.full((n, 2 * stride), -1, dtype=torch.int64, device="cuda:0")
+    psz = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    ss.export(padded.data_ptr(), stride, psz.data_ptr())
+    torch.cuda.synchronize()
+    starts = torch.arange(n, dtype=torch.int64, device="cuda:0") * stride
+
+    def count_rows(src, sizes, nn, r0, r1, out):
+        ctx.intersect_all(src.data_ptr(), starts.data_ptr(), sizes.data_ptr(), 2, nn, r0, r1,
+                          out.data_ptr())
+        torch.cuda.synchronize()
+
+    got = sks_dist.all_vs_all_rows(padded, psz, n, 1, 0, count_rows).cpu().numpy()
+    want = np.array([[O.intersect(sk[i], sk[j]) for j in range(n)] for i in range(n)])
+    assert want[0, 4] > 0
+    assert np.array_equal(got, want)
