@@ -425,7 +425,16 @@ __global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ da
   const uint64_t* src = data + starts[i];
   for (uint32_t b = threadIdx.x; b < B; b += kB) h[b] = 0;
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < sz; e += kB) atomicAdd(&h[bucket_hash(src[e], log_b)], 1u);
+  // four loads in flight per thread before their histogram atomics
+  uint32_t e = threadIdx.x;
+  for (; e + 3 * kB < sz; e += 4 * kB) {
+    uint64_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[e + u * kB];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) atomicAdd(&h[bucket_hash(v[u], log_b)], 1u);
+  }
+  for (; e < sz; e += kB) atomicAdd(&h[bucket_hash(src[e], log_b)], 1u);
   __syncthreads();
   uint32_t* dst = counts + (uint64_t)(i - base) * B;  // (blk * 64 + slot) * B
   for (uint32_t b = threadIdx.x; b < B; b += kB) dst[b] = h[b];
@@ -513,11 +522,19 @@ __global__ __launch_bounds__(kB) void k_hb_stage(const uint64_t* __restrict__ da
   const uint32_t* o = goff + (uint64_t)(i - base) * G;
   for (uint32_t g = threadIdx.x; g < G; g += kB) cur[g] = o[g];
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < sz; e += kB) {
-    const uint64_t v = src[e];
-    const uint32_t g = bucket_hash(v, log_b) >> (log_b - log_g);
-    stage[atomicAdd(&cur[g], 1u)] = v;
+  auto put = [&](uint64_t v) {
+    stage[atomicAdd(&cur[bucket_hash(v, log_b) >> (log_b - log_g)], 1u)] = v;
+  };
+  // four loads in flight per thread before their cursor atomics
+  uint32_t e = threadIdx.x;
+  for (; e + 3 * kB < sz; e += 4 * kB) {
+    uint64_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[e + u * kB];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) put(v[u]);
   }
+  for (; e < sz; e += kB) put(src[e]);
 }
 
 // Phase 2: one workgroup per (block, coarse group) places the group's
@@ -540,16 +557,28 @@ __global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ st
     cur[slot * 64 + bl] = off[rowb + (uint64_t)slot * B + bl];
   }
   __syncthreads();
+  // a wave per slot run; each lane loads its (up to) four elements of the run
+  // before placing any, so a run of <= 256 elements is one round of loads (one
+  // dependent load per lane and iteration before: 119 us for config 4)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (uint32_t slot = wave; slot < 64; slot += kB / 64) {
     const uint64_t gi = ((uint64_t)blk * 64 + slot) * G + g;
     const uint32_t s0 = goff[gi], n = gcounts[gi];
-    for (uint32_t e = lane; e < n; e += 64) {
-      const uint64_t v = stage[s0 + e];
-      const uint32_t bl = bucket_hash(v, log_b) - g * bpg;
-      const uint32_t d = atomicAdd(&cur[slot * 64 + bl], 1u);
-      out[d] = v;
-      ids[d] = (uint8_t)slot;
+    for (uint32_t e0 = 0; e0 < n; e0 += 256) {
+      uint64_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t e = e0 + lane + 64 * u;
+        v[u] = e < n ? stage[s0 + e] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (e0 + lane + 64 * u >= n) continue;
+        const uint32_t bl = bucket_hash(v[u], log_b) - g * bpg;
+        const uint32_t d = atomicAdd(&cur[slot * 64 + bl], 1u);
+        out[d] = v[u];
+        ids[d] = (uint8_t)slot;
+      }
     }
   }
 }
