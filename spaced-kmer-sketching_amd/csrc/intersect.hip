@@ -380,9 +380,6 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 // workgroup streams the column block in coalesced chunks of whole buckets
 // that fit the table (<= kJCap elements; a larger bucket is cut into
 // sub-chunks) and the row block's same buckets with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
-#ifndef SKS_JOIN_LOG_SLOTS
-#define SKS_JOIN_LOG_SLOTS 11
-#endif
 #ifndef SKS_JOIN_DIAG  // diagnostics only (wrong counts): 1 no probes / hit adds,
 #define SKS_JOIN_DIAG 0  // 2 no count flush
 #endif
@@ -392,22 +389,23 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 #ifndef SKS_JOIN_THREADS
 #define SKS_JOIN_THREADS 512
 #endif
+// 4096 table slots for <= 1024 column elements per chunk (load <= 1/4; 2048
+// slots at load <= 1/2 measured slower: longer probe chains)
+#ifndef SKS_JOIN_LOG_SLOTS
+#define SKS_JOIN_LOG_SLOTS 12
+#endif
 constexpr int kJB = SKS_JOIN_THREADS;       // threads per k_join workgroup
-constexpr int kJLog = SKS_JOIN_LOG_SLOTS;
-constexpr int kJSlots = 1 << kJLog;          // hash slots
-constexpr int kJCap = kJSlots / 2;          // column elements per chunk (load <= 1/2)
+constexpr int kFLog = SKS_JOIN_LOG_SLOTS;
+constexpr int kFSlots = 1 << kFLog;          // 32-bit table slots
+constexpr int kJCap = 1024;                  // column elements per chunk
 constexpr int kJMade = kJCap / kJB;         // column elements per thread per chunk
 constexpr int kJWin = 256;                  // bucket offsets staged per window
 constexpr uint32_t kJMaxLogB = 14;          // B <= 16384 (LDS histogram of k_hb_count)
 constexpr int kCntLd = kTile + 1;
-constexpr uint64_t kEmpty = ~0ull;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t bucket_hash(uint64_t v, uint32_t log_b) {
   return log_b ? (uint32_t)((v * 0x9E3779B97F4A7C15ull) >> (64 - log_b)) : 0u;
-}
-__device__ __forceinline__ uint32_t join_hash(uint64_t v) {
-  return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x85EBCA77u) >> (32 - kJLog);
 }
 
 // One workgroup per sketch i in [first, first + count): per-bucket element
@@ -592,11 +590,11 @@ struct JoinArgs {
   uint64_t tile_begin;
   int32_t* out;
   uint64_t ld;
-  uint32_t cap;  // column elements per chunk (<= kJCap): table load <= cap / kJSlots
+  uint32_t cap;  // column elements per chunk (<= kJCap): table load <= cap / kFSlots
 };
 
-// Elements of one chunk held in registers: column elements k = cs + tid + 256u
-// (u < kJMade: a chunk holds <= kJCap) and the first kJRowPf * 256 row elements;
+// Elements of one chunk held in registers: column elements k = cs + tid + kJB * u
+// (u < kJMade: a chunk holds <= kJCap) and the first kJRowPf * kJB row elements;
 // the rest of a (rare) larger row range is read in the probe loop.
 constexpr int kJRowPf = 1536 / kJB;
 // s_waitcnt immediate for gfx9 "vmcnt(0)" with expcnt / lgkmcnt left at their
@@ -641,21 +639,37 @@ __device__ unsigned long long g_join_stamps[8];
 #define JSTAMP(i) do {} while (0)
 #endif
 
+// ---- k_join: the join kernel ----------------------------------------------------------------
+//
+// Each chunk's column elements are first staged as entries {value, column
+// bit} in LDS (plain stores); the hash table then holds 32-bit slots
+// (fingerprint << 10 | entry index).  An insert is one 32-bit compare-swap
+// (the 64-bit one runs at about half its rate) and, for a value already present,
+// a check of the entry it names plus an OR of the column bit into that entry;
+// a probe reads 32-bit slots and, on a fingerprint match, the 16-byte entry.
+// Values need no reserved "empty" key (the empty marker lives in the slot), and
+// the entries need no reset: the next chunk's staging overwrites them.
+constexpr uint32_t kFFree = 0xFFFFFFFFu;
+static_assert(kJCap <= 1024, "entry index must fit 10 bits");
+
+__device__ __forceinline__ uint32_t fp_slot(uint64_t v) {
+  return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x85EBCA77u) >> (32 - kFLog);
+}
+__device__ __forceinline__ uint32_t fp_tag(uint64_t v) {  // 22 bits, never all ones
+  const uint32_t t = (uint32_t)((v * 0xD6E8FEB86659FD93ull) >> 42);
+  return t == 0x3FFFFFu ? 0x3FFFFEu : t;
+}
+
 __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
 #ifdef SKS_JOIN_STAMPS
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
-  // slot h = {key, mask of columns}: one ds_read_b128 per probe step
-  // slot h: key s_key[h], mask of the columns holding it s_msk[h]. Probes read
-  // the 8-byte key only (half the LDS banks of a 16-byte slot under random
-  // access) and fetch the mask on a hit.
-  __shared__ unsigned long long s_key[kJSlots];
-  __shared__ unsigned long long s_msk[kJSlots];
+  __shared__ uint32_t s_slot[kFSlots];
+  __shared__ ulonglong2 s_ent[kJCap];  // {value, mask of the columns holding it}
   __shared__ uint32_t s_cnt[kTile * kCntLd];
   __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
-  __shared__ uint16_t s_next[kJWin];       // greedy chunk end of a chunk starting at bucket b
-  __shared__ unsigned long long s_special;  // columns holding the value ~0 (== kEmpty)
+  __shared__ uint16_t s_next[kJWin];
 
   const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
   const uint32_t grp = blockIdx.x % a.n_groups;
@@ -678,17 +692,11 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   const uint8_t* cids = a.c.ids + cb;
   const uint32_t* roff = a.r.boff + (uint64_t)rblk * (a.B + 1);
   const uint32_t* coff = a.c.boff + (uint64_t)J * (a.B + 1);
-  const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);  // slots < r_valid are rows
+  const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);
 
-  for (int i = tid; i < kJSlots; i += kJB) {
-    s_key[i] = kEmpty;
-    s_msk[i] = 0ull;
-  }
+  for (int i = tid; i < kFSlots; i += kJB) s_slot[i] = kFFree;
   for (int i = tid; i < kTile * kCntLd; i += kJB) s_cnt[i] = 0;
-  if (tid == 0) s_special = 0;
 
-  // a row element's bit loop starts at column `lane`: lanes holding the same
-  // row with similar masks then add to different counters
   auto add_hits = [&](uint32_t r, unsigned long long m) {
     m = (m >> lane) | (lane ? m << (64 - lane) : 0ull);
     uint32_t* crow = &s_cnt[r * kCntLd];
@@ -698,6 +706,23 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       atomicAdd(&crow[c], 1u);
     }
   };
+  // columns holding v (0 if none)
+  auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
+    const uint32_t tag = fp_tag(v);
+    for (;;) {
+      if (x == kFFree) return 0ull;
+      if ((x >> 10) == tag) {
+        const ulonglong2 e = s_ent[x & 1023u];
+        if (e.x == v) return e.y;
+      }
+      h = (h + 1) & (kFSlots - 1);
+      x = s_slot[h];
+    }
+  };
+
+  uint32_t made[kJMade];  // slots this thread created in the current chunk
+#pragma unroll
+  for (int u = 0; u < kJMade; ++u) made[u] = kNoSlot;
 
   const uint32_t b0 = grp * a.buckets_per_group;
   const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
@@ -709,12 +734,9 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       s_coff[i] = coff[wb + i];
     }
     __syncthreads();
-    // chunk = whole buckets [bs, be) whose column elements fit the table: the
-    // largest be with coff[be] - coff[bs] <= cap (at least bs + 1), found
-    // for every start bucket at once by binary search
     for (uint32_t i = tid; i < we - wb; i += kJB) {
       const uint32_t cs = s_coff[i];
-      uint32_t lo = i + 1, hi = we - wb;  // answer in [lo, hi]
+      uint32_t lo = i + 1, hi = we - wb;
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (s_coff[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
@@ -722,13 +744,8 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       s_next[i] = (uint16_t)lo;
     }
     __syncthreads();
-    // A chunk is buckets [bs, be) with column elements [cs, ce).  A single
-    // bucket holding more than cap column elements (sketches far larger than the
-    // bucket count was sized for, or hash skew) is cut into sub-chunks of cap
-    // column elements, each joined against ALL of the bucket's row elements: a
-    // value's columns may then sit in two sub-chunks, and each contributes its
-    // own columns' hits, so the counts stay exact for any population.
     JSTAMP(0);
+    // chunks and oversized-bucket sub-chunks exactly as in k_join
     auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
     uint32_t bs = wb, be = chunk_end(wb);
     uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
@@ -736,16 +753,9 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
     join_fetch(cdata, cids, rdata, rids, cs, ce, s_roff[0], s_roff[be - wb], tid, cur);
     while (bs < we) {
       const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
-      // This chunk's elements (prefetched during the previous chunk) have
-      // landed: say so before the next prefetch is issued.  Without it the
-      // compiler's wait for `cur` (merged with the first chunk's loads at the
-      // loop head) was a vmcnt(1) placed after the new prefetch, i.e. every
-      // chunk waited for the NEXT chunk's loads before its first insert
-      // (config 4: 53k of 117k cycles per workgroup in the insert phase).
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-      // prefetch the next chunk's elements while this one is joined
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // this chunk's elements have landed
       uint32_t nbs, nbe, ncs, nce;
-      if (ce < s_coff[be - wb]) {  // rest of an oversized bucket
+      if (ce < s_coff[be - wb]) {
         nbs = bs;
         nbe = be;
         ncs = ce;
@@ -759,66 +769,66 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       if (nbs < we)
         join_fetch(cdata, cids, rdata, rids, ncs, nce, s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
 
-      // 1) insert the column elements: every first CAS in flight together,
-      //    then the collisions walk on
-      uint32_t hs[kJMade];
-      unsigned long long prev[kJMade];
+      // 0) free the previous chunk's slots (its probes are done: barrier below
+      //    the probe loop) and stage this chunk's entries
+#pragma unroll
+      for (int u = 0; u < kJMade; ++u) {
+        if (made[u] != kNoSlot) s_slot[made[u]] = kFFree;
+        made[u] = kNoSlot;
+        const uint32_t e = tid + kJB * u;
+        if (cs + e < ce) s_ent[e] = make_ulonglong2(cur.cv[u], 1ull << cur.cid[u]);
+      }
+      __syncthreads();
+      // 1) insert: one 32-bit compare-swap per element; a value already
+      //    present adds its column bit to the entry the slot names
+      uint32_t hs[kJMade], prev[kJMade], tags[kJMade];
 #pragma unroll
       for (int u = 0; u < kJMade; ++u) {
         hs[u] = kNoSlot;
-        if (cs + tid + kJB * u < ce) {
-          const uint64_t v = cur.cv[u];
-          if (v == kEmpty) {
-            atomicOr(&s_special, 1ull << cur.cid[u]);
-          } else {
-            hs[u] = join_hash(v);
-            prev[u] = atomicCAS(&s_key[hs[u]], (unsigned long long)kEmpty, (unsigned long long)v);
-          }
+        const uint32_t e = tid + kJB * u;
+        if (cs + e < ce) {
+          hs[u] = fp_slot(cur.cv[u]);
+          tags[u] = fp_tag(cur.cv[u]);
+          prev[u] = atomicCAS(&s_slot[hs[u]], kFFree, (tags[u] << 10) | e);
         }
       }
-      uint32_t made[kJMade];
 #pragma unroll
       for (int u = 0; u < kJMade; ++u) {
-        made[u] = kNoSlot;
-        if (hs[u] != kNoSlot) {
-          const uint64_t v = cur.cv[u];
-          uint32_t h = hs[u];
-          unsigned long long p = prev[u];
-          while (p != kEmpty && p != v) {
-            h = (h + 1) & (kJSlots - 1);
-            p = atomicCAS(&s_key[h], (unsigned long long)kEmpty, (unsigned long long)v);
+        if (hs[u] == kNoSlot) continue;
+        const uint64_t v = cur.cv[u];
+        const uint32_t e = tid + kJB * u;
+        uint32_t h = hs[u], x = prev[u];
+        for (;;) {
+          if (x == kFFree) {
+            made[u] = h;
+            break;
           }
-          if (p == kEmpty) made[u] = h;
-          atomicOr(&s_msk[h], 1ull << cur.cid[u]);
+          if ((x >> 10) == tags[u] && s_ent[x & 1023u].x == v) {
+            atomicOr(&s_ent[x & 1023u].y, 1ull << cur.cid[u]);
+            break;
+          }
+          h = (h + 1) & (kFSlots - 1);
+          x = atomicCAS(&s_slot[h], kFFree, (tags[u] << 10) | e);
         }
       }
       __syncthreads();
       JSTAMP(1);
       // 2) probe with the row elements: first slots read together
-      const unsigned long long special = s_special;
-      unsigned long long sl[kJRowPf];
+      uint32_t sl[kJRowPf], sh[kJRowPf];
 #pragma unroll
       for (int u = 0; u < kJRowPf; ++u) {
-        sl[u] = kEmpty;
-        if (cur.rid[u] < r_valid && cur.rv[u] != kEmpty) sl[u] = s_key[join_hash(cur.rv[u])];
+        sl[u] = kFFree;
+        sh[u] = 0;
+        if (cur.rid[u] < r_valid) {
+          sh[u] = fp_slot(cur.rv[u]);
+          sl[u] = s_slot[sh[u]];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kJRowPf; ++u) {
         const uint32_t r = cur.rid[u];
         if (r >= r_valid) continue;
-        const uint64_t v = cur.rv[u];
-        unsigned long long m;
-        if (v == kEmpty) {
-          m = special;
-        } else {
-          unsigned long long x = sl[u];
-          uint32_t h = join_hash(v);
-          while (x != v && x != kEmpty) {
-            h = (h + 1) & (kJSlots - 1);
-            x = s_key[h];
-          }
-          m = x == v ? s_msk[h] : 0ull;
-        }
+        const unsigned long long m = lookup(cur.rv[u], sh[u], sl[u]);
         if (SKS_JOIN_DIAG & 1) continue;
         if (m) add_hits(r, m);
       }
@@ -826,32 +836,12 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
         const uint32_t r = rids[k];
         if (r >= r_valid) continue;
         const uint64_t v = rdata[k];
-        unsigned long long m = 0;
-        if (v == kEmpty) {
-          m = special;
-        } else {
-          uint32_t h = join_hash(v);
-          unsigned long long x = s_key[h];
-          while (x != v && x != kEmpty) {
-            h = (h + 1) & (kJSlots - 1);
-            x = s_key[h];
-          }
-          m = x == v ? s_msk[h] : 0ull;
-        }
+        const uint32_t h = fp_slot(v);
+        const unsigned long long m = lookup(v, h, s_slot[h]);
         if (m) add_hits(r, m);
       }
       __syncthreads();
       JSTAMP(2);
-      // 3) reset the slots this thread created (and the ~0 mask)
-#pragma unroll
-      for (int u = 0; u < kJMade; ++u)
-        if (made[u] != kNoSlot) {
-          s_key[made[u]] = kEmpty;
-          s_msk[made[u]] = 0ull;
-        }
-      if (tid == 0) s_special = 0;
-      __syncthreads();
-      JSTAMP(3);
       cur = nxt;
       bs = nbs;
       be = nbe;
@@ -862,7 +852,6 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   __syncthreads();
   JSTAMP(5);
   if (SKS_JOIN_DIAG & 2) return;
-  // counts -> global (one atomic per nonzero pair; both halves for sym off-diagonal)
   for (int i = tid; i < kTile * kTile; i += kJB) {
     const uint32_t r = i >> 6, c = i & 63;
     const uint32_t cnt = s_cnt[r * kCntLd + c];
