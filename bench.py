@@ -652,7 +652,8 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
                    "genome_len": C4_LEN, "s": C4_S, "w": W, "k": K,
                    "pair_sharding": "block-aligned genomes per rank; upper-triangle 64x64 "
                                     "join tiles split over ranks",
-                   "collective": ("all_gather_into_tensor join layouts + all_reduce counts (RCCL)"
+                   "collective": ("all_gather_into_tensor join layouts + all_reduce counts "
+                                  + ("(RCCL)" if dev == "cuda" else "(gloo, via host)")
                                   if world > 1 else "none")},
         "cpu_baseline": cpu,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
