@@ -538,8 +538,12 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   MetaArena arena(c);
   size_t o_src = arena.add(src_off), o_csr = arena.add(csr), o_uniq = arena.add_zero(k);
   // narrow bottom-s with every genome's candidates in one workgroup's registers:
-  // sort, unique and select per genome in one kernel (post.hip k_bottom_fused)
-  const bool fused = bottom && !S.wide && max_len <= sks::bottom_fused_capacity() &&
+  // sort, unique and select per genome in one kernel (post.hip k_bottom_fused).
+  // A single genome goes the device-wide way instead: one workgroup sorting its
+  // ~1.1 s candidates alone takes longer than the multi-workgroup radix sort
+  // (config 2: 0.35 vs 0.30 ms per build; from two genomes on the fused kernel
+  // wins, tools/ab_c2.sh)
+  const bool fused = bottom && !S.wide && max_len <= sks::bottom_fused_capacity() && k >= 2 &&
                      getenv("SKS_NO_FUSED_BOTTOM") == nullptr;
   std::vector<uint64_t> f_retry, f_pad(1, 0);
   size_t o_cnt = 0, o_retry = 0, o_pad = 0, o_res = 0;

@@ -287,6 +287,85 @@ __device__ __forceinline__ uint32_t block_rank(bool p, uint32_t* wsum, uint32_t*
   return before + in_wave;
 }
 
+// Block-wide maximum of one value per thread (wsum64: kSelWaves words).
+__device__ __forceinline__ uint64_t block_max(uint64_t v, uint64_t* wsum64) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  if ((threadIdx.x & 63) == 0) wsum64[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t m = 0;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) m = wsum64[w] > m ? wsum64[w] : m;
+  __syncthreads();
+  return m;
+}
+
+// Radix select (8-bit digits, most significant first) of the kk-th smallest
+// (1-based) of the values f[i], i < n, with valid(i).  Starts at the digit of
+// vmax's top bit (the candidates' fmh are below the scan's threshold, so the
+// digits above it are zero) and stops as soon as the chosen digit's bucket is
+// kept whole (kk equals its population) — with 64-bit hashes two or three
+// digits instead of eight.  The kept values are those with
+// (v & pmask) < prefix, plus, with (v & pmask) == prefix, all of them (whole)
+// or the first kk in index order.
+struct RadixSel {
+  uint64_t prefix, pmask;
+  uint32_t kk;
+  bool whole;
+};
+template <class Valid>
+__device__ __forceinline__ RadixSel radix_select(const uint64_t* f, uint32_t n, uint32_t kk,
+                                                 uint64_t vmax, Valid valid, uint32_t* hist,
+                                                 uint32_t* s_sel) {
+  const int tid = threadIdx.x;
+  RadixSel r{0, 0, kk, false};
+  const int top = vmax ? 63 - __builtin_clzll(vmax) : 0;
+  for (int shift = (top / 8) * 8; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kSelB) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kSelB) {
+      const uint64_t v = f[i];
+      if (valid(i) && (v & r.pmask) == r.prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: the digit where the running count reaches kk
+      uint32_t h4[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { h4[q] = hist[4 * tid + q]; sum += h4[q]; }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += t;
+      }
+      const uint64_t bal = __ballot(incl >= r.kk);
+      const int L = __builtin_ctzll(bal);
+      if (tid == L) {
+        uint32_t c = incl - sum;
+        int q = 0;
+        while (c + h4[q] < r.kk) c += h4[q++];
+        s_sel[0] = 4 * L + q;  // digit
+        s_sel[1] = c;          // valid values below it
+        s_sel[2] = h4[q];      // its population
+      }
+    }
+    __syncthreads();
+    r.prefix |= (uint64_t)s_sel[0] << shift;
+    r.pmask |= 255ull << shift;
+    r.kk -= s_sel[1];
+    const bool whole = r.kk == s_sel[2];
+    __syncthreads();
+    if (whole) {
+      r.whole = true;
+      break;
+    }
+  }
+  return r;
+}
+
 template <int FLAVOUR>
 __global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restrict__ uk,
                                                          const uint64_t* __restrict__ uoff,
@@ -297,7 +376,8 @@ __global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restr
   extern __shared__ uint64_t f[];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t wsum[kSelWaves];
-  __shared__ uint32_t s_digit, s_below;
+  __shared__ uint64_t wsum64[kSelWaves];
+  __shared__ uint32_t s_sel[3];
   const uint32_t g = blockIdx.x;
   const uint64_t b = uoff[g], n = uoff[g + 1] - b;
   const uint64_t lim = limit[g];
@@ -308,52 +388,24 @@ __global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restr
     for (uint64_t i = tid; i < n; i += kSelB) dst[i] = uk[b + i];
     return;
   }
-  for (uint64_t i = tid; i < n; i += kSelB) f[i] = hash_bitset128<FLAVOUR>(uk[b + i], 0) ^ kconst;
-  uint64_t prefix = 0, pmask = 0;
-  uint32_t k = (uint32_t)lim;  // rank (1-based) of the wanted fmh among the prefix matches
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 256; i += kSelB) hist[i] = 0;
-    __syncthreads();
-    for (uint64_t i = tid; i < n; i += kSelB) {
-      const uint64_t v = f[i];
-      if ((v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    if (tid < 64) {  // wave 0: the digit where the running count reaches k
-      uint32_t h4[4], sum = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) { h4[q] = hist[4 * tid + q]; sum += h4[q]; }
-      uint32_t incl = sum;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (tid >= o) incl += t;
-      }
-      const uint64_t bal = __ballot(incl >= k);
-      const int L = __builtin_ctzll(bal);
-      if (tid == L) {
-        uint32_t c = incl - sum;
-        int q = 0;
-        while (c + h4[q] < k) c += h4[q++];
-        s_digit = 4 * L + q;
-        s_below = c;
-      }
-    }
-    __syncthreads();
-    prefix |= (uint64_t)s_digit << shift;
-    pmask |= 255ull << shift;
-    k -= s_below;
-    __syncthreads();
+  uint64_t mx = 0;
+  for (uint64_t i = tid; i < n; i += kSelB) {
+    const uint64_t v = hash_bitset128<FLAVOUR>(uk[b + i], 0) ^ kconst;
+    f[i] = v;
+    mx = v > mx ? v : mx;
   }
-  // prefix = F*; keep fmh < F* and the first k with fmh == F*, in k-mer order
+  mx = block_max(mx, wsum64);  // its barriers also publish f[]
+  const RadixSel sel = radix_select(f, (uint32_t)n, (uint32_t)lim, mx, [](uint32_t) { return true; },
+                                    hist, s_sel);
+  // keep the selected values in k-mer order
   uint32_t eq_base = 0, out_base = 0;
   for (uint64_t base = 0; base < n; base += kSelB) {
     const uint64_t i = base + tid;
-    const uint64_t v = i < n ? f[i] : ~0ull;
-    const bool eq = i < n && v == prefix;
+    const uint64_t v = i < n ? f[i] & sel.pmask : ~0ull;
+    const bool eq = i < n && !sel.whole && v == sel.prefix;
     uint32_t eq_tot, keep_tot;
     const uint32_t eq_rank = eq_base + block_rank(eq, wsum, &eq_tot);
-    const bool keep = i < n && (v < prefix || (eq && eq_rank < k));
+    const bool keep = i < n && (v < sel.prefix || (v == sel.prefix && (sel.whole || eq_rank < sel.kk)));
     const uint32_t pos = out_base + block_rank(keep, wsum, &keep_tot);
     if (keep) dst[pos] = uk[b + i];
     eq_base += eq_tot;
@@ -409,7 +461,8 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   __shared__ unsigned long long s_last[kSelB];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t wsum[kSelWaves];
-  __shared__ uint32_t s_digit, s_below;
+  __shared__ uint64_t wsum64[kSelWaves];
+  __shared__ uint32_t s_sel[3];
   const uint32_t g = blockIdx.x;
   const int tid = threadIdx.x;
   const uint64_t base = src_off[g];
@@ -468,56 +521,26 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   if (tid == 0) res[g] = lim;
   uint64_t* dst = out + dst_off[g];
   auto valid_at = [&](uint32_t i) { return i < n && !((dup[i >> 5] >> (i & 31)) & 1u); };
-  uint64_t prefix = 0;
-  uint32_t kk = (uint32_t)lim;
   const bool all = distinct <= lim;
+  RadixSel sel{0, 0, 0, true};
   if (!all) {
-    uint64_t pmask = 0;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-      for (int i = tid; i < 256; i += kSelB) hist[i] = 0;
-      __syncthreads();
-      for (uint32_t i = tid; i < n; i += kSelB) {
-        const uint64_t v = f[i];
-        if (valid_at(i) && (v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
-      }
-      __syncthreads();
-      if (tid < 64) {  // wave 0: the digit where the running count reaches kk
-        uint32_t h4[4], sum = 0;
+    uint64_t mx = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { h4[q] = hist[4 * tid + q]; sum += h4[q]; }
-        uint32_t incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t t = __shfl_up(incl, o, 64);
-          if (tid >= o) incl += t;
-        }
-        const uint64_t bal = __ballot(incl >= kk);
-        const int L = __builtin_ctzll(bal);
-        if (tid == L) {
-          uint32_t c = incl - sum;
-          int q = 0;
-          while (c + h4[q] < kk) c += h4[q++];
-          s_digit = 4 * L + q;
-          s_below = c;
-        }
-      }
-      __syncthreads();
-      prefix |= (uint64_t)s_digit << shift;
-      pmask |= 255ull << shift;
-      kk -= s_below;
-      __syncthreads();
-    }
+    for (uint32_t j = 0; j < ITEMS; ++j) mx = fv[j] > mx ? fv[j] : mx;  // 0 for non-distinct
+    mx = block_max(mx, wsum64);
+    sel = radix_select(f, n, (uint32_t)lim, mx, valid_at, hist, s_sel);
   }
-  // keep (all distinct) or (fmh < F*, and the first kk with fmh == F*), in k-mer order
+  // keep (all distinct) or the selected ones, in k-mer order
   uint32_t eq_base = 0, out_base = 0;
   for (uint32_t b0 = 0; b0 < n; b0 += kSelB) {
     const uint32_t i = b0 + tid;
     const bool ok = valid_at(i);
-    const uint64_t v = ok ? f[i] : ~0ull;
-    const bool eq = ok && !all && v == prefix;
+    const uint64_t v = ok ? f[i] & sel.pmask : ~0ull;
+    const bool eq = ok && !all && !sel.whole && v == sel.prefix;
     uint32_t eq_tot, keep_tot;
     const uint32_t eq_rank = eq_base + block_rank(eq, wsum, &eq_tot);
-    const bool keep = ok && (all || v < prefix || (eq && eq_rank < kk));
+    const bool keep =
+        ok && (all || v < sel.prefix || (v == sel.prefix && (sel.whole || eq_rank < sel.kk)));
     const uint32_t pos = out_base + block_rank(keep, wsum, &keep_tot);
     if (keep) dst[pos] = runs_expand(rec[base + i], runs);
     eq_base += eq_tot;

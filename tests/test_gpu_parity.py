@@ -161,9 +161,11 @@ def test_bottom_s_many_genomes(torch_cuda, ctx):
 
 
 def test_bottom_s_unfused_paths(torch_cuda, ctx, monkeypatch):
-    """The per-genome fused post kernel is the default for genomes of <= 16384
-    candidates; SKS_NO_FUSED_BOTTOM routes them through compaction + segmented
-    sort + unique + k_bottom_select instead. Both must give the oracle's sets."""
+    """The per-genome fused post kernel is the default for builds of two or more
+    genomes of <= 16384 candidates (a single genome takes the device-wide path);
+    SKS_NO_FUSED_BOTTOM routes them through compaction + segmented sort + unique
+    + k_bottom_select instead. Both must give the oracle's sets; both selects
+    stop their radix passes early once the chosen digit's bucket is kept whole."""
     genomes = [synth.bases(3000 + 997 * i, seed=1300 + i % 3, mut_seed=1400 + i,
                            mut_rate=0.02 * (i % 4)).tobytes() for i in range(40)]
     m = O.mask(31, 21, 5)
