@@ -59,13 +59,84 @@ hipError_t pinned_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
   return hipSuccess;
 }
 
+// Host -> device copies of small metadata go through a per-thread pinned ring
+// and do not wait: the bytes are copied into the ring at once (the caller's
+// buffer may go away), the DMA is queued on `s`, and an event marks when that
+// part of the ring may be rewritten.  A build used to synchronise its stream
+// after every metadata upload (a dozen round trips for one 5 Mb genome).
+namespace {
+struct RingUse {
+  size_t off, len;
+  int device;
+  hipEvent_t ev;
+};
+struct PinnedRing {
+  char* p = nullptr;
+  size_t bytes = 0, head = 0;
+  std::vector<RingUse> pending;
+  std::vector<std::pair<int, hipEvent_t>> spare;  // (device, event) ready for reuse
+};
+thread_local PinnedRing t_ring;  // never freed (see t_stage)
+
+void ring_retire(PinnedRing& R, size_t i) {
+  R.spare.emplace_back(R.pending[i].device, R.pending[i].ev);
+  R.pending.erase(R.pending.begin() + (std::ptrdiff_t)i);
+}
+}  // namespace
+
 hipError_t pinned_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return hipSuccess;
+  PinnedRing& R = t_ring;
   hipError_t e;
-  if ((e = stage_reserve(bytes)) != hipSuccess) return e;
-  std::memcpy(t_stage.p, src, bytes);
-  if ((e = hipMemcpyAsync(dst, t_stage.p, bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-  return hipStreamSynchronize(s);  // the stage is reused by the next copy
+  int dev = 0;
+  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+  const size_t need = (bytes + 255) & ~size_t(255);
+  // completed copies free their part of the ring
+  for (size_t i = 0; i < R.pending.size();) {
+    if (hipEventQuery(R.pending[i].ev) == hipSuccess) {
+      ring_retire(R, i);
+    } else {
+      (void)hipGetLastError();  // hipErrorNotReady is not an error here
+      ++i;
+    }
+  }
+  if (need > R.bytes) {  // grow: drain, then reallocate
+    for (const RingUse& u : R.pending)
+      if ((e = hipEventSynchronize(u.ev)) != hipSuccess) return e;
+    while (!R.pending.empty()) ring_retire(R, R.pending.size() - 1);
+    if (R.p) (void)hipHostFree(R.p);
+    R.p = nullptr;
+    R.bytes = R.head = 0;
+    const size_t nb = std::max<size_t>(4 * need, size_t(1) << 20);
+    if ((e = hipHostMalloc(reinterpret_cast<void**>(&R.p), nb, hipHostMallocDefault)) != hipSuccess)
+      return e;
+    R.bytes = nb;
+  }
+  if (R.head + need > R.bytes) R.head = 0;
+  const size_t off = R.head;
+  for (size_t i = 0; i < R.pending.size();) {  // copies still reading [off, off + need)
+    const RingUse& u = R.pending[i];
+    if (u.off < off + need && off < u.off + u.len) {
+      if ((e = hipEventSynchronize(u.ev)) != hipSuccess) return e;
+      ring_retire(R, i);
+    } else {
+      ++i;
+    }
+  }
+  std::memcpy(R.p + off, src, bytes);
+  if ((e = hipMemcpyAsync(dst, R.p + off, bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+  hipEvent_t ev = nullptr;
+  for (size_t i = 0; i < R.spare.size(); ++i)
+    if (R.spare[i].first == dev) {
+      ev = R.spare[i].second;
+      R.spare.erase(R.spare.begin() + (std::ptrdiff_t)i);
+      break;
+    }
+  if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+  R.pending.push_back({off, need, dev, ev});
+  R.head = off + need;
+  return hipSuccess;
 }
 
 }  // namespace sks
@@ -587,14 +658,14 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
       keep_off.push_back(keep_off.back() + res[i]);
     }
     std::vector<uint64_t> dense = prefix(limit);
-    MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
+    MetaArena arena2(c);  // uploads are stream-ordered: safe to rewrite the arena
     const size_t o_psrc = arena2.add(f_pad), o_pdst = arena2.add(dense);
     SKS_TRY(arena2.upload());
     SKS_TRY(alloc_u64(&po.d, dense[k], &po.bytes));
     SKS_HIP(sks::compact_regions(col(c, 5), po.d, arena2.ptr(o_psrc), arena2.ptr(o_pdst), k,
                                  max_lim, st));
     po.off = keep_off;
-    SKS_HIP(hipStreamSynchronize(st));
+    // no stream sync: the pass's outputs are consumed in stream order
     passes.push_back(po);
     return SKS_OK;
   }
@@ -692,7 +763,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
       // every distinct candidate, contiguous per genome at uoff
       SKS_HIP(sks::seg_unique_scatter(col(c, 3), nullptr, T, max_len, d_csr, k, d_flag, d_pos,
                                       nullptr, nullptr, col(c, 5), nullptr, st, &runs));
-      MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
+      MetaArena arena2(c);  // uploads are stream-ordered: safe to rewrite the arena
       size_t o_uoff = arena2.add(uoff), o_lim = arena2.add(limit), o_dst = arena2.add(dst);
       SKS_TRY(arena2.upload());
       SKS_TRY(alloc_u64(&po.d, U, &po.bytes));
@@ -700,7 +771,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
       po.off = keep_off;
       SKS_HIP(sks::launch_bottom_select(col(c, 5), arena2.ptr(o_uoff), arena2.ptr(o_dst),
                                         arena2.ptr(o_lim), k, S.kconst, S.pol.flavour, po.d, st));
-      SKS_HIP(hipStreamSynchronize(st));
+      // no stream sync: the pass's outputs are consumed in stream order
       passes.push_back(po);
       return SKS_OK;
     }
@@ -753,7 +824,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   // not-done segments get limit 0, so this prefix is also keep_off's layout
   std::vector<uint64_t> dst = prefix(limit);
   const uint64_t U = dst[k];
-  MetaArena arena2(c);  // the stream is idle here: safe to rewrite the arena
+  MetaArena arena2(c);  // uploads are stream-ordered: safe to rewrite the arena
   size_t o_csr2 = arena2.add(csr), o_lim = arena2.add(limit), o_dst = arena2.add(dst);
   SKS_TRY(arena2.upload());
   d_csr = arena2.ptr(o_csr2);
@@ -775,7 +846,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
                                 mask_hi_bits, c->tmp, st));
     SKS_HIP(sks::launch_interleave(col(c, 6), col(c, 5), U, po.d, st));
   }
-  SKS_HIP(hipStreamSynchronize(st));
+  // no stream sync: the pass's outputs are consumed in stream order
   passes.push_back(po);
   return SKS_OK;
 }
@@ -917,9 +988,11 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
                              S.wide, c->device, st, c->grid_override));
     SKS_HIP(hipEventRecord(c->ev_s1, st));
     tm.scan_launches += n_tiles ? 1 : 0;
-    std::vector<uint64_t> counts(m), wins(m);
-    SKS_HIP(sks::pinned_d2h(counts.data(), p.seg_count, m * sizeof(uint64_t), st));
-    SKS_HIP(sks::pinned_d2h(wins.data(), p.seg_windows, m * sizeof(uint64_t), st));
+    // survivor and window counts sit next to each other in the arena: one read-back
+    if (o_win != o_cnt + m + 1) return sks::fail(SKS_E_HIP, "sks_sketch_build: arena layout");
+    std::vector<uint64_t> cw(2 * (m + 1));
+    SKS_HIP(sks::pinned_d2h(cw.data(), arena.ptr(o_cnt), cw.size() * sizeof(uint64_t), st));
+    std::vector<uint64_t> counts(cw.begin(), cw.begin() + m), wins(cw.begin() + (m + 1), cw.begin() + (m + 1) + m);
     float ms = 0;
     SKS_HIP(hipEventElapsedTime(&ms, c->ev_s0, c->ev_s1));
     tm.scan_ms += ms;

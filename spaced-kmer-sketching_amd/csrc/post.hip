@@ -20,7 +20,12 @@ namespace sks {
 
 hipError_t Scratch::reserve(size_t n) {
   if (n <= bytes) return hipSuccess;
-  if (ptr) (void)hipFree(ptr);
+  // queued work may still read the old buffer (metadata uploads do not wait
+  // for their stream): let it finish before the buffer goes (growth is rare)
+  if (ptr) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ptr);
+  }
   ptr = nullptr;
   bytes = 0;
   size_t want = std::max<size_t>(n, 1 << 20);
