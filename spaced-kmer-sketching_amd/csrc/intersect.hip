@@ -473,16 +473,29 @@ __global__ void k_hb_offsets(const uint32_t* __restrict__ counts, const uint32_t
                              uint32_t* __restrict__ boff, uint64_t* __restrict__ bstart,
                              uint32_t* __restrict__ stat, uint32_t G,
                              const uint32_t* __restrict__ gcounts, uint32_t* __restrict__ goff) {
+  __shared__ uint32_t s_max[kB / 64];
   const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  if (idx >= (uint64_t)n_blk * (B + 1)) return;
-  const uint32_t blk = (uint32_t)(idx / (B + 1)), b = (uint32_t)(idx % (B + 1));
-  const uint32_t base = bbase[(uint64_t)blk * B];
-  const uint32_t v = bbase[(uint64_t)blk * B + b];  // b == B: the next block's start
+  const bool in = idx < (uint64_t)n_blk * (B + 1);
+  const uint32_t blk = in ? (uint32_t)(idx / (B + 1)) : 0, b = in ? (uint32_t)(idx % (B + 1)) : B;
+  const uint32_t base = in ? bbase[(uint64_t)blk * B] : 0;
+  const uint32_t v = in ? bbase[(uint64_t)blk * B + b] : 0;  // b == B: the next block's start
+  // the largest block-bucket: one atomic per workgroup (one per wave cost
+  // ~12 us of this kernel's 27 on one contended word, config 4)
+  uint32_t pop = in && b < B ? bbase[(uint64_t)blk * B + b + 1] - v : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pop = max(pop, (uint32_t)__shfl_xor(pop, o, 64));
+  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = pop;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t m = 0;
+    for (int w = 0; w < kB / 64; ++w) m = max(m, s_max[w]);
+    if (m) atomicMax(stat, m);
+  }
+  if (!in) return;
   boff[idx] = v - base;
   if (b == 0) bstart[blk] = base;
   if (blk == n_blk - 1 && b == B) bstart[n_blk] = v;
   if (b == B) return;
-  atomicMax(stat, bbase[(uint64_t)blk * B + b + 1] - v);
   const uint64_t row0 = (uint64_t)blk * 64 * B + b;
   uint32_t run = v;
 #pragma unroll 8
@@ -538,7 +551,14 @@ __global__ __launch_bounds__(kB) void k_hb_stage(const uint64_t* __restrict__ da
 // Phase 2: one workgroup per (block, coarse group) places the group's
 // elements (64 slot runs in `stage`) at their (bucket, slot) cells. All its
 // writes fall in the group's own contiguous range of the layout (~|S| * 64 / G
-// elements), which L2 assembles into whole lines.
+// elements), which L2 assembles into whole lines.  The u8 slot ids of a group
+// of <= kPlaceIds elements are assembled in LDS and written out in order
+// afterwards: one scattered byte store per element cost about as much as the
+// 8-byte value stores (config 4: k_hb_place 110 -> 72 us).  Assembling the
+// values too needs smaller groups (LDS), and the staging pass then writes
+// shorter runs: 16 or 32 buckets per group measured 214-226 us for the whole
+// layout build against 186.
+constexpr uint32_t kPlaceIds = 16384;
 __global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ stage,
                                                  const uint32_t* __restrict__ off,
                                                  const uint32_t* __restrict__ goff,
@@ -547,14 +567,25 @@ __global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ st
                                                  uint64_t* __restrict__ out,
                                                  uint8_t* __restrict__ ids) {
   __shared__ uint32_t cur[64 * 64];  // [slot][bucket in group], B / G <= 64
+  __shared__ uint8_t s_ids[kPlaceIds];
+  __shared__ uint32_t s_total;
   const uint32_t G = 1u << log_g, bpg = B >> log_g;
   const uint32_t blk = blockIdx.x >> log_g, g = blockIdx.x & (G - 1);
   const uint64_t rowb = (uint64_t)blk * 64 * B + (uint64_t)g * bpg;
   for (uint32_t t = threadIdx.x; t < 64 * bpg; t += kB) {
     const uint32_t slot = t / bpg, bl = t % bpg;
-    cur[slot * 64 + bl] = off[rowb + (uint64_t)slot * B + bl];
+    cur[slot * bpg + bl] = off[rowb + (uint64_t)slot * B + bl];
+  }
+  if (threadIdx.x < 64) {  // wave 0: the group's element count
+    uint32_t c = gcounts[((uint64_t)blk * 64 + threadIdx.x) * G + g];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (threadIdx.x == 0) s_total = c;
   }
   __syncthreads();
+  const uint32_t base = cur[0];  // slot 0, first bucket: the group's first cell
+  const uint32_t total = s_total;
+  const bool local_ids = total <= kPlaceIds;
   // a wave per slot run; each lane loads its (up to) four elements of the run
   // before placing any, so a run of <= 256 elements is one round of loads (one
   // dependent load per lane and iteration before: 119 us for config 4)
@@ -573,12 +604,16 @@ __global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ st
       for (int u = 0; u < 4; ++u) {
         if (e0 + lane + 64 * u >= n) continue;
         const uint32_t bl = bucket_hash(v[u], log_b) - g * bpg;
-        const uint32_t d = atomicAdd(&cur[slot * 64 + bl], 1u);
+        const uint32_t d = atomicAdd(&cur[slot * bpg + bl], 1u);
         out[d] = v[u];
-        ids[d] = (uint8_t)slot;
+        if (local_ids) s_ids[d - base] = (uint8_t)slot;
+        else ids[d] = (uint8_t)slot;
       }
     }
   }
+  if (!local_ids) return;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < total; i += kB) ids[base + i] = s_ids[i];
 }
 
 struct JoinArgs {
