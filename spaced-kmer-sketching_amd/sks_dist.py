@@ -169,16 +169,30 @@ def _max_over(x, world, device):
 
 
 def _gather_flat(t, world):
+    return _gather_many([t], world)[0]
+
+
+def _gather_many(ts, world):
+    """All-gather of flat tensors, rank-major; with RCCL the gathers are queued
+    together (async) and waited on once, so their latencies overlap."""
     if world == 1:
-        return t
+        return list(ts)
     if dist.get_backend() == "nccl":
-        out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous())
-        return out
-    host = t.cpu()
-    parts = [torch.empty_like(host) for _ in range(world)]
-    dist.all_gather(parts, host)
-    return torch.cat(parts).to(t.device)
+        outs, works = [], []
+        for t in ts:
+            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+            works.append(dist.all_gather_into_tensor(out, t.contiguous(), async_op=True))
+            outs.append(out)
+        for w in works:
+            w.wait()
+        return outs
+    res = []
+    for t in ts:
+        host = t.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host)
+        res.append(torch.cat(parts).to(t.device))
+    return res
 
 
 def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity, build, count,
@@ -236,7 +250,7 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
         meta[: nb_local * B1] = boff[: nb_local * B1].to(device=device, dtype=torch.int32)
         meta[bpr * B1: bpr * B1 + nb_local + 1] = bstart[: nb_local + 1].to(device=device,
                                                                               dtype=torch.int32)
-    g_data, g_ids, g_meta = _gather_flat(pd, world), _gather_flat(pi, world), _gather_flat(meta, world)
+    g_data, g_ids, g_meta = _gather_many([pd, pi, meta], world)
     g_meta = g_meta.view(world, bpr * B1 + bpr + 1)
     g_boff = g_meta[:, : bpr * B1].reshape(-1).contiguous()
     g_bst = g_meta[:, bpr * B1: bpr * B1 + bpr].to(torch.int64) & 0xFFFFFFFF
