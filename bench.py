@@ -610,7 +610,8 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         t1 = time.perf_counter()
         # layouts of this rank's blocks, all-gathered; symmetric join tiles of
         # this rank; all-reduce of the counts
-        build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs)
+        build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs,
+                                                stat=world > 1)
         out = mat if dev == "cuda" else torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32)
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max, sksffi.join_layout_log_b,
                                        sksffi.join_layout_capacity(), build, count, device=dev,
@@ -845,7 +846,7 @@ def main():
 
     pairs = None
     if not args.no_pairs:
-        pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 3)),
+        pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 10)),
                           warmup=1, cpu_pairs=not args.no_cpu_baseline)
 
     c3s = None

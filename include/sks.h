@@ -260,11 +260,13 @@ int sks_sketch_union_wide(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64
  * be concatenated: append data/ids/boff and add the data offset to bstart. */
 /* log_b for a largest sketch of max_sketch_size elements (all ranks must agree). */
 uint32_t sks_join_layout_log_b(uint32_t max_sketch_size);
-/* Largest block-bucket population sks_intersect_sym_layout accepts. */
+/* Block-bucket population one join chunk holds; larger buckets are joined in
+ * sub-chunks (exact, slower), so a caller may raise log_b while the largest
+ * block-bucket exceeds it. */
 uint32_t sks_join_layout_capacity(void);
 /* Builds the layout of sketches (d_data, d_starts, d_sizes)[0, n) (u64 elements)
  * into caller buffers; *max_block_bucket (host) receives the largest
- * block-bucket population — above sks_join_layout_capacity() use log_b + 1. */
+ * block-bucket population (waits for the build); NULL skips that read-back. */
 int sks_join_layout_build(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
                           const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_out_data,
                           uint8_t* d_out_ids, uint32_t* d_out_boff, uint64_t* d_out_bstart,

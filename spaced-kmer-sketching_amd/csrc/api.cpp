@@ -1440,9 +1440,11 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
     SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, 0, n, total, log_b, d_out_data,
                                    d_out_ids, d_out_boff, d_out_bstart, stat, w, tmp, c->stream));
   }
-  uint32_t h = 0;
-  SKS_HIP(sks::pinned_d2h(&h, stat, 4, c->stream));
-  if (max_block_bucket) *max_block_bucket = h;
+  if (max_block_bucket) {  // NULL: no read-back, the call does not wait for the build
+    uint32_t h = 0;
+    SKS_HIP(sks::pinned_d2h(&h, stat, 4, c->stream));
+    *max_block_bucket = h;
+  }
   return SKS_OK;
 }
 

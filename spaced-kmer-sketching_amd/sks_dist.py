@@ -215,8 +215,8 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     nb_local = (g1 - g0 + TILE - 1) // TILE
     while True:
         data, ids, boff, bstart, mb = build(log_b)
-        if world == 1:
-            if mb <= capacity or log_b >= max_log_b:
+        if world == 1:  # mb None: the build skipped its read-back (counts are exact anyway)
+            if mb is None or mb <= capacity or log_b >= max_log_b:
                 break
         else:
             # one all-reduce for the capacity check and the padded layout size
@@ -262,13 +262,16 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     return out
 
 
-def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
+def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None, stat=True):
     """The build / count callables of all_vs_all_join for this rank's sketches
     on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
     `local_sizes` its sizes (numpy).  build(log_b) runs sks_join_layout_build
     into device buffers (kept in `cache` across calls of the same shape) and
     returns them on `device`; count(...) runs sks_intersect_sym_layout (on the
-    GPU, staging through `device` tensors when that is the CPU, as with gloo)."""
+    GPU, staging through `device` tensors when that is the CPU, as with gloo).
+    stat=False: the build does not read back its largest block-bucket (mb is
+    None), so nothing waits between the layout and the count — for world 1,
+    where the bucket count is then the first one tried."""
     n_local = len(local_sizes)
     nb_local = (n_local + TILE - 1) // TILE
     data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
@@ -285,7 +288,8 @@ def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
                           torch.empty(max(nb_local * B1, 1), dtype=torch.int32, device="cuda"),
                           torch.empty(nb_local + 1, dtype=torch.int64, device="cuda"))
         out = cache[key]
-        mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out))
+        mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out),
+                                   stat=stat)
         return tuple(t.to(device) for t in out) + (mx,)
 
     def count(n, log_b, d, i, b, s, t0, t1, out):

@@ -305,14 +305,15 @@ class Context:
         return int(k.value)
 
     def join_layout_build(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_data, out_ids,
-                          out_boff, out_bstart):
-        """sks_join_layout_build; returns the largest block-bucket population."""
+                          out_boff, out_bstart, stat=True):
+        """sks_join_layout_build; returns the largest block-bucket population, or
+        None with stat=False (no read-back: the call does not wait for the build)."""
         mx = C.c_uint32(0)
         check(lib().sks_join_layout_build(self.h, C.c_void_p(data_ptr), C.c_void_p(starts_ptr),
                                           C.c_void_p(sizes_ptr), n, log_b, C.c_void_p(out_data),
                                           C.c_void_p(out_ids), C.c_void_p(out_boff),
-                                          C.c_void_p(out_bstart), C.byref(mx)))
-        return mx.value
+                                          C.c_void_p(out_bstart), C.byref(mx) if stat else None))
+        return mx.value if stat else None
 
     def intersect_sym_layout(self, n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out):
         check(lib().sks_intersect_sym_layout(self.h, n, log_b, C.c_void_p(data), C.c_void_p(ids),

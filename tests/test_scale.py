@@ -87,7 +87,7 @@ def test_config4_all_vs_all_1000x5mb(env):
         assert np.array_equal(ss.sketch(g), want), g
         assert int(ss.windows()[g]) == nw
     # the bench's pair path, world 1
-    build, count = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda")
+    build, count = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda", stat=False)
     out = torch.full((n, n), -1, dtype=torch.int32, device="cuda")
     mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), sksffi.join_layout_log_b,
                                    sksffi.join_layout_capacity(), build, count, device="cuda", out=out)
