@@ -57,14 +57,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup(n_gpus, backend):
+def dist_setup(n_gpus, backend, rehearsal=False):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knob: SKS_BENCH_DEVICE=0 puts every rank on GPU 0 (use with gloo)
     if os.environ.get("SKS_BENCH_DEVICE") is not None:
         local = int(os.environ["SKS_BENCH_DEVICE"])
-    if world > 1:
+    # --dist-rehearsal: a process group even at world 1 (torchrun --nproc-per-node 1),
+    # so every all-gather / all-reduce of the N > 1 paths runs on RCCL on one GPU
+    if world > 1 or rehearsal:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -76,8 +78,14 @@ def dist_setup(n_gpus, backend):
     return world, rank, local
 
 
+def collective():
+    """A process group is up (world > 1, or the world-1 RCCL rehearsal)."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(world):
-    if world > 1:
+    if collective():
         import torch.distributed as dist
         dist.barrier()
 
@@ -91,14 +99,14 @@ def _reduce_scalar(x, op):
 
 
 def max_over_ranks(x, world):
-    if world == 1:
+    if not collective():
         return x
     import torch.distributed as dist
     return _reduce_scalar(x, dist.ReduceOp.MAX)
 
 
 def sum_over_ranks(x, world):
-    if world == 1:
+    if not collective():
         return x
     import torch.distributed as dist
     return _reduce_scalar(x, dist.ReduceOp.SUM)
@@ -381,7 +389,7 @@ def run_c3_sharded(ctx, world, rank, mask, buf, steps, warmup):
             "scaling": "strong", "ms_per_genome": tot * 1e3, "sketch_size": int(sk.numel()),
             "config": {"workload": "config3 genome split across ranks ((w-1) halos), union",
                        "collective": "all_gather of chunk sketches + all_reduce of windows"
-                       if world > 1 else "none"},
+                       if collective() else "none"},
             "check": "equals the whole-genome sketch (rank 0)"}
 
 
@@ -611,7 +619,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         # layouts of this rank's blocks, all-gathered; symmetric join tiles of
         # this rank; all-reduce of the counts
         build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs,
-                                                stat=world > 1)
+                                                stat=collective())
         out = mat if dev == "cuda" else torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32)
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max, sksffi.join_layout_log_b,
                                        sksffi.join_layout_capacity(), build, count, device=dev,
@@ -655,7 +663,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
                                     "join tiles split over ranks",
                    "collective": ("all_gather_into_tensor join layouts + all_reduce counts "
                                   + ("(RCCL)" if dev == "cuda" else "(gloo, via host)")
-                                  if world > 1 else "none")},
+                                  if collective() else "none")},
         "cpu_baseline": cpu,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
         "ms_end_to_end": (t_sketch + t_pairs) * 1e3,
@@ -685,7 +693,7 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
     ones = [bin(m).count("1") // 2 for m in masks]
     starts = torch.arange(n, dtype=torch.int64, device="cuda") * C4_S
     n_tiles = sksffi.intersect_sym_tiles(n)
-    dev = "cuda" if world > 1 and os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
+    dev = "cuda" if collective() and os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
 
     # seeds are independent: `lanes` seeds run at once, each lane a context on its
     # own HIP stream with its own buffers, driven by its own host thread, so one
@@ -747,8 +755,8 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
                    "seeds": C5_SEEDS, "s": C4_S, "w": W, "k": K,
                    "sharding": "seeds over ranks", "consensus": "mean ANI over seeds",
                    "seeds_in_flight": max(1, lanes_n),
-                   "collective": ("all_reduce of ANI sums (RCCL)" if world > 1 and dev == "cuda"
-                                  else ("all_reduce (gloo)" if world > 1 else "none"))},
+                   "collective": ("all_reduce of ANI sums (RCCL)" if collective() and dev == "cuda"
+                                  else ("all_reduce (gloo)" if collective() else "none"))},
     }
 
 
@@ -782,12 +790,15 @@ def main():
     ap.add_argument("--inflight", type=int, default=2,
                     help="config-3 builds in flight (one context + HIP stream each)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="start the process group at world 1 too (under torchrun), so the "
+                         "collective paths run on the backend")
     ap.add_argument("--traffic-json", default=latest_traffic_json(),
                     help="PMC HBM traffic of the scan launches this command times "
                          "(tools/profile_round.sh; default: the newest profiles/rNN)")
     args = ap.parse_args()
 
-    world, rank, local = dist_setup(args.gpus, args.dist_backend)
+    world, rank, local = dist_setup(args.gpus, args.dist_backend, args.dist_rehearsal)
     ctx = sksffi.Context(local)
     mask = sksffi.mask_generate(W, K, MASK_SEED)
 
@@ -898,7 +909,7 @@ def main():
             "c3_one_genome_sharded": c3s,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if collective():
         import torch.distributed as dist
         dist.destroy_process_group()
 

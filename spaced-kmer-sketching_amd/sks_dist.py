@@ -16,6 +16,13 @@ import torch.distributed as dist
 TILE = 64
 
 
+def _solo(world):
+    """True when no exchange is needed: one rank and no process group.  A process
+    group of size 1 (tests/test_rccl.py: RCCL on one GPU) takes the collective
+    path, so every all-gather / all-reduce below runs on the backend."""
+    return world == 1 and not (dist.is_available() and dist.is_initialized())
+
+
 def genome_shard(n_genomes, world, rank):
     per = (n_genomes + world - 1) // world
     g0 = min(n_genomes, rank * per)
@@ -43,7 +50,7 @@ def sym_tile_coords(t, n):
 
 def gather_sketches(local, local_sizes, world):
     """local: [per, stride] int64 padded sketches; local_sizes: [per] int32."""
-    if world == 1:
+    if _solo(world):
         return local, local_sizes
     per, stride = local.shape
     if dist.get_backend() == "nccl":
@@ -83,7 +90,7 @@ def all_vs_all(local, local_sizes, n_genomes, world, rank, count_sym, out=None):
     if out is None:
         out = torch.empty((n_genomes, n_genomes), dtype=torch.int32, device=local.device)
     count_sym(src, src_sz, n_genomes, t0, t1, out)
-    if world > 1:
+    if not _solo(world):
         sum_matrix(out)
     return out
 
@@ -104,7 +111,7 @@ def all_vs_all_rows(local, local_sizes, n_genomes, world, rank, count_rows):
     rows = torch.zeros((r1 - r0, n_genomes), dtype=torch.int32, device=local.device)
     if r1 > r0:
         count_rows(src, src_sz, n_genomes, r0, r1, rows)
-    if world == 1:
+    if _solo(world):
         return rows
     per = (n_genomes + world - 1) // world
     pad = torch.zeros((per, n_genomes), dtype=torch.int32, device=local.device)
@@ -138,7 +145,7 @@ def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
     parts = [ani_for_seed(s) for s in mine]
     for r in parts:
         acc += (r.result() if hasattr(r, "result") else r).to(device)
-    if world > 1:
+    if not _solo(world):
         sum_matrix(acc)
     acc /= n_seeds
     return acc, mine
@@ -161,7 +168,7 @@ def block_shard(n_genomes, world, rank):
 
 
 def _max_over(x, world, device):
-    if world == 1:
+    if _solo(world):
         return int(x)
     t = torch.tensor([int(x)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -175,7 +182,7 @@ def _gather_flat(t, world):
 def _gather_many(ts, world):
     """All-gather of flat tensors, rank-major; with RCCL the gathers are queued
     together (async) and waited on once, so their latencies overlap."""
-    if world == 1:
+    if _solo(world):
         return list(ts)
     if dist.get_backend() == "nccl":
         outs, works = [], []
@@ -215,14 +222,15 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     nb_local = (g1 - g0 + TILE - 1) // TILE
     while True:
         data, ids, boff, bstart, mb = build(log_b)
-        if world == 1:  # mb None: the build skipped its read-back (counts are exact anyway)
+        if _solo(world):  # mb None: the build skipped its read-back (counts are exact anyway)
             if mb is None or mb <= capacity or log_b >= max_log_b:
                 break
         else:
             # one all-reduce for the capacity check and the padded layout size
             tot = bstart[nb_local:nb_local + 1].to(device=device, dtype=torch.int64) if nb_local \
                 else torch.zeros(1, dtype=torch.int64, device=device)
-            both = torch.cat([torch.tensor([int(mb)], dtype=torch.int64, device=device), tot])
+            both = torch.cat([torch.tensor([0 if mb is None else int(mb)], dtype=torch.int64,
+                                           device=device), tot])
             dist.all_reduce(both, op=dist.ReduceOp.MAX)
             mb_all, cap_e = (int(v) for v in both.cpu())
             if mb_all <= capacity or log_b >= max_log_b:
@@ -232,7 +240,7 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     t0, t1 = tile_shard(sym_tiles(n_genomes), world, rank)
     if out is None:
         out = torch.empty((n_genomes, n_genomes), dtype=torch.int32, device=device)
-    if world == 1:  # the local layout is the whole layout
+    if _solo(world):  # the local layout is the whole layout
         count(n_genomes, log_b, data, ids, boff, bstart, t0, t1, out)
         return out
     tot = int(bstart[nb_local]) if nb_local else 0
@@ -320,7 +328,7 @@ def sketch_genome_sharded(n_bytes, w, world, rank, build_chunk, union, device="c
     every rank."""
     a, b = genome_chunk(n_bytes, w, world, rank)
     vals, nw = build_chunk(a, b)
-    if world == 1:
+    if _solo(world):
         return vals, nw
     k = vals.shape[0]
     rest = tuple(vals.shape[1:])
