@@ -616,10 +616,12 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         local_max = int(local_sizes.max()) if n_local else 0
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        # layouts of this rank's blocks, all-gathered; symmetric join tiles of
-        # this rank; all-reduce of the counts
+        # layouts of this rank's blocks, built into the padded send buffers and
+        # all-gathered; symmetric join tiles of this rank; all-reduce of the
+        # counts.  stat=False: no block-bucket read-back (bucket count from the
+        # largest sketch; counts are exact at any)
         build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs,
-                                                stat=collective())
+                                                stat=False)
         out = mat if dev == "cuda" else torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32)
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max, sksffi.join_layout_log_b,
                                        sksffi.join_layout_capacity(), build, count, device=dev,

@@ -206,8 +206,13 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
                     device="cpu", out=None, max_log_b=14):
     """Full n x n int32 intersection matrix on every rank.
 
-    build(log_b) -> (data u64[tot], ids u8[tot], boff u32[nb*(B+1)], bstart u64[nb+1],
-                     max_block_bucket) for this rank's block-aligned genomes (block_shard);
+    build(log_b, pad) -> (data u64[], ids u8[], boff u32[], bstart u64[], max_block_bucket)
+    builds the layout of this rank's block-aligned genomes (block_shard).  pad is
+    None for one rank without a process group; otherwise (cap_e, bpr) and the
+    buffers must have exactly cap_e data / id entries, bpr * (B + 1) bucket starts
+    and bpr + 1 block starts (entries past the rank's own blocks are never read:
+    those blocks lie beyond n), so they are all-gathered as they are.
+    max_block_bucket may be None (the build skipped that read-back).
     count(n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out) fills `out`
     (zeroed first) with the counts of upper-triangle tiles [tile_begin, tile_end), both halves
     — the contract of sks_intersect_sym_layout.
@@ -218,53 +223,33 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     table-sized sub-chunks and probes the bucket's row elements once per
     sub-chunk, so the counts at max_log_b are exact for any sketch size."""
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
-    log_b = log_b_for(_max_over(local_max_size, world, device))
-    nb_local = (g1 - g0 + TILE - 1) // TILE
+    max_all = _max_over(local_max_size, world, device)
+    log_b = log_b_for(max_all)
+    solo = _solo(world)
+    # every rank's layout holds at most bpr * 64 * (largest sketch) elements, so
+    # the layouts are built straight into padded send buffers of that size: no
+    # all-reduce of the layout sizes and no copies before the gather
+    pad = None if solo else (max(1, bpr * TILE * max_all), bpr)
     while True:
-        data, ids, boff, bstart, mb = build(log_b)
-        if _solo(world):  # mb None: the build skipped its read-back (counts are exact anyway)
-            if mb is None or mb <= capacity or log_b >= max_log_b:
-                break
-        else:
-            # one all-reduce for the capacity check and the padded layout size
-            tot = bstart[nb_local:nb_local + 1].to(device=device, dtype=torch.int64) if nb_local \
-                else torch.zeros(1, dtype=torch.int64, device=device)
-            both = torch.cat([torch.tensor([0 if mb is None else int(mb)], dtype=torch.int64,
-                                           device=device), tot])
-            dist.all_reduce(both, op=dist.ReduceOp.MAX)
-            mb_all, cap_e = (int(v) for v in both.cpu())
-            if mb_all <= capacity or log_b >= max_log_b:
-                break
+        data, ids, boff, bstart, mb = build(log_b, pad)
+        if mb is None or log_b >= max_log_b:
+            break
+        if (mb if solo else _max_over(mb, world, device)) <= capacity:
+            break
         log_b += 1
-    B1 = (1 << log_b) + 1
     t0, t1 = tile_shard(sym_tiles(n_genomes), world, rank)
     if out is None:
         out = torch.empty((n_genomes, n_genomes), dtype=torch.int32, device=device)
-    if _solo(world):  # the local layout is the whole layout
+    if solo:  # the local layout is the whole layout
         count(n_genomes, log_b, data, ids, boff, bstart, t0, t1, out)
         return out
-    tot = int(bstart[nb_local]) if nb_local else 0
-    cap_e = max(1, cap_e)
-    # pad to the common per-rank shape (missing blocks are empty); bucket and
-    # block starts travel together in one int32 gather (< 2^32 per layout)
-    pd = torch.zeros(cap_e, dtype=torch.int64, device=device)
-    pi = torch.zeros(cap_e, dtype=torch.uint8, device=device)
-    meta = torch.zeros(bpr * B1 + bpr + 1, dtype=torch.int32, device=device)
-    meta[bpr * B1:] = tot
-    if tot:
-        pd[:tot] = data[:tot]
-        pi[:tot] = ids[:tot]
-    if nb_local:
-        meta[: nb_local * B1] = boff[: nb_local * B1].to(device=device, dtype=torch.int32)
-        meta[bpr * B1: bpr * B1 + nb_local + 1] = bstart[: nb_local + 1].to(device=device,
-                                                                              dtype=torch.int32)
-    g_data, g_ids, g_meta = _gather_many([pd, pi, meta], world)
-    g_meta = g_meta.view(world, bpr * B1 + bpr + 1)
-    g_boff = g_meta[:, : bpr * B1].reshape(-1).contiguous()
-    g_bst = g_meta[:, bpr * B1: bpr * B1 + bpr].to(torch.int64) & 0xFFFFFFFF
-    g_bst = g_bst + torch.arange(world, device=device, dtype=torch.int64).view(world, 1) * cap_e
+    cap_e = pad[0]
+    g_data, g_ids, g_boff, g_bst = _gather_many([data, ids, boff, bstart], world)
+    # block k of rank r starts at r * cap_e in the gathered data
+    g_bst = g_bst.view(world, bpr + 1)[:, :bpr] + \
+        torch.arange(world, device=g_bst.device, dtype=torch.int64).view(world, 1) * cap_e
     g_bst = torch.cat([g_bst.reshape(-1),
-                       torch.tensor([world * cap_e], dtype=torch.int64, device=device)])
+                       torch.full((1,), world * cap_e, dtype=torch.int64, device=g_bst.device)])
     count(n_genomes, log_b, g_data, g_ids, g_boff, g_bst, t0, t1, out)
     sum_matrix(out)
     return out
@@ -273,28 +258,31 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
 def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None, stat=True):
     """The build / count callables of all_vs_all_join for this rank's sketches
     on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
-    `local_sizes` its sizes (numpy).  build(log_b) runs sks_join_layout_build
+    `local_sizes` its sizes (numpy).  build(log_b, pad) runs sks_join_layout_build
     into device buffers (kept in `cache` across calls of the same shape) and
     returns them on `device`; count(...) runs sks_intersect_sym_layout (on the
     GPU, staging through `device` tensors when that is the CPU, as with gloo).
     stat=False: the build does not read back its largest block-bucket (mb is
-    None), so nothing waits between the layout and the count — for world 1,
-    where the bucket count is then the first one tried."""
+    None), so nothing waits between the layout and the count; the bucket count
+    is then the first one tried (a speed choice only: counts are exact at any)."""
     n_local = len(local_sizes)
     nb_local = (n_local + TILE - 1) // TILE
     data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
     tot = int(local_sizes.astype("int64").sum()) if n_local else 0
     cache = {} if cache is None else cache
 
-    def build(log_b):
+    def build(log_b, pad=None):
         B1 = (1 << log_b) + 1
-        key = (tot, log_b, nb_local)
+        # padded (all_vs_all_join with a process group): the send buffers
+        # themselves, cap_e elements and bpr blocks, gathered as they are
+        cap_e, nb = pad if pad is not None else (max(tot, 1), max(nb_local, 1))
+        key = (cap_e, log_b, nb)
         if key not in cache:  # layout buffers persist across steps
             cache.clear()
-            cache[key] = (torch.empty(max(tot, 1), dtype=torch.int64, device="cuda"),
-                          torch.empty(max(tot, 1), dtype=torch.uint8, device="cuda"),
-                          torch.empty(max(nb_local * B1, 1), dtype=torch.int32, device="cuda"),
-                          torch.empty(nb_local + 1, dtype=torch.int64, device="cuda"))
+            cache[key] = (torch.empty(cap_e, dtype=torch.int64, device="cuda"),
+                          torch.empty(cap_e, dtype=torch.uint8, device="cuda"),
+                          torch.zeros(nb * B1, dtype=torch.int32, device="cuda"),
+                          torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
         out = cache[key]
         mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out),
                                    stat=stat)

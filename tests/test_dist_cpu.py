@@ -285,9 +285,17 @@ def _join_worker(rank, world, port, q, capacity, max_log_b):
     mine = sk[g0:g1]
     built = []
 
-    def build(lb):
+    def build(lb, pad):
         built.append(lb)
-        return _np_layout(mine, lb)
+        d, i, b, s, mx = _np_layout(mine, lb)
+        cap_e, bpr = pad  # the padded send-buffer shape all_vs_all_join gathers
+        assert d.numel() <= cap_e and b.numel() <= bpr * ((1 << lb) + 1)
+        pd = torch.full((cap_e,), -7, dtype=torch.int64)
+        pi = torch.full((cap_e,), 99, dtype=torch.uint8)
+        pb = torch.full((bpr * ((1 << lb) + 1),), -3, dtype=torch.int32)
+        ps = torch.full((bpr + 1,), -5, dtype=torch.int64)  # junk past the own blocks
+        pd[:d.numel()], pi[:i.numel()], pb[:b.numel()], ps[:s.numel()] = d, i, b, s
+        return pd, pi, pb, ps, mx
     mat = sks_dist.all_vs_all_join(
         N_GENOMES, world, rank, max((len(s) for s in mine), default=0),
         lambda m: 1 if capacity < 100 else 3, capacity=capacity, build=build,
