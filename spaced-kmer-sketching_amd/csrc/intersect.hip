@@ -381,7 +381,7 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 // that fit the table (<= kJCap elements; a larger bucket is cut into
 // sub-chunks) and the row block's same buckets with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
 #ifndef SKS_JOIN_DIAG  // diagnostics only (wrong counts): 1 no probes / hit adds,
-#define SKS_JOIN_DIAG 0  // 2 no count flush
+#define SKS_JOIN_DIAG 0  // 2 no count flush, 4 probes without hit adds
 #endif
 // 512 threads (8 waves): with the table's LDS allowing 3 workgroups per CU,
 // 24 waves per CU instead of 12 hide the LDS round trips of the insert and
@@ -755,6 +755,7 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
     }
   };
 
+  uint32_t diag_acc = 0;  // SKS_JOIN_DIAG & 4: hits counted, not added
   uint32_t made[kJMade];  // slots this thread created in the current chunk
 #pragma unroll
   for (int u = 0; u < kJMade; ++u) made[u] = kNoSlot;
@@ -865,6 +866,7 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
         if (r >= r_valid) continue;
         const unsigned long long m = lookup(cur.rv[u], sh[u], sl[u]);
         if (SKS_JOIN_DIAG & 1) continue;
+        if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
         if (m) add_hits(r, m);
       }
       for (uint32_t k = rs + tid + kJB * kJRowPf; k < re; k += kJB) {
@@ -873,6 +875,7 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
         const uint64_t v = rdata[k];
         const uint32_t h = fp_slot(v);
         const unsigned long long m = lookup(v, h, s_slot[h]);
+        if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
         if (m) add_hits(r, m);
       }
       __syncthreads();
@@ -886,6 +889,7 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   }
   __syncthreads();
   JSTAMP(5);
+  if (SKS_JOIN_DIAG & 4) atomicAdd(&s_cnt[0], diag_acc);
   if (SKS_JOIN_DIAG & 2) return;
   for (int i = tid; i < kTile * kTile; i += kJB) {
     const uint32_t r = i >> 6, c = i & 63;
