@@ -657,6 +657,17 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         "unit": "ordered pairs/s", "scaling": "strong",
         "ms_pair_phase": t_pairs * 1e3, "ms_sketch_phase": t_sketch * 1e3,
         "pair_kernel_ms_rank0": k_ms,
+        # streamed-equivalent bytes of the pair kernel, 8 B per
+        # element of both sets + 4 B per count, for every ordered pair this rank's
+        # tiles cover (symmetric tiles give both halves); the join reads each
+        # sketch from the layout once per tile row / column (LDS / L2 reuse), so
+        # this figure can exceed what HBM moves — it is labelled, not an HBM claim
+        "roofline_streamed_equivalent": {
+            "bytes_per_pair": 8 * 2 * C4_S + 4,
+            "pairs_this_rank": C4_GENOMES * C4_GENOMES / world,
+            "achieved_GBps": (8 * 2 * C4_S + 4) * C4_GENOMES * C4_GENOMES / world / (k_ms * 1e-3) / 1e9
+            if k_ms else None,
+            "hbm_peak_GBps": HBM_PEAK_GBS},
         "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - W + 1) / t_sketch,
         "ani_mean_all_pairs": float(np.mean(ani)),
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
