@@ -10,8 +10,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
+#include <functional>
 #include <iostream>
 #include <mutex>
+#include <numeric>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -29,6 +31,7 @@ namespace {
 
 std::mutex g_mu;
 int g_device = 0;
+bool g_device_set = false;
 sks_ctx* g_ctx = nullptr;
 bool g_exit_on_io = true;
 int g_flavour = SKS_HASH_BOOST_MIX;
@@ -54,13 +57,16 @@ sks_ctx* ctx() {
   return g_ctx;
 }
 
-DevMem::DevMem(size_t bytes) {
-  check_hip(hipSetDevice(g_device), "hipSetDevice");
+DevMem::DevMem(size_t bytes, int dev) : device(dev < 0 ? g_device : dev) {
+  check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipMalloc(&p, bytes ? bytes : 1), "hipMalloc");
 }
 
 DevMem::~DevMem() {
-  if (p) (void)hipFree(p);
+  if (p) {
+    (void)hipSetDevice(device);
+    (void)hipFree(p);
+  }
 }
 
 sks_fasta* open_fasta(const char* path) {
@@ -82,13 +88,13 @@ struct FastaHandle {
 };
 
 // Sketch a device buffer of consecutive segments (off[i], off[i+1]) in one build.
-std::vector<kmer_set> sketch_device(const uint8_t* d_seq, const std::vector<uint64_t>& off,
+std::vector<kmer_set> sketch_device(sks_ctx* c, const uint8_t* d_seq, const std::vector<uint64_t>& off,
                                     const kmer_bitset& mask, int w, const sketch_policy& pol) {
   const size_t n_seg = off.size() - 1;
   sks_policy p{pol.kind, pol.flavour, pol.param, pol.nonce};
   uint64_t m[2] = {mask.lo(), mask.hi()};
   sks_sketch_set* set = nullptr;
-  check(sks_sketch_build(ctx(), d_seq, off.back(), off.data(), (uint32_t)n_seg, w, m, &p, &set));
+  check(sks_sketch_build(c, d_seq, off.back(), off.data(), (uint32_t)n_seg, w, m, &p, &set));
   const int ew = sks_sketch_set_elem_words(set);
   std::vector<uint32_t> sizes(n_seg);
   sks_sketch_set_sizes(set, sizes.data());
@@ -123,30 +129,111 @@ std::vector<kmer_set> sketch_streams(const std::vector<std::vector<uint8_t>>& st
   for (auto& s : streams) all.insert(all.end(), s.begin(), s.end());
   DevMem d(all.size());
   check_hip(hipMemcpy(d.p, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy H2D");
-  return sketch_device(d.as<uint8_t>(), off, mask, w, pol);
+  return sketch_device(ctx(), d.as<uint8_t>(), off, mask, w, pol);
 }
 
 // Raw FASTA files: the host only reads bytes; strings_from_fasta runs on the
 // device (sks_fasta_parse_device) straight into the segment layout.
-std::vector<kmer_set> sketch_raw_files(const std::vector<std::vector<uint8_t>>& raws,
+std::vector<kmer_set> sketch_raw_files(sks_ctx* c, int device,
+                                       const std::vector<const std::vector<uint8_t>*>& raws,
                                        const kmer_bitset& mask, int w, const sketch_policy& pol) {
   std::vector<uint64_t> in_off(1, 0);
-  for (auto& r : raws) in_off.push_back(in_off.back() + r.size());
-  DevMem d_raw(in_off.back());
+  for (auto* r : raws) in_off.push_back(in_off.back() + r->size());
+  DevMem d_raw(in_off.back(), device);
   for (size_t i = 0; i < raws.size(); ++i)
-    if (!raws[i].empty())
-      check_hip(hipMemcpy(d_raw.as<uint8_t>() + in_off[i], raws[i].data(), raws[i].size(),
+    if (!raws[i]->empty())
+      check_hip(hipMemcpy(d_raw.as<uint8_t>() + in_off[i], raws[i]->data(), raws[i]->size(),
                           hipMemcpyHostToDevice), "hipMemcpy H2D");
-  DevMem d_stream(in_off.back() + raws.size());  // a stream is at most raw + 1 bytes
+  DevMem d_stream(in_off.back() + raws.size(), device);  // a stream is at most raw + 1 bytes
   std::vector<uint64_t> off(1, 0);
   for (size_t i = 0; i < raws.size(); ++i) {
     uint64_t nb = 0, nr = 0;
-    check(sks_fasta_parse_device(ctx(), d_raw.as<uint8_t>() + in_off[i], raws[i].size(),
-                                 d_stream.as<uint8_t>() + off.back(), raws[i].size() + 1, nullptr, 0,
+    check(sks_fasta_parse_device(c, d_raw.as<uint8_t>() + in_off[i], raws[i]->size(),
+                                 d_stream.as<uint8_t>() + off.back(), raws[i]->size() + 1, nullptr, 0,
                                  &nb, &nr));
     off.push_back(off.back() + nb);
   }
-  return sketch_device(d_stream.as<uint8_t>(), off, mask, w, pol);
+  return sketch_device(c, d_stream.as<uint8_t>(), off, mask, w, pol);
+}
+
+std::vector<kmer_set> sketch_raw_files(const std::vector<std::vector<uint8_t>>& raws,
+                                       const kmer_bitset& mask, int w, const sketch_policy& pol) {
+  std::vector<const std::vector<uint8_t>*> r;
+  for (auto& x : raws) r.push_back(&x);
+  return sketch_raw_files(ctx(), g_device, r, mask, w, pol);
+}
+
+// ---- device pool of the parallel_* entry points ---------------------------------------------
+namespace {
+std::vector<int> g_devices;  // set_devices; empty = default
+struct PoolCtx {
+  int device;
+  sks_ctx* ctx;
+};
+std::vector<PoolCtx> g_pool;  // one context per list entry (a repeated device gets several)
+
+std::vector<int> default_devices() {
+  if (const char* e = getenv("SKS_FACADE_DEVICES")) {
+    std::vector<int> d;
+    for (const char* q = e; *q;) {
+      char* end = nullptr;
+      const long v = strtol(q, &end, 10);
+      if (end == q) break;
+      d.push_back((int)v);
+      q = *end == ',' ? end + 1 : end;
+    }
+    if (!d.empty()) return d;
+  }
+  if (g_device_set) return {g_device};
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return {g_device};
+  std::vector<int> d(n);
+  std::iota(d.begin(), d.end(), 0);
+  return d;
+}
+}  // namespace
+
+std::vector<int> pool_devices() {
+  std::lock_guard<std::mutex> lock(g_mu);
+  return g_devices.empty() ? default_devices() : g_devices;
+}
+
+// Context of pool entry i (created on first use; entries persist for the process).
+sks_ctx* pool_ctx(size_t i, int device) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  if (g_pool.size() <= i) g_pool.resize(i + 1, PoolCtx{-1, nullptr});
+  PoolCtx& p = g_pool[i];
+  if (p.ctx && p.device != device) {
+    sks_ctx_destroy(p.ctx);
+    p.ctx = nullptr;
+  }
+  if (!p.ctx) {
+    check(sks_ctx_create(device, nullptr, &p.ctx));
+    p.device = device;
+  }
+  return p.ctx;
+}
+
+// Runs job(k, device, ctx) for k in [0, n_parts) on the pool, one host thread
+// per part; the first exception (in part order) is rethrown.
+void on_pool(size_t n_parts, const std::vector<int>& devs,
+             const std::function<void(size_t, int, sks_ctx*)>& job) {
+  std::vector<std::exception_ptr> err(n_parts);
+  std::vector<sks_ctx*> cs(n_parts);
+  for (size_t k = 0; k < n_parts; ++k) cs[k] = pool_ctx(k, devs[k]);
+  std::vector<std::thread> ts;
+  for (size_t k = 0; k < n_parts; ++k)
+    ts.emplace_back([&, k]() {
+      try {
+        check_hip(hipSetDevice(devs[k]), "hipSetDevice");
+        job(k, devs[k], cs[k]);
+      } catch (...) {
+        err[k] = std::current_exception();
+      }
+    });
+  for (auto& t : ts) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
 }
 
 // Whole-file read; false if the file cannot be opened or read.
@@ -193,6 +280,17 @@ std::vector<std::vector<uint8_t>> read_files(int num_files, char* filenames[]) {
 }
 
 namespace {
+
+// Devices of the pair count in progress: empty = the facade's own context
+// (compute_pairwise_...), else the pool (parallel_compute_pairwise_...).
+thread_local std::vector<int> g_pair_devices;
+struct PairDevices {  // scope of a parallel_ pair count (one device keeps the facade's context)
+  std::vector<int> saved;
+  explicit PairDevices(std::vector<int> d) : saved(std::move(g_pair_devices)) {
+    g_pair_devices = d.size() >= 2 ? std::move(d) : std::vector<int>{};
+  }
+  ~PairDevices() { g_pair_devices = std::move(saved); }
+};
 
 // Pair counts on the GPU for sets sharing a mask; pairs with different masks
 // have no common k-mer (identity includes the mask, kmer.hpp:82-85).
@@ -289,13 +387,6 @@ std::vector<int> pair_counts_single_mask(const std::vector<const kmer_set*>& a,
   }
   std::vector<int> out(a.size(), 0);
   if (a.empty()) return out;
-  DevMem d_words(words.size() * 8), d_starts(starts.size() * 8), d_sizes(sizes.size() * 4),
-      d_a(ia.size() * 4), d_b(ib.size() * 4), d_out(a.size() * 4);
-  check_hip(hipMemcpy(d_words.p, words.data(), words.size() * 8, hipMemcpyHostToDevice), "H2D");
-  check_hip(hipMemcpy(d_starts.p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice), "H2D");
-  check_hip(hipMemcpy(d_sizes.p, sizes.data(), sizes.size() * 4, hipMemcpyHostToDevice), "H2D");
-  check_hip(hipMemcpy(d_a.p, ia.data(), ia.size() * 4, hipMemcpyHostToDevice), "H2D");
-  check_hip(hipMemcpy(d_b.p, ib.data(), ib.size() * 4, hipMemcpyHostToDevice), "H2D");
   std::vector<int32_t> res(a.size());
   const uint64_t n = uniq.size();
   // Pair lists that cover a large part of the n x n matrix — the reference's
@@ -303,21 +394,58 @@ std::vector<int> pair_counts_single_mask(const std::vector<const kmer_set*>& a,
   // (kmer-sketching.cpp:195-200) — are counted as the whole symmetric matrix by
   // the join kernel (sks_intersect_sym) and gathered; sparse lists go through
   // one wavefront per pair (sks_intersect_pairs).
-  if (n >= 64 && n <= 16384 && a.size() * 4 >= n * n) {
-    DevMem d_mat(n * n * 4);
-    check(sks_intersect_sym(ctx(), d_words.as<uint64_t>(), d_starts.as<uint64_t>(),
-                            d_sizes.as<uint32_t>(), ew, (uint32_t)n, 0, sks_intersect_sym_tiles((uint32_t)n),
-                            d_mat.as<int32_t>()));
-    check(sks_ctx_synchronize(ctx()));
-    std::vector<int32_t> mat(n * n);
-    check_hip(hipMemcpy(mat.data(), d_mat.p, mat.size() * 4, hipMemcpyDeviceToHost), "D2H");
-    for (size_t i = 0; i < a.size(); ++i) res[i] = mat[(uint64_t)ia[i] * n + ib[i]];
-  } else {
-    check(sks_intersect_pairs(ctx(), d_words.as<uint64_t>(), d_starts.as<uint64_t>(),
-                              d_sizes.as<uint32_t>(), ew, d_a.as<int32_t>(), d_b.as<int32_t>(),
-                              a.size(), d_out.as<int32_t>()));
-    check(sks_ctx_synchronize(ctx()));
-    check_hip(hipMemcpy(res.data(), d_out.p, res.size() * 4, hipMemcpyDeviceToHost), "D2H");
+  const bool dense = n >= 64 && n <= 16384 && a.size() * 4 >= n * n;
+  // parallel_* callers spread the work over the device pool (kmer_set.cpp:
+  // 167-184's cilk_for over pairs): every device holds all sketches and counts
+  // a contiguous share of the symmetric tiles (dense) or of the pair list
+  const std::vector<int> devs = g_pair_devices.empty() ? std::vector<int>{g_device} : g_pair_devices;
+  // (128-bit k-mers: row blocks of sks_intersect_all, as partial symmetric tile
+  // ranges take u64 sketches only)
+  const bool by_rows = dense && ew == 2 && devs.size() > 1;
+  const uint64_t units = !dense ? a.size() : by_rows ? n : sks_intersect_sym_tiles((uint32_t)n);
+  const size_t parts = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(devs.size(), units));
+  std::vector<std::vector<int32_t>> mats(dense ? parts : 0);
+  auto job = [&](size_t k, int device, sks_ctx* c) {
+    const uint64_t u0 = units * k / parts, u1 = units * (k + 1) / parts;
+    DevMem d_words(words.size() * 8, device), d_starts(starts.size() * 8, device),
+        d_sizes(sizes.size() * 4, device);
+    check_hip(hipMemcpy(d_words.p, words.data(), words.size() * 8, hipMemcpyHostToDevice), "H2D");
+    check_hip(hipMemcpy(d_starts.p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice), "H2D");
+    check_hip(hipMemcpy(d_sizes.p, sizes.data(), sizes.size() * 4, hipMemcpyHostToDevice), "H2D");
+    if (by_rows) {  // rows [u0, u1) of the n x n matrix, the rest 0
+      mats[k].assign(n * n, 0);
+      if (u1 > u0) {
+        DevMem d_rows((u1 - u0) * n * 4, device);
+        check(sks_intersect_all(c, d_words.as<uint64_t>(), d_starts.as<uint64_t>(), d_sizes.as<uint32_t>(),
+                                ew, (uint32_t)n, (uint32_t)u0, (uint32_t)u1, d_rows.as<int32_t>()));
+        check(sks_ctx_synchronize(c));
+        check_hip(hipMemcpy(mats[k].data() + u0 * n, d_rows.p, (u1 - u0) * n * 4, hipMemcpyDeviceToHost),
+                  "D2H");
+      }
+    } else if (dense) {
+      DevMem d_mat(n * n * 4, device);
+      check(sks_intersect_sym(c, d_words.as<uint64_t>(), d_starts.as<uint64_t>(), d_sizes.as<uint32_t>(),
+                              ew, (uint32_t)n, u0, u1, d_mat.as<int32_t>()));
+      check(sks_ctx_synchronize(c));
+      mats[k].resize(n * n);
+      check_hip(hipMemcpy(mats[k].data(), d_mat.p, n * n * 4, hipMemcpyDeviceToHost), "D2H");
+    } else if (u1 > u0) {
+      const uint64_t m = u1 - u0;
+      DevMem d_a(m * 4, device), d_b(m * 4, device), d_out(m * 4, device);
+      check_hip(hipMemcpy(d_a.p, ia.data() + u0, m * 4, hipMemcpyHostToDevice), "H2D");
+      check_hip(hipMemcpy(d_b.p, ib.data() + u0, m * 4, hipMemcpyHostToDevice), "H2D");
+      check(sks_intersect_pairs(c, d_words.as<uint64_t>(), d_starts.as<uint64_t>(), d_sizes.as<uint32_t>(),
+                                ew, d_a.as<int32_t>(), d_b.as<int32_t>(), m, d_out.as<int32_t>()));
+      check(sks_ctx_synchronize(c));
+      check_hip(hipMemcpy(res.data() + u0, d_out.p, m * 4, hipMemcpyDeviceToHost), "D2H");
+    }
+  };
+  if (g_pair_devices.empty()) job(0, g_device, ctx());
+  else on_pool(parts, devs, job);
+  if (dense) {  // each (i, j) is written by exactly one tile / row block of one part; the rest are 0
+    for (size_t k = 1; k < parts; ++k)
+      for (uint64_t e = 0; e < n * n; ++e) mats[0][e] += mats[k][e];
+    for (size_t i = 0; i < a.size(); ++i) res[i] = mats[0][(uint64_t)ia[i] * n + ib[i]];
   }
   for (size_t i = 0; i < a.size(); ++i) {
     const bool same = a[i]->mask == b[i]->mask || a[i]->elements.empty() || b[i]->elements.empty();
@@ -335,7 +463,15 @@ void set_device(int device) {
     g_ctx = nullptr;
   }
   g_device = device;
+  g_device_set = true;
 }
+
+void set_devices(const std::vector<int>& devices) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_devices = devices;
+}
+
+std::vector<int> parallel_devices() { return pool_devices(); }
 
 void set_exit_on_io_error(bool exit_on_error) { g_exit_on_io = exit_on_error; }
 void set_hash_flavour(int flavour) { g_flavour = flavour; }
@@ -519,8 +655,35 @@ std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files,
                                                           const kmer_bitset& mask,
                                                           const int window_length,
                                                           const sketch_policy& policy) {
-  return sks::sketch_raw_files(sks::read_files(num_files, fasta_filenames), mask, window_length,
-                               policy);
+  // the reference's cilk_for over files (kmer_set.cpp:112-133) on the node's
+  // GPUs: the files are cut into one contiguous range per device of about equal
+  // bytes, each range parsed and sketched in one batched build on its device
+  const std::vector<std::vector<uint8_t>> raws = sks::read_files(num_files, fasta_filenames);
+  const std::vector<int> devs = sks::pool_devices();
+  const size_t n = raws.size(), parts = std::min(devs.size(), n);
+  if (parts < 2) return sks::sketch_raw_files(raws, mask, window_length, policy);
+  uint64_t total = 0;
+  for (auto& r : raws) total += r.size() + 1;
+  std::vector<size_t> cut(1, 0);  // part k holds files [cut[k], cut[k + 1])
+  uint64_t acc = 0;
+  for (size_t i = 0; i < n && cut.size() < parts; ++i) {
+    acc += raws[i].size() + 1;
+    // close part k once it reaches its share, leaving a file for every later part
+    if (acc * parts >= total * cut.size() && n - (i + 1) >= parts - cut.size()) cut.push_back(i + 1);
+  }
+  while (cut.size() < parts) cut.push_back(cut.back());
+  cut.push_back(n);
+  std::vector<std::vector<kmer_set>> part_out(parts);
+  sks::on_pool(parts, devs, [&](size_t k, int device, sks_ctx* c) {
+    std::vector<const std::vector<uint8_t>*> mine;
+    for (size_t i = cut[k]; i < cut[k + 1]; ++i) mine.push_back(&raws[i]);
+    if (!mine.empty()) part_out[k] = sks::sketch_raw_files(c, device, mine, mask, window_length, policy);
+  });
+  std::vector<kmer_set> out;
+  out.reserve(n);
+  for (auto& po : part_out)
+    for (auto& ks : po) out.push_back(std::move(ks));
+  return out;
 }
 
 namespace {
@@ -721,7 +884,12 @@ std::vector<int> compute_pairwise_kmer_set_intersections(const std::vector<kmer_
 
 std::vector<int> parallel_compute_pairwise_kmer_set_intersections(
     const std::vector<kmer_set*>& kmer_sets_1, const std::vector<kmer_set*>& kmer_sets_2) {
-  return compute_pairwise_kmer_set_intersections(kmer_sets_1, kmer_sets_2);
+  if (kmer_sets_1.size() != kmer_sets_2.size())
+    throw std::runtime_error("Lists of kmer sets for intersection computation have different lengths");
+  std::vector<const kmer_set*> a(kmer_sets_1.begin(), kmer_sets_1.end());
+  std::vector<const kmer_set*> b(kmer_sets_2.begin(), kmer_sets_2.end());
+  sks::PairDevices scope(sks::pool_devices());
+  return sks::pair_counts(a, b);
 }
 
 // ---- fasta_processing.hpp ---------------------------------------------------------------------------------

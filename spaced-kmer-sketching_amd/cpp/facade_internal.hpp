@@ -15,10 +15,12 @@ void check(int rc);
 void check_hip(hipError_t e, const char* what);
 sks_ctx* ctx();  // the facade's context on the selected device (set_device)
 
-// Device buffer owned by the facade (freed on destruction; not copyable).
+// Device buffer owned by the facade (freed on destruction; not copyable), on
+// `device` (-1: the facade's device, set_device).
 struct DevMem {
   void* p = nullptr;
-  explicit DevMem(size_t bytes);
+  int device = 0;
+  explicit DevMem(size_t bytes, int device = -1);
   ~DevMem();
   DevMem(const DevMem&) = delete;
   DevMem& operator=(const DevMem&) = delete;

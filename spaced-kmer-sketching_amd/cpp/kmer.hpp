@@ -383,6 +383,13 @@ std::vector<int> parallel_compute_pairwise_kmer_set_intersections(
 namespace sks {
 // Device used by the facade (default 0); call before the first sketch.
 void set_device(int device);
+// Devices the parallel_* entry points spread their work over (the reference's
+// cilk_for over files and pairs, kmer_set.cpp:112-133,167-184, mapped onto the
+// node's GPUs).  Default: every visible device, or the one set_device chose;
+// the environment variable SKS_FACADE_DEVICES ("0,1,..."; a device may repeat,
+// giving it several contexts) overrides the default.  An empty list restores it.
+void set_devices(const std::vector<int>& devices);
+std::vector<int> parallel_devices();
 // Unreadable FASTA: the reference prints to stderr and exit(1)s
 // (fasta_processing.cpp:86-90).  That is the default here too; pass false to
 // get a std::runtime_error instead.

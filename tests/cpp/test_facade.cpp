@@ -57,7 +57,8 @@ static int sketch(int argc, char** argv) {
   }
   bool same = true;
   for (int i = 0; i < n; ++i) same = same && data[i].elements == serial[i].elements;
-  std::printf("],\"serial_equal\":%s,", same ? "true" : "false");
+  std::printf("],\"serial_equal\":%s,\"devices\":%d,", same ? "true" : "false",
+              (int)sks::parallel_devices().size());
   if (!same) {  // diagnostics: the serial build's sets
     std::printf("\"serial_sets\":[");
     for (int i = 0; i < n; ++i) {

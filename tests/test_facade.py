@@ -39,10 +39,26 @@ def test_facade_missing_file_exits_like_reference(facade_bin, tmp_path):
     assert r.stderr.startswith(f"Unable to open {missing}. \n Exiting...")
 
 
+# SKS_FACADE_DEVICES: the parallel_* entry points spread files and pairs over a
+# device pool; "0,0,0" gives three contexts on the one GPU of the test box, so
+# the split / per-device build / merge in file order runs (kmer_set.cpp:112-133,
+# 167-184) and must equal the serial entry points and the oracle
+POOLS = [None, "0,0,0"]
+
+
+def _env(pool):
+    env = dict(os.environ)
+    env.pop("SKS_FACADE_DEVICES", None)
+    if pool:
+        env["SKS_FACADE_DEVICES"] = pool
+    return env
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("pool", POOLS)
 @pytest.mark.parametrize("w,k,seed,param,kind", [(21, 21, 0, 200, "frac"), (31, 21, 0, 50, "frac"),
                                                  (31, 21, 3, 300, "bottom"), (40, 30, 0, 40, "frac")])
-def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
+def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind, pool):
     files = []
     for i in range(4):
         g = synth.bases(30000, seed=77, mut_seed=500 + i, mut_rate=0.01 * i)
@@ -52,7 +68,7 @@ def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
         p.write_bytes(synth.fasta_text([(f"g{i}_a", g[:17000]), (f"g{i}_b", g[17000:])], width=70))
         files.append(str(p))
     r = subprocess.run([facade_bin, "sketch", str(w), str(k), str(seed), str(param), kind] + files,
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=_env(pool))
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     m = O.mask(w, k, seed)
@@ -68,6 +84,8 @@ def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
     assert out["inter"] == inter
     for flag in ("serial_equal", "inter_serial_equal", "runs_equal", "cut_equal"):
         assert out[flag], flag
+    if pool:
+        assert out["devices"] == 3
     assert out["single01"] == inter[1]
     kk = bin(m).count("1") // 2
     assert out["k"] == kk
@@ -77,8 +95,9 @@ def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pool", POOLS)
 @pytest.mark.parametrize("w,k,param", [(31, 21, 10), (40, 30, 5)])
-def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param):
+def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param, pool):
     """70 sets: the all-pairs list of generate_all_pairs_from_vector covers the
     whole matrix, so the facade counts it with the symmetric join
     (sks_intersect_sym) and gathers; counts and ANI equal the oracle's."""
@@ -89,7 +108,7 @@ def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param):
         p.write_bytes(synth.fasta_text([(f"h{i}", g)], width=60))
         files.append(str(p))
     r = subprocess.run([facade_bin, "sketch", str(w), str(k), "0", str(param), "frac"] + files,
-                       capture_output=True, text=True, timeout=300)
+                       capture_output=True, text=True, timeout=300, env=_env(pool))
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     m = O.mask(w, k, 0)
@@ -98,6 +117,8 @@ def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param):
     inter = [O.intersect(sk[i], sk[j]) for i in range(n) for j in range(n)]
     assert out["inter"] == inter
     assert out["inter_serial_equal"]
+    if pool:
+        assert out["devices"] == 3
 
 
 REF_CALLER = os.path.join(ROOT, "tests", "cpp", "build", "ref_caller")
