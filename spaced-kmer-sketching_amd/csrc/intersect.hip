@@ -380,9 +380,6 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 // workgroup streams the column block in coalesced chunks of whole buckets
 // that fit the table (<= kJCap elements; a larger bucket is cut into
 // sub-chunks) and the row block's same buckets with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
-#ifndef SKS_JOIN_HITS_SPLIT  // hit loop over the 64-bit mask (0) or its 32-bit halves (1, 2)
-#define SKS_JOIN_HITS_SPLIT 0
-#endif
 #ifndef SKS_JOIN_DIAG  // diagnostics only (wrong counts): 1 no probes / hit adds,
 #define SKS_JOIN_DIAG 0  // 2 no count flush, 4 probes without hit adds
 #endif
@@ -738,40 +735,11 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   auto add_hits = [&](uint32_t r, unsigned long long m) {
     m = (m >> lane) | (lane ? m << (64 - lane) : 0ull);
     uint32_t* crow = &s_cnt[r * kCntLd];
-#if SKS_JOIN_HITS_SPLIT == 0
     while (m) {
       const uint32_t c = ((uint32_t)__builtin_ctzll(m) + lane) & 63;
       m &= m - 1;
       atomicAdd(&crow[c], 1u);
     }
-#else
-    uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
-#if SKS_JOIN_HITS_SPLIT == 1
-    while (lo) {
-      const uint32_t c = ((uint32_t)__builtin_ctz(lo) + lane) & 63;
-      lo &= lo - 1;
-      atomicAdd(&crow[c], 1u);
-    }
-    while (hi) {
-      const uint32_t c = ((uint32_t)__builtin_ctz(hi) + lane + 32) & 63;
-      hi &= hi - 1;
-      atomicAdd(&crow[c], 1u);
-    }
-#else
-    while (lo | hi) {
-      if (lo) {
-        const uint32_t c = ((uint32_t)__builtin_ctz(lo) + lane) & 63;
-        lo &= lo - 1;
-        atomicAdd(&crow[c], 1u);
-      }
-      if (hi) {
-        const uint32_t c = ((uint32_t)__builtin_ctz(hi) + lane + 32) & 63;
-        hi &= hi - 1;
-        atomicAdd(&crow[c], 1u);
-      }
-    }
-#endif
-#endif
   };
   // columns holding v (0 if none)
   auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
