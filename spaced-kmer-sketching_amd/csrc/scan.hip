@@ -395,6 +395,9 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
       ulonglong2* cb = s_cand + __builtin_amdgcn_readfirstlane(tid >> 6) * kCandCap;
       const uint32_t pmask = p.low_mask & 0xFu;
       const uint32_t kbits = (uint32_t)p.kconst & pmask;
+      // low bits of c = 2^s * d the pre-filter has not tested (none when s <= 4):
+      // a finished candidate needs only d | fmh then
+      const uint32_t rest_lo = p.low_mask & ~0xFu, rest_hi = p.high_mask;
       uint32_t cnt = 0;  // wave-uniform
       auto finish = [&](uint32_t n) {  // candidates [0, n), n <= 64
         __builtin_amdgcn_wave_barrier();
@@ -402,8 +405,11 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
           const ulonglong2 e = cb[lane];
           uint64_t y = mul_const<kMixMul>(e.x);
           y ^= y >> 28;
-          if (div_test(y ^ p.kconst, p.low_mask, p.high_mask, p.dinv, p.dlim))
-            emit<MODE>(p, q, g.seg, e.y, 0);
+          const uint64_t f = y ^ p.kconst;
+          bool keep = mul_uniform(f, p.dinv) <= p.dlim;
+          if (rest_lo | rest_hi)  // wave-uniform
+            keep = keep && ((((uint32_t)f & rest_lo) | ((uint32_t)(f >> 32) & rest_hi)) == 0);
+          if (keep) emit<MODE>(p, q, g.seg, e.y, 0);
         }
         __builtin_amdgcn_wave_barrier();
       };

@@ -125,6 +125,22 @@ def test_frac_narrow_windows(torch_cuda, ctx, w, k):
             check_against_oracle(ss, genomes, w, m, "frac", c, flavour)
 
 
+def test_frac_prefilter_even_c(torch_cuda, ctx):
+    """The low-bits pre-filter kernel (scan_kernel<frac, 0, PRE>, even c) with
+    c = 2^s * d for s below, at and above the 4 pre-filtered bits (the finished
+    candidates test the remaining low bits only when s > 4), d = 1, and s >= 32
+    (the high-word test): every sketch equals the oracle's (kmer.hpp:135-149,
+    kmer-sketching.cpp:29-34 with c in place of 200)."""
+    w, k = 31, 21
+    genomes = _genomes(w, [0, 30, 4097, 90000, 400000], lower=True)
+    m = O.mask(w, k, 0)
+    for c in (2, 6, 16, 96, 1000, 1024, 3 << 20, 1 << 33):
+        ss, _ = build(torch_cuda, ctx, genomes, w, m, "frac", c, 0)
+        check_against_oracle(ss, genomes, w, m, "frac", c, 0)
+        if c <= 1000:
+            assert int(ss.sizes()[4]) > 0, c
+
+
 @pytest.mark.parametrize("w,k", [(33, 33), (40, 21), (50, 40), (63, 30), (64, 64)])
 def test_frac_wide_windows(torch_cuda, ctx, w, k):
     genomes = _genomes(w, [0, w, 4096 + w, 30000, 70001], lower=True)
