@@ -800,7 +800,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-c3-sharded", action="store_true")
     ap.add_argument("--no-c2", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--sweep-inflight", type=int, default=2,
+                    help="config-5 seeds in flight (one context + HIP stream each)")
+    ap.add_argument("--inflight", type=int, default=3,
                     help="config-3 builds in flight (one context + HIP stream each)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--dist-rehearsal", action="store_true",
@@ -884,7 +886,7 @@ def main():
     sweep = None
     if not args.no_sweep:
         sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1,
-                               lanes_n=args.inflight)
+                               lanes_n=args.sweep_inflight)
 
     cpu = cpu_x = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
