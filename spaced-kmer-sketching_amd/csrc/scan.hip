@@ -133,17 +133,8 @@ __device__ __forceinline__ void pack16(const uint32_t (&x)[5], uint32_t sb, uint
   for (int k = 0; k < 4; ++k) {
     w[k] = funnel(x[k + 1], x[k], sb);  // alignbit by 0 returns x[k]
     const uint32_t low = w[k] | 0x20202020u;
-#if SKS_PACK_PERM
-    // the low 3 bits of A/a C/c G/g T/t are 1 3 7 4: one v_perm per table
-    // gives the codes and the expected lower-case letters (0 elsewhere, which
-    // never equals a byte with bit 5 set)
-    const uint32_t idx = w[k] & 0x07070707u;
-    const uint32_t code = __builtin_amdgcn_perm(0x02000003u, 0x01000000u, idx);
-    const uint32_t expect = __builtin_amdgcn_perm(0x67000074u, 0x63006100u, idx);
-#else
     const uint32_t code = ((low >> 1) ^ (low >> 2)) & 0x03030303u;
     const uint32_t expect = __builtin_amdgcn_perm(0u, 0x74676361u, code);
-#endif
     sad = __builtin_amdgcn_sad_u8(low, expect, sad);
     g[k] = code * 0x01041040u;  // gathered codes in bits 24..31
   }
@@ -277,32 +268,15 @@ constexpr int kBeOff = 2;  // s_be[kBeOff + i] = word i; two zero words in front
 
 constexpr uint32_t kCandCap = 128;  // pre-filter candidates per wave (< 64 + 64)
 
-#ifndef SKS_PACK_PERM
-#define SKS_PACK_PERM 0
-#endif
-#ifndef SKS_SCAN_ALIAS
-#define SKS_SCAN_ALIAS 0
-#endif
-
 template <int MODE, int FLAVOUR, int PRE = 0>
 __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanParams p) {
-#if SKS_SCAN_ALIAS
-  // the raw tile bytes (read by the pack) and the pre-filter candidates (the
-  // windows) are never live together: the candidates are finished before the
-  // tile ends and the next tile's bytes are stored after a barrier
-  constexpr int kRawBytes = kLoadVecs * 16, kCandBytes = (PRE ? (kBlock / 64) * kCandCap : 1) * 16;
-  __shared__ ulonglong2 s_share[(kRawBytes > kCandBytes ? kRawBytes : kCandBytes) / 16];
-  uint32_t* const s_raw = reinterpret_cast<uint32_t*>(s_share);
-  ulonglong2* const s_cand = s_share;
-#else
   __shared__ uint32_t s_raw[kLoadVecs * 4];
-  // (z, c) of windows past the low-bits pre-filter, per wave (PRE only)
-  __shared__ ulonglong2 s_cand[PRE ? (kBlock / 64) * kCandCap : 1];
-#endif
   __shared__ uint32_t s_be[kWords + 2 + kBeOff];
   __shared__ uint32_t s_lc[kWords + 2];
   __shared__ uint32_t s_inv[kWords + 2];
   __shared__ Queue<MODE> q;
+  // (z, c) of windows past the low-bits pre-filter, per wave (PRE only)
+  __shared__ ulonglong2 s_cand[PRE ? (kBlock / 64) * kCandCap : 1];
 
   const int tid = threadIdx.x;
   const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
