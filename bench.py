@@ -269,7 +269,12 @@ def run_end_to_end_overlapped(ctx, mask, host, ref, steps, pieces=8):
     big = max(lens)
     slots = [torch.empty(big, dtype=torch.uint8, device="cuda") for _ in range(2)]
     rec = torch.empty(big + 1, dtype=torch.uint8, device="cuda")
-    copy_stream = torch.cuda.Stream()
+    # HIP maps streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues, so
+    # a copy stream of normal priority can share the compute stream's queue (it
+    # did after the config-3 and config-2 legs had taken six pool streams: every
+    # copy then waited behind a piece's kernels, 78 instead of 57 ms); a
+    # high-priority stream comes from a queue pool of its own
+    copy_stream = torch.cuda.Stream(priority=-1)
     ev = [torch.cuda.Event() for _ in range(2)]
     cat = torch.empty(2 * len(ref) + 4096, dtype=torch.int64, device="cuda")
     uni = torch.empty_like(cat)

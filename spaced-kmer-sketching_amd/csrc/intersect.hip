@@ -745,6 +745,9 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
 
   for (int i = tid; i < kFSlots / 4; i += kJB)
     reinterpret_cast<uint4*>(s_slot)[i] = make_uint4(kFFree, kFFree, kFFree, kFFree);
+  // a tile on the diagonal: row block = column block, in the same layout (rows
+  // taken from a separate layout start off a block boundary, so never match)
+  const bool self_tile = row0 == col0;
 #if SKS_JOIN_BITSLICE
   for (int i = tid; i < kPlanes * kTile / 2; i += kJB) reinterpret_cast<uint4*>(s_pl)[i] = make_uint4(0, 0, 0, 0);
   __shared__ uint32_t s_top;  // planes used (the highest carry chain)
@@ -752,7 +755,6 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   // its own column: those self-hits are counted per row with plain adds, outside
   // the carry chains (unrelated sketches would otherwise run a chain per element)
   __shared__ uint32_t s_self[kTile];
-  const bool self_tile = row0 == col0;
   if (tid < kTile) s_self[tid] = 0;
   if (tid == 0) s_top = 0;
   uint32_t top = 0;
@@ -822,8 +824,14 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
     auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
     uint32_t bs = wb, be = chunk_end(wb);
     uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
+    // a chunk of whole buckets of a diagonal tile needs no row elements: its
+    // rows are its columns (step 2 below)
+    auto rows_end = [&](uint32_t bs_, uint32_t be_, uint32_t cs_, uint32_t ce_) {
+      const bool whole = cs_ == s_coff[bs_ - wb] && ce_ == s_coff[be_ - wb];
+      return self_tile && whole ? s_roff[bs_ - wb] : s_roff[be_ - wb];
+    };
     JoinChunk cur;
-    join_fetch(cdata, cids, rdata, rids, cs, ce, s_roff[0], s_roff[be - wb], tid, cur);
+    join_fetch(cdata, cids, rdata, rids, cs, ce, s_roff[0], rows_end(bs, be, cs, ce), tid, cur);
     while (bs < we) {
       const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
       __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // this chunk's elements have landed
@@ -840,7 +848,8 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       nce = min(s_coff[nbe - wb], ncs + a.cap);
       JoinChunk nxt;
       if (nbs < we)
-        join_fetch(cdata, cids, rdata, rids, ncs, nce, s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
+        join_fetch(cdata, cids, rdata, rids, ncs, nce, s_roff[nbs - wb], rows_end(nbs, nbe, ncs, nce), tid,
+                   nxt);
 
       // 0) free the previous chunk's slots (its probes are done: barrier below
       //    the probe loop) and stage this chunk's entries
@@ -854,10 +863,11 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       __syncthreads();
       // 1) insert: one 32-bit compare-swap per element; a value already
       //    present adds its column bit to the entry the slot names
-      uint32_t hs[kJMade], prev[kJMade], tags[kJMade];
+      uint32_t hs[kJMade], prev[kJMade], tags[kJMade], ent[kJMade];
 #pragma unroll
       for (int u = 0; u < kJMade; ++u) {
         hs[u] = kNoSlot;
+        ent[u] = 0;
         const uint32_t e = tid + kJB * u;
         if (cs + e < ce) {
           hs[u] = fp_slot(cur.cv[u]);
@@ -874,10 +884,12 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
         for (;;) {
           if (x == kFFree) {
             made[u] = h;
+            ent[u] = e;
             break;
           }
           if ((x >> 10) == tags[u] && s_ent[x & 1023u].x == v) {
             atomicOr(&s_ent[x & 1023u].y, 1ull << cur.cid[u]);
+            ent[u] = x & 1023u;
             break;
           }
           h = (h + 1) & (kFSlots - 1);
@@ -886,7 +898,28 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       }
       __syncthreads();
       JSTAMP(1);
-      // 2) probe with the row elements: first slots read together
+      // 2) probe with the row elements: first slots read together. A diagonal
+      //    tile's chunk of whole buckets has the column elements as its row
+      //    elements: each one's hits are the final mask of the entry it joined
+      if (self_tile && cs == s_coff[bs - wb] && ce == s_coff[be - wb]) {
+#pragma unroll
+        for (int u = 0; u < kJMade; ++u) {
+          const uint32_t r = cur.cid[u];
+          if (hs[u] == kNoSlot || r >= r_valid) continue;
+          const unsigned long long m = s_ent[ent[u]].y;
+          if (SKS_JOIN_DIAG & 1) continue;
+          if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
+          add_hits(r, m);
+        }
+        __syncthreads();
+        JSTAMP(2);
+        cur = nxt;
+        bs = nbs;
+        be = nbe;
+        cs = ncs;
+        ce = nce;
+        continue;
+      }
       uint32_t sl[kJRowPf], sh[kJRowPf];
 #pragma unroll
       for (int u = 0; u < kJRowPf; ++u) {

@@ -496,6 +496,12 @@ def test_many_sketches_tiled_and_symmetric(torch_cuda, kernel_ctx):
     ctx.intersect_all(data, starts, sizes, 1, n, 0, n, out.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().reshape(n, n), want)
+    # block-aligned rows ending inside a block: the diagonal tile (rows 64..69
+    # against columns 64..127) joins without probes and must skip rows >= 70
+    rows = torch.zeros(((70 - 64) * n,), dtype=torch.int32, device="cuda:0")
+    ctx.intersect_all(data, starts, sizes, 1, n, 64, 70, rows.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(rows.cpu().numpy().reshape(6, n), want[64:70])
     rows = torch.zeros(((70 - 65) * n,), dtype=torch.int32, device="cuda:0")
     ctx.intersect_all(data, starts, sizes, 1, n, 65, 70, rows.data_ptr())
     torch.cuda.synchronize()

@@ -3,7 +3,7 @@ host memory -> H2D -> device parse -> sketch): the serial and overlapped
 timings of bench.run_end_to_end, then the overlapped step once more with host
 timestamps per piece (copy wait, parse, sketch, export, free) and the copy
 stream's own event time per piece, to see where the overlap is lost.
-    python tools/bench_e2e.py [steps]"""
+    python tools/bench_e2e.py [steps] [c2]   (c2: run bench's config-2 leg first)"""
 import os
 import sys
 import time
@@ -22,6 +22,8 @@ def main():
     ctx = sksffi.Context(0)
     mask = sksffi.mask_generate(bench.W, bench.K, bench.MASK_SEED)
     buf, n_bytes = bench.make_c3(ctx, seed_base=3)
+    if "c2" in sys.argv[2:]:
+        bench.run_c2(ctx, mask, steps=4, warmup=1, inflight=3)
     res = bench.run_end_to_end(ctx, mask, buf, steps)
     print("serial ms", round(res["ms"], 2), {k: round(v, 2) for k, v in res["ms_phases"].items()},
           "overlapped ms", round(res["overlapped"]["ms"], 2), flush=True)
@@ -53,10 +55,12 @@ def main():
     rec = torch.empty(max(lens) + 1, dtype=torch.uint8, device="cuda")
     cs = torch.cuda.Stream()
     ws = torch.cuda.Stream()  # the instrumented context's own stream (free_on_stream)
-    ctx = sksffi.Context(0, ws.cuda_stream)
+    main_ctx = ctx
+    sctx = sksffi.Context(0, ws.cuda_stream)
     ev_b = [torch.cuda.Event(enable_timing=True) for _ in lens]
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in lens]
-    for free_mode in ("free", "free_on_stream", "keep"):
+    for free_mode, ctx in (("free", main_ctx), ("free", sctx), ("free_on_stream", sctx),
+                           ("keep", sctx)):
         for rep in range(2):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -94,7 +98,7 @@ def main():
             keep.clear()
             torch.cuda.synchronize()
             copy_ms = [ev_b[p].elapsed_time(ev_e[p]) for p in range(len(lens))]
-            print(f"[{free_mode} rep {rep}] total {tot:.1f} ms; copy-stream ms per piece "
+            print(f"[{free_mode} {'null-stream ctx' if ctx is main_ctx else 'stream ctx'} rep {rep}] total {tot:.1f} ms; copy-stream ms per piece "
                   f"{[round(x, 1) for x in copy_ms]}", flush=True)
             for r in rows:
                 print("   piece %d: wait-copy %.2f parse %.2f sketch %.2f sizes %.2f free %.2f" % r, flush=True)
