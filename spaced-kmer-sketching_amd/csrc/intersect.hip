@@ -401,16 +401,12 @@ constexpr int kJCap = 1024;                  // column elements per chunk
 constexpr int kJMade = kJCap / kJB;         // column elements per thread per chunk
 constexpr int kJWin = 256;                  // bucket offsets staged per window
 constexpr uint32_t kJMaxLogB = 14;          // B <= 16384 (LDS histogram of k_hb_count)
-[[maybe_unused]] constexpr int kCntLd = kTile + 1;
-// Hit counts as bit-sliced counters (SKS_JOIN_BITSLICE, default): plane b of
+// Hit counts as bit-sliced counters: plane b of
 // tile row r is the 64-bit word of bit b of the row's 64 column counts, and a
 // hit with column mask m is a carry chain of atomic XORs (m &= old after each
 // plane: a plane bit that was set carries).  A mask of k columns then costs
-// about log2(k) + 2 LDS atomics instead of k (the 32-bit counter matrix,
-// SKS_JOIN_BITSLICE=0).
-#ifndef SKS_JOIN_BITSLICE
-#define SKS_JOIN_BITSLICE 1
-#endif
+// about log2(k) + 2 LDS atomics instead of k (a 32-bit count matrix with one
+// ds_add per set bit, rounds 1-2: 0.653 -> 0.604 ms on config 4).
 constexpr int kPlanes = 32;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
@@ -712,11 +708,7 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
 #endif
   __shared__ uint32_t s_slot[kFSlots];
   __shared__ ulonglong2 s_ent[kJCap];  // {value, mask of the columns holding it}
-#if SKS_JOIN_BITSLICE
   __shared__ unsigned long long s_pl[kPlanes * kTile];  // plane b of row r at [b * 64 + r]
-#else
-  __shared__ uint32_t s_cnt[kTile * kCntLd];
-#endif
   __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
   __shared__ uint16_t s_next[kJWin];
 
@@ -748,7 +740,6 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   // a tile on the diagonal: row block = column block, in the same layout (rows
   // taken from a separate layout start off a block boundary, so never match)
   const bool self_tile = row0 == col0;
-#if SKS_JOIN_BITSLICE
   for (int i = tid; i < kPlanes * kTile / 2; i += kJB) reinterpret_cast<uint4*>(s_pl)[i] = make_uint4(0, 0, 0, 0);
   __shared__ uint32_t s_top;  // planes used (the highest carry chain)
   // A tile on the diagonal (row block = column block) finds every row element in
@@ -768,18 +759,6 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
     for (; m && b < kPlanes; ++b) m &= atomicXor(p + b * kTile, m);
     top = max(top, b);
   };
-#else
-  for (int i = tid; i < kTile * kCntLd; i += kJB) s_cnt[i] = 0;
-  auto add_hits = [&](uint32_t r, unsigned long long m) {
-    m = (m >> lane) | (lane ? m << (64 - lane) : 0ull);
-    uint32_t* crow = &s_cnt[r * kCntLd];
-    while (m) {
-      const uint32_t c = ((uint32_t)__builtin_ctzll(m) + lane) & 63;
-      m &= m - 1;
-      atomicAdd(&crow[c], 1u);
-    }
-  };
-#endif
   // columns holding v (0 if none)
   auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
     const uint32_t tag = fp_tag(v);
@@ -961,7 +940,6 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   JSTAMP(5);
   if (SKS_JOIN_DIAG & 4) atomicAdd(&s_slot[0], diag_acc);
   if (SKS_JOIN_DIAG & 2) return;
-#if SKS_JOIN_BITSLICE
   // planes the carry chains reached (unrelated tiles: none or one)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) top = max(top, (uint32_t)__shfl_xor(top, o, 64));
@@ -973,11 +951,6 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
     uint32_t cnt = 0;
     for (int b = 0; b < np; ++b) cnt |= (uint32_t)((s_pl[b * kTile + r] >> c) & 1ull) << b;
     if (self_tile && c == r) cnt += s_self[r];
-#else
-  for (int i = tid; i < kTile * kTile; i += kJB) {
-    const uint32_t r = i >> 6, c = i & 63;
-    const uint32_t cnt = s_cnt[r * kCntLd + c];
-#endif
     if (!cnt) continue;
     const uint32_t gr = row0 + r, gc = col0 + c;
     if (gr >= row_lim || gc >= a.n) continue;
