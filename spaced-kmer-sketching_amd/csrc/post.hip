@@ -441,11 +441,21 @@ template <int ITEMS>
 using FuseSort = rocprim::block_radix_sort<unsigned long long, kSelB, ITEMS, rocprim::empty_type, 1, 1,
                                            SKS_FUSE_RADIX_BITS,
                                            rocprim::block_radix_rank_algorithm::SKS_FUSE_RANK>;
+// The sort is a counting sort on the top kBkLog bits of the packed keys (4096
+// buckets, four per thread) followed by an insertion sort of each thread's
+// buckets in LDS; rocPRIM's block radix sort — whose LDS exchange is 74% bank
+// conflicts and 0.24 of the kernel's 0.54 ms on config 4 — remains the
+// fallback when a bucket holds more than kBkMax keys (keys crowding a few top
+// bit patterns, e.g. low-complexity sequence).
+constexpr int kBkLog = 12;
+constexpr uint32_t kBk = 1u << kBkLog;
+constexpr uint32_t kBkPer = kBk / kSelB;
+constexpr uint32_t kBkMax = 64;
 template <int ITEMS>
 constexpr size_t fuse_lds() {
-  return sizeof(typename FuseSort<ITEMS>::storage_type) > kSelB * ITEMS * sizeof(uint64_t)
-             ? sizeof(typename FuseSort<ITEMS>::storage_type)
-             : kSelB * ITEMS * sizeof(uint64_t);
+  constexpr size_t rp = sizeof(typename FuseSort<ITEMS>::storage_type);
+  constexpr size_t cs = kSelB * ITEMS * sizeof(uint64_t) + kBk * sizeof(uint32_t);  // keys + buckets
+  return rp > cs ? rp : cs;
 }
 
 template <int FLAVOUR, int ITEMS>
@@ -479,7 +489,78 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     const uint32_t i = tid * ITEMS + j;
     k[j] = i < n ? runs_pack(rec[base + i], runs) : ~0ull;  // pads sort after equal keys
   }
-  FuseSort<ITEMS>().sort(k, sort_storage, 0, key_bits);
+  {
+    uint64_t* skeys = reinterpret_cast<uint64_t*>(smem);
+    uint32_t* sbin = reinterpret_cast<uint32_t*>(smem + kCap * sizeof(uint64_t));
+    const int shift = key_bits > kBkLog ? key_bits - kBkLog : 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kBkPer; ++q) sbin[tid * kBkPer + q] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < ITEMS; ++j)
+      if (tid * ITEMS + j < n) atomicAdd(&sbin[(uint32_t)(k[j] >> shift)], 1u);
+    __syncthreads();
+    uint32_t cb[kBkPer], sum = 0, mx = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kBkPer; ++q) {
+      cb[q] = sbin[tid * kBkPer + q];
+      sum += cb[q];
+      mx = cb[q] > mx ? cb[q] : mx;
+    }
+    // exclusive scan of the per-thread sums and the largest bucket, block-wide
+    const int lane = tid & 63, wave = tid >> 6;
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+    if (lane == 63) wsum[wave] = inc;
+    if (lane == 0) hist[wave] = mx;  // hist[] is free until the select
+    __syncthreads();
+    uint32_t excl = inc - sum, bmax = 0;
+#pragma unroll
+    for (int w = 0; w < kSelWaves; ++w) {
+      excl += w < wave ? wsum[w] : 0u;
+      bmax = hist[w] > bmax ? hist[w] : bmax;
+    }
+    __syncthreads();
+    if (bmax > kBkMax) {  // uniform: the keys are still in registers
+      FuseSort<ITEMS>().sort(k, sort_storage, 0, key_bits);
+    } else {
+      uint32_t run = excl;
+#pragma unroll
+      for (uint32_t q = 0; q < kBkPer; ++q) {  // bucket cursors
+        sbin[tid * kBkPer + q] = run;
+        run += cb[q];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < ITEMS; ++j)
+        if (tid * ITEMS + j < n) skeys[atomicAdd(&sbin[(uint32_t)(k[j] >> shift)], 1u)] = k[j];
+      __syncthreads();
+      // this thread's buckets are the contiguous range [excl, excl + sum); keys
+      // of earlier buckets are smaller, so an insertion sort of the range only
+      // moves keys within their bucket
+      for (uint32_t i = excl + 1; i < excl + sum; ++i) {
+        const uint64_t key = skeys[i];
+        uint32_t j = i;
+        while (j > excl && skeys[j - 1] > key) {
+          skeys[j] = skeys[j - 1];
+          --j;
+        }
+        skeys[j] = key;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < ITEMS; ++j) {
+        const uint32_t i = tid * ITEMS + j;
+        k[j] = i < n ? skeys[i] : ~0ull;
+      }
+    }
+  }
   s_last[tid] = k[ITEMS - 1];
   __syncthreads();
   const unsigned long long before = tid ? s_last[tid - 1] : 0ull;

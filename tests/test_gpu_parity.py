@@ -176,6 +176,26 @@ def test_bottom_s_many_genomes(torch_cuda, ctx):
             check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
 
 
+def test_bottom_s_fused_sort_paths(torch_cuda, ctx):
+    """k_bottom_fused sorts each genome's candidates by a counting sort on the
+    top 12 packed-key bits plus per-bucket insertion sorts, and falls back to
+    rocPRIM's block radix sort when a bucket holds more than 64 keys. A genome
+    of only A and C crowds its canonical k-mers into 2^6 of the 4096 buckets
+    (fallback); the others are ordinary (bucket sort), one repeats a 5 kb
+    stretch many times (equal keys in a bucket); all in one launch, both
+    flavours, against the oracle."""
+    rng = np.random.default_rng(77)
+    ac = np.where(rng.random(200_000) < 0.5, ord("A"), ord("C")).astype(np.uint8).tobytes()
+    rep = synth.bases(5000, seed=78).tobytes()
+    genomes = [ac, synth.bases(150_000, seed=79).tobytes(), rep * 30 + synth.bases(80_000, seed=80).tobytes(),
+               synth.bases(120_000, seed=81, mut_seed=82, mut_rate=0.02).tobytes()]
+    m = O.mask(31, 21, 0)
+    for flavour in (0, 1):
+        for s_ in (2000, 10000):
+            ss, _ = build(torch_cuda, ctx, genomes, 31, m, "bottom", s_, flavour)
+            check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
+
+
 def test_bottom_s_unfused_paths(torch_cuda, ctx, monkeypatch):
     """The per-genome fused post kernel is the default for builds of two or more
     genomes of <= 16384 candidates (a single genome takes the device-wide path);
