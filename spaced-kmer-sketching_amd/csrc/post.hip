@@ -292,6 +292,24 @@ __device__ __forceinline__ uint32_t block_rank(bool p, uint32_t* wsum, uint32_t*
   return before + in_wave;
 }
 
+// exclusive block scan of one count per thread (wsum: kSelWaves words)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t before = inc - v;
+#pragma unroll
+  for (int w = 0; w < kSelWaves; ++w) before += w < wave ? wsum[w] : 0u;
+  __syncthreads();
+  return before;
+}
+
 // Block-wide maximum of one value per thread (wsum64: kSelWaves words).
 __device__ __forceinline__ uint64_t block_max(uint64_t v, uint64_t* wsum64) {
 #pragma unroll
@@ -425,8 +443,7 @@ __global__ __launch_bounds__(kSelB) void k_bottom_select(const uint64_t* __restr
 // in-order compaction. Replaces compaction + segmented sort + unique + scatter
 // + select (five kernels and a host sync) for genomes of <= kFuseCap candidates.
 // res[g] = sketch size, or ~0 when the genome has fewer than s distinct
-// candidates under a finite threshold (the build retries it). The sorted
-// packed keys are written back over the record region.
+// candidates under a finite threshold (the build retries it).
 // ITEMS keys per thread (8, 12 or 16): the smallest that holds the pass's
 // largest genome, so that padding is not sorted (pads cost as much as keys).
 constexpr uint32_t kFuseMaxItems = 16;
@@ -571,7 +588,6 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     const uint32_t i = tid * ITEMS + j;
     const bool is_dup = i > 0 && k[j] == (j ? k[j - 1] : before);
     const bool valid = i < n && !is_dup;
-    if (i < n) rec[base + i] = k[j];
     fv[j] = valid ? hash_bitset128<FLAVOUR>(runs_expand(k[j], runs), 0) ^ kconst : 0ull;
     mine += valid ? 1u : 0u;
     dmask |= (valid ? 0u : 1u) << j;
@@ -616,22 +632,29 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     mx = block_max(mx, wsum64);
     sel = radix_select(f, n, (uint32_t)lim, mx, valid_at, hist, s_sel);
   }
-  // keep (all distinct) or the selected ones, in k-mer order
-  uint32_t eq_base = 0, out_base = 0;
-  for (uint32_t b0 = 0; b0 < n; b0 += kSelB) {
-    const uint32_t i = b0 + tid;
-    const bool ok = valid_at(i);
-    const uint64_t v = ok ? f[i] & sel.pmask : ~0ull;
+  // keep (all distinct) or the selected ones, in k-mer order: the sorted keys,
+  // their fmh and validity are in registers in blocked order (thread t holds
+  // positions t * ITEMS ..), so two block scans place them — the ties at the
+  // selected digit (the first kk in k-mer order) and the kept ones
+  uint32_t lt_m = 0, eq_m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < ITEMS; ++j) {
+    const bool ok = !((dmask >> j) & 1u);
+    const uint64_t v = fv[j] & sel.pmask;
     const bool eq = ok && !all && !sel.whole && v == sel.prefix;
-    uint32_t eq_tot, keep_tot;
-    const uint32_t eq_rank = eq_base + block_rank(eq, wsum, &eq_tot);
-    const bool keep =
-        ok && (all || v < sel.prefix || (v == sel.prefix && (sel.whole || eq_rank < sel.kk)));
-    const uint32_t pos = out_base + block_rank(keep, wsum, &keep_tot);
-    if (keep) dst[pos] = runs_expand(rec[base + i], runs);
-    eq_base += eq_tot;
-    out_base += keep_tot;
+    const bool lt = ok && (all || v < sel.prefix || (v == sel.prefix && sel.whole));
+    lt_m |= (lt ? 1u : 0u) << j;
+    eq_m |= (eq ? 1u : 0u) << j;
   }
+  uint32_t eq_rank = block_excl_scan((uint32_t)__builtin_popcount(eq_m), wsum);
+  uint32_t keep_m = lt_m;
+#pragma unroll
+  for (uint32_t j = 0; j < ITEMS; ++j)
+    if ((eq_m >> j) & 1u) keep_m |= (eq_rank++ < sel.kk ? 1u : 0u) << j;
+  uint32_t pos = block_excl_scan((uint32_t)__builtin_popcount(keep_m), wsum);
+#pragma unroll
+  for (uint32_t j = 0; j < ITEMS; ++j)
+    if ((keep_m >> j) & 1u) dst[pos++] = runs_expand(k[j], runs);
 }
 
 template <int FLAVOUR>
