@@ -339,20 +339,18 @@ struct RadixSel {
   uint32_t kk;
   bool whole;
 };
-template <class Valid>
-__device__ __forceinline__ RadixSel radix_select(const uint64_t* f, uint32_t n, uint32_t kk,
-                                                 uint64_t vmax, Valid valid, uint32_t* hist,
-                                                 uint32_t* s_sel) {
+// count(shift, prefix, pmask) adds this thread's values v with (v & pmask) ==
+// prefix to hist[(v >> shift) & 255].
+template <class Count>
+__device__ __forceinline__ RadixSel radix_select_by(Count count, uint32_t kk, uint64_t vmax,
+                                                    uint32_t* hist, uint32_t* s_sel) {
   const int tid = threadIdx.x;
   RadixSel r{0, 0, kk, false};
   const int top = vmax ? 63 - __builtin_clzll(vmax) : 0;
   for (int shift = (top / 8) * 8; shift >= 0; shift -= 8) {
     for (int i = tid; i < 256; i += kSelB) hist[i] = 0;
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kSelB) {
-      const uint64_t v = f[i];
-      if (valid(i) && (v & r.pmask) == r.prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
-    }
+    count(shift, r.prefix, r.pmask);
     __syncthreads();
     if (tid < 64) {  // wave 0: the digit where the running count reaches kk
       uint32_t h4[4], sum = 0;
@@ -387,6 +385,21 @@ __device__ __forceinline__ RadixSel radix_select(const uint64_t* f, uint32_t n, 
     }
   }
   return r;
+}
+
+// The same over values f[i], i < n, with valid(i), in LDS (striped).
+template <class Valid>
+__device__ __forceinline__ RadixSel radix_select(const uint64_t* f, uint32_t n, uint32_t kk,
+                                                 uint64_t vmax, Valid valid, uint32_t* hist,
+                                                 uint32_t* s_sel) {
+  return radix_select_by(
+      [&](int shift, uint64_t prefix, uint64_t pmask) {
+        for (uint32_t i = threadIdx.x; i < n; i += kSelB) {
+          const uint64_t v = f[i];
+          if (valid(i) && (v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+        }
+      },
+      kk, vmax, hist, s_sel);
 }
 
 template <int FLAVOUR>
@@ -488,8 +501,6 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   constexpr uint32_t kCap = kSelB * ITEMS;
   extern __shared__ unsigned char smem[];
   auto& sort_storage = *reinterpret_cast<typename FuseSort<ITEMS>::storage_type*>(smem);
-  uint64_t* f = reinterpret_cast<uint64_t*>(smem);  // reused after the sort
-  __shared__ uint32_t dup[kCap / 32];                // 1 = not a distinct candidate
   __shared__ unsigned long long s_last[kSelB];
   __shared__ uint32_t hist[256];
   __shared__ uint32_t wsum[kSelWaves];
@@ -592,17 +603,6 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     mine += valid ? 1u : 0u;
     dmask |= (valid ? 0u : 1u) << j;
   }
-  __syncthreads();  // the sort storage becomes f[]
-#pragma unroll
-  for (uint32_t j = 0; j < ITEMS; ++j) f[tid * ITEMS + j] = fv[j];
-  if (tid < (int)(kCap / 32)) dup[tid] = 0;
-  __syncthreads();
-  // ITEMS flags per thread; a thread's run may straddle two 32-bit words
-  {
-    const uint32_t bit0 = tid * ITEMS, w0 = bit0 >> 5, sh = bit0 & 31;
-    atomicOr(&dup[w0], dmask << sh);
-    if (sh + ITEMS > 32) atomicOr(&dup[w0 + 1], dmask >> (32 - sh));
-  }
   uint32_t distinct;
   {
     uint32_t v = mine;
@@ -622,7 +622,6 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   const uint64_t lim = distinct < s_param ? distinct : s_param;
   if (tid == 0) res[g] = lim;
   uint64_t* dst = out + dst_off[g];
-  auto valid_at = [&](uint32_t i) { return i < n && !((dup[i >> 5] >> (i & 31)) & 1u); };
   const bool all = distinct <= lim;
   RadixSel sel{0, 0, 0, true};
   if (!all) {
@@ -630,7 +629,15 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j) mx = fv[j] > mx ? fv[j] : mx;  // 0 for non-distinct
     mx = block_max(mx, wsum64);
-    sel = radix_select(f, n, (uint32_t)lim, mx, valid_at, hist, s_sel);
+    // the distinct candidates' fmh are in registers (fv, 0 where dmask is set)
+    sel = radix_select_by(
+        [&](int shift, uint64_t prefix, uint64_t pmask) {
+#pragma unroll
+          for (uint32_t j = 0; j < ITEMS; ++j)
+            if (!((dmask >> j) & 1u) && (fv[j] & pmask) == prefix)
+              atomicAdd(&hist[(fv[j] >> shift) & 255u], 1u);
+        },
+        (uint32_t)lim, mx, hist, s_sel);
   }
   // keep (all distinct) or the selected ones, in k-mer order: the sorted keys,
   // their fmh and validity are in registers in blocked order (thread t holds
