@@ -3,5 +3,8 @@
 // sks_containment / sks_binomial_estimator (bit-identical doubles).
 #pragma once
 
+#include <cmath>        // ani_estimator.hpp:11
+#include "logging.hpp"  // ani_estimator.hpp:12
+
 double containment(int intersection, int set_size);
 double binomial_estimator(double containment, int kmer_num_ones);

@@ -5,8 +5,12 @@
 #pragma once
 
 #include <cstdint>
+#include <fstream>   // fasta_processing.hpp:14-15
+#include <iostream>
 #include <string>
 #include <vector>
+
+#include "logging.hpp"  // fasta_processing.hpp:16
 
 typedef std::vector<uint8_t> acgt_string;
 

@@ -6,6 +6,8 @@
 #include <utility>
 #include <vector>
 
+#include "stl_includes.hpp"  // generators.hpp:10
+
 template <typename T>
 std::pair<std::vector<T>, std::vector<T>> generate_pairwise_from_vector(const std::vector<T>& v) {
   std::vector<T> first, second;

@@ -23,6 +23,8 @@
 #include <string>
 #include <vector>
 
+#include "stl_includes.hpp"  // kmer.hpp:12 — the reference's transitive STL surface
+#include "logging.hpp"       // kmer.hpp:21
 #include "sks.h"
 
 // ---- constants (kmer.hpp:37-54) --------------------------------------------------------
