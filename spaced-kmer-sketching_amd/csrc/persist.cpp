@@ -2,7 +2,8 @@
 // reference re-parses and re-sketches every FASTA for each of its 62
 // configurations, kmer-sketching.cpp:168).
 //
-// File format "SKSKETCH" version 1, little-endian, 8-byte aligned sections:
+// File format "SKSKETCH", little-endian, 8-byte aligned sections.
+// Version 1 (one window / mask for the whole file; every C-ABI set):
 //   header (96 bytes)
 //     char     magic[8]   = "SKSKETCH"
 //     uint32   version    = 1
@@ -17,12 +18,19 @@
 //     uint64   n            sketches
 //     uint64   total        elements over all sketches
 //     uint64   names_bytes  0, or the size of the name table
-//     uint64   reserved     0
+//     uint64   groups       0 (version 1); the group count (version 2)
 //   uint32 sizes[n]           (zero-padded to a multiple of 8 bytes)
 //   uint64 windows[n]         k-mer windows hashed per genome
-//   uint64 data[total * elem_words]   each sketch sorted ascending, unique
+//   [version 2 only] group table, `groups` entries of 32 bytes:
+//     uint32 set, int32 window, uint64 mask_lo, uint64 mask_hi, uint64 size
+//   uint64 data[total * elem_words]   each sketch (v1) / group (v2) sorted ascending, unique
 //   char   names[names_bytes] n NUL-terminated strings (when names_bytes > 0)
 //   uint64 checksum           FNV-1a 64 of every byte before it
+// Version 2 is what the C++ facade writes for kmer_sets the reference allows but
+// version 1 cannot hold (kmer.hpp:170-178 accepts any mix of masks): a set is a
+// list of (window, mask) groups in set order, sizes[i] = the sum of set i's
+// group sizes, and the header's window / mask are the first group's.  The C ABI
+// reads version 1 only (an sks_sketch_set has one mask).
 // A reader rejects a wrong magic / version, inconsistent sizes, a truncated
 // or over-long file, a checksum mismatch and unsorted sketches (SKS_E_IO).
 #include <cerrno>
@@ -42,6 +50,7 @@ namespace {
 
 constexpr char kMagic[8] = {'S', 'K', 'S', 'K', 'E', 'T', 'C', 'H'};
 constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersionGroups = 2;
 
 struct Header {
   char magic[8];
@@ -57,9 +66,17 @@ struct Header {
   uint64_t n;
   uint64_t total;
   uint64_t names_bytes;
-  uint64_t reserved1;
+  uint64_t groups;
 };
 static_assert(sizeof(Header) == 96, "sketch file header layout");
+
+struct GroupRec {
+  uint32_t set;
+  int32_t window;
+  uint64_t mask_lo, mask_hi;
+  uint64_t size;
+};
+static_assert(sizeof(GroupRec) == 32, "sketch file group layout");
 
 struct Fnv {
   uint64_t h = 0xcbf29ce484222325ull;
@@ -90,15 +107,17 @@ bool less128(const uint64_t* a, const uint64_t* b, int ew) {
 
 }  // namespace
 
-int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::vector<uint32_t>& sizes,
-                      const std::vector<uint64_t>& windows, const uint64_t* data,
-                      const std::vector<std::string>& names) {
+namespace {
+
+int write_impl(const char* path, const SketchFileMeta& meta, const std::vector<uint32_t>& sizes,
+               const std::vector<uint64_t>& windows, const std::vector<SketchGroup>* groups,
+               const uint64_t* data, const std::vector<std::string>& names) {
   if (!path) return fail(SKS_E_ARG, "sketch file: null path");
   if (windows.size() != sizes.size() || (!names.empty() && names.size() != sizes.size()))
     return fail(SKS_E_ARG, "sketch file: names / windows must match the number of sketches");
   Header h{};
   std::memcpy(h.magic, kMagic, 8);
-  h.version = kVersion;
+  h.version = groups ? kVersionGroups : kVersion;
   h.elem_words = (uint32_t)meta.elem_words;
   h.window = meta.window;
   h.policy_kind = meta.policy.kind;
@@ -109,6 +128,17 @@ int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::v
   h.mask_hi = meta.mask[1];
   h.n = sizes.size();
   for (uint32_t v : sizes) h.total += v;
+  std::vector<GroupRec> recs;
+  if (groups) {
+    uint64_t gtotal = 0;
+    for (const SketchGroup& g : *groups) {
+      if (g.set >= sizes.size()) return fail(SKS_E_ARG, "sketch file: group names a missing set");
+      recs.push_back(GroupRec{g.set, g.window, g.mask[0], g.mask[1], g.size});
+      gtotal += g.size;
+    }
+    if (gtotal != h.total) return fail(SKS_E_ARG, "sketch file: group sizes do not add up");
+    h.groups = recs.size();
+  }
   std::string table;
   for (const std::string& s : names) {
     if (s.find('\0') != std::string::npos) return fail(SKS_E_ARG, "sketch file: name contains NUL");
@@ -124,6 +154,7 @@ int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::v
   const uint64_t zero = 0;
   w.put(&zero, pad8(sizes.size() * 4) - sizes.size() * 4);
   w.put(windows.data(), windows.size() * 8);
+  w.put(recs.data(), recs.size() * sizeof(GroupRec));
   w.put(data, h.total * h.elem_words * 8);
   w.put(table.data(), table.size());
   const uint64_t sum = w.fnv.h;
@@ -133,9 +164,10 @@ int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::v
   return SKS_OK;
 }
 
-int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
-                     std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
-                     std::vector<std::string>& names) {
+int read_impl(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
+              std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
+              std::vector<std::string>& names, std::vector<SketchGroup>* groups,
+              bool* grouped_out = nullptr) {
   if (!path) return fail(SKS_E_ARG, "sketch file: null path");
   FILE* f = fopen(path, "rb");
   if (!f) return fail(SKS_E_IO, std::string("sketch file: cannot open ") + path);
@@ -151,16 +183,23 @@ int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_
   Header h;
   std::memcpy(&h, buf.data(), sizeof h);
   if (std::memcmp(h.magic, kMagic, 8) != 0) return fail(SKS_E_IO, where + "not a sketch file");
-  if (h.version != kVersion) return fail(SKS_E_IO, where + "unsupported version " + std::to_string(h.version));
-  if (h.window < 1 || h.window > 64 || h.elem_words != (h.window > 32 ? 2u : 1u))
+  if (h.version == kVersionGroups && !groups)
+    return fail(SKS_E_IO, where + "version 2 (kmer_sets with several masks): load it with sks::load_kmer_sets");
+  if (h.version != kVersion && h.version != kVersionGroups)
+    return fail(SKS_E_IO, where + "unsupported version " + std::to_string(h.version));
+  const bool grouped = h.version == kVersionGroups;
+  if (h.window < 1 || h.window > 64 || h.elem_words < 1 || h.elem_words > 2 ||
+      (!grouped && h.elem_words != (h.window > 32 ? 2u : 1u)))
     return fail(SKS_E_IO, where + "bad window / element width");
-  if (h.n > (1ull << 32) || h.total > (1ull << 40)) return fail(SKS_E_IO, where + "bad counts");
+  if (h.n > (1ull << 32) || h.total > (1ull << 40) || (!grouped && h.groups) || h.groups > (1ull << 32))
+    return fail(SKS_E_IO, where + "bad counts");
   // every region must fit in the file before any offset past it is formed: the
   // counts are bounded above, so o_names cannot wrap; names_bytes is checked
   // against the bytes left rather than added first
   const size_t o_sizes = sizeof(Header);
   const size_t o_win = o_sizes + pad8(h.n * 4);
-  const size_t o_data = o_win + h.n * 8;
+  const size_t o_groups = o_win + h.n * 8;
+  const size_t o_data = o_groups + h.groups * sizeof(GroupRec);
   const size_t o_names = o_data + h.total * h.elem_words * 8;
   const size_t body = buf.size() - 8;  // bytes before the checksum
   if (o_names > body || h.names_bytes > body - o_names)
@@ -182,9 +221,31 @@ int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_
   for (uint32_t v : sizes) total += v;
   if (total != h.total) return fail(SKS_E_IO, where + "sizes do not add up");
   const int ew = (int)h.elem_words;
+  // runs that must each be sorted and unique: the sketches (v1) or the groups (v2)
+  std::vector<uint64_t> runs;
+  if (grouped) {
+    std::vector<GroupRec> recs(h.groups);
+    if (!recs.empty()) std::memcpy(recs.data(), buf.data() + o_groups, recs.size() * sizeof(GroupRec));
+    std::vector<uint64_t> per_set(h.n, 0);
+    groups->clear();
+    uint32_t prev_set = 0;
+    for (const GroupRec& r : recs) {
+      if (r.set >= h.n || r.set < prev_set || r.window < 1 || r.window > 64 ||
+          (r.window > 32 && ew != 2) || r.size > h.total)
+        return fail(SKS_E_IO, where + "bad group table");
+      prev_set = r.set;
+      per_set[r.set] += r.size;
+      runs.push_back(r.size);
+      groups->push_back(SketchGroup{r.set, r.window, {r.mask_lo, r.mask_hi}, r.size});
+    }
+    for (uint64_t i = 0; i < h.n; ++i)
+      if (per_set[i] != sizes[i]) return fail(SKS_E_IO, where + "group sizes do not add up");
+  } else {
+    runs.assign(sizes.begin(), sizes.end());
+  }
   uint64_t e = 0;
-  for (uint32_t v : sizes) {
-    for (uint32_t i = 1; i < v; ++i)
+  for (uint64_t v : runs) {
+    for (uint64_t i = 1; i < v; ++i)
       if (!less128(&data[(e + i - 1) * ew], &data[(e + i) * ew], ew))
         return fail(SKS_E_IO, where + "a sketch is not sorted and unique");
     e += v;
@@ -205,7 +266,37 @@ int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_
   meta.mask[0] = h.mask_lo;
   meta.mask[1] = h.mask_hi;
   meta.policy = sks_policy{h.policy_kind, h.flavour, h.param, h.nonce};
+  if (grouped_out) *grouped_out = grouped;
   return SKS_OK;
+}
+
+}  // namespace
+
+int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::vector<uint32_t>& sizes,
+                      const std::vector<uint64_t>& windows, const uint64_t* data,
+                      const std::vector<std::string>& names) {
+  return write_impl(path, meta, sizes, windows, nullptr, data, names);
+}
+
+int write_sketch_file_groups(const char* path, const SketchFileMeta& meta,
+                             const std::vector<uint32_t>& sizes, const std::vector<uint64_t>& windows,
+                             const std::vector<SketchGroup>& groups, const uint64_t* data,
+                             const std::vector<std::string>& names) {
+  return write_impl(path, meta, sizes, windows, &groups, data, names);
+}
+
+int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
+                     std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
+                     std::vector<std::string>& names) {
+  return read_impl(path, meta, sizes, windows, data, names, nullptr);
+}
+
+int read_sketch_file_any(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
+                         std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
+                         std::vector<std::string>& names, std::vector<SketchGroup>& groups,
+                         bool& grouped) {
+  grouped = false;
+  return read_impl(path, meta, sizes, windows, data, names, &groups, &grouped);
 }
 
 }  // namespace sks

@@ -55,6 +55,23 @@ int write_sketch_file(const char* path, const SketchFileMeta& meta, const std::v
 int read_sketch_file(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
                      std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
                      std::vector<std::string>& names);
+// Version 2: sets made of (window, mask) groups (the facade's mixed-mask
+// kmer_sets).  `data` holds the groups back to back, in set order.
+struct SketchGroup {
+  uint32_t set;
+  int32_t window;
+  uint64_t mask[2];
+  uint64_t size;
+};
+int write_sketch_file_groups(const char* path, const SketchFileMeta& meta,
+                             const std::vector<uint32_t>& sizes, const std::vector<uint64_t>& windows,
+                             const std::vector<SketchGroup>& groups, const uint64_t* data,
+                             const std::vector<std::string>& names);
+// Reads version 1 or 2; `grouped` tells which (groups is empty for version 1).
+int read_sketch_file_any(const char* path, SketchFileMeta& meta, std::vector<uint32_t>& sizes,
+                         std::vector<uint64_t>& windows, std::vector<uint64_t>& data,
+                         std::vector<std::string>& names, std::vector<SketchGroup>& groups,
+                         bool& grouped);
 
 void parse_fasta_bytes(const uint8_t* data, uint64_t n, sks_fasta* out);
 

@@ -197,6 +197,76 @@ static int store(char** argv) {
   return same ? 0 : 2;
 }
 
+// test_facade store_mixed <path> <case>: sets the reference's kmer_set can hold
+// but one (window, mask) per file cannot — case 0: a set with k-mers under two
+// masks (kmer.hpp:170-178), an empty set, a 40-wide set; case 1: one mask and
+// an empty set among full ones (written as version 1).  Saves, loads, compares
+// every field; prints "sets <n> sizes <size/other masks>..." (exit 2 on a
+// mismatch).  A 5th argument "gpu" also compares all pair intersections.
+static bool same_set(const kmer_set& a, const kmer_set& b) {
+  if (a.has_mask != b.has_mask || a.elements != b.elements || a.kmer_set_size() != b.kmer_set_size())
+    return false;
+  if (a.has_mask && (a.mask != b.mask || a.window_length != b.window_length)) return false;
+  if (a.other_masks.size() != b.other_masks.size()) return false;
+  for (size_t g = 0; g < a.other_masks.size(); ++g)
+    if (a.other_masks[g].mask != b.other_masks[g].mask ||
+        a.other_masks[g].window_length != b.other_masks[g].window_length ||
+        a.other_masks[g].elements != b.other_masks[g].elements)
+      return false;
+  return true;
+}
+
+static int store_mixed(char** argv) {
+  const int which = std::atoi(argv[3]);
+  const kmer_bitset m1 = generate_random_spaced_seed_mask(31, 21, 0);
+  const kmer_bitset m2 = generate_random_spaced_seed_mask(31, 21, 5);
+  const kmer_bitset m3 = generate_random_spaced_seed_mask(40, 30, 1);
+  uint64_t x = 0x9e3779b97f4a7c15ull;
+  auto kmers = [&](const kmer_bitset& m, int w, int n) {
+    std::vector<kmer> v;
+    for (int j = 0; j < n; ++j) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      kmer_bitset bits(x, x * 31);
+      v.push_back(kmer{w, bits, m, bits & m});
+    }
+    return v;
+  };
+  std::vector<kmer_set> sets(3);
+  if (which == 0) {
+    std::vector<kmer> a = kmers(m1, 31, 40), b = kmers(m2, 31, 25);
+    a.insert(a.end(), b.begin(), b.end());
+    a.push_back(a[3]);  // a duplicate collapses
+    sets[0].insert_kmers(a);
+    sets[2].insert_kmers(kmers(m3, 40, 30));
+  } else {
+    sets[0].insert_kmers(kmers(m1, 31, 40));
+    sets[2].insert_kmers(kmers(m1, 31, 7));
+  }
+  sks::save_kmer_sets(argv[2], sets, sketch_policy::bottom(100, 1), {"mixed", "empty", "wide"});
+  std::vector<std::string> names;
+  sketch_policy pol;
+  auto back = sks::load_kmer_sets(argv[2], &names, &pol);
+  bool same = back.size() == sets.size() && pol.param == 100 && pol.kind == SKS_BOTTOM_S &&
+              names == std::vector<std::string>{"mixed", "empty", "wide"};
+  for (size_t i = 0; same && i < sets.size(); ++i) {
+    if (which == 1 && sets[i].kmer_set_size() == 0) {
+      // version 1 gives an empty set the file's mask; it stays empty
+      same = back[i].kmer_set_size() == 0 && back[i].other_masks.empty();
+      continue;
+    }
+    same = same_set(back[i], sets[i]);
+  }
+  // the loaded sets intersect like the originals (on the GPU: only with "gpu")
+  const bool gpu = argv[4] && std::string(argv[4]) == "gpu";
+  for (size_t i = 0; gpu && same && i < sets.size(); ++i)
+    for (size_t j = 0; same && j < sets.size(); ++j)
+      same = kmer_set_intersection(back[i], back[j]) == kmer_set_intersection(sets[i], sets[j]);
+  std::printf("sets %zu sizes", back.size());
+  for (const kmer_set& s : back) std::printf(" %d/%zu", s.kmer_set_size(), s.other_masks.size());
+  std::printf("\n");
+  return same ? 0 : 2;
+}
+
 static int load(char** argv) {
   try {
     std::vector<std::string> names;
@@ -217,6 +287,7 @@ int main(int argc, char** argv) {
   if (mode == "list" && argc == 7) return list(argv);
   if (mode == "store" && argc == 4) return store(argv);
   if (mode == "load" && argc == 3) return load(argv);
+  if (mode == "store_mixed" && (argc == 4 || argc == 5)) return store_mixed(argv);
   if (mode == "missing" && argc == 3) {
     char* f[1] = {argv[2]};
     kmer_bitset mask = generate_random_spaced_seed_mask(21, 21, 0);

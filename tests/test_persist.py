@@ -191,3 +191,52 @@ def test_device_save_load_concat(gpu, tmp_path, w, k, kind, param):
     import sksffi
     with pytest.raises(sksffi.SksError):
         ctx.concat([a, other])
+
+
+def _store_mixed(facade_bin, path, case, gpu=False):
+    args = [facade_bin, "store_mixed", str(path), str(case)] + (["gpu"] if gpu else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    return r.stdout
+
+
+def test_host_store_mixed_masks_and_empty_sets(facade_bin, tmp_path):
+    """kmer_sets with k-mers under several masks (kmer.hpp:170-178) and empty
+    sets survive save_kmer_sets / load_kmer_sets (format version 2 when one
+    (window, mask) per file cannot hold them, version 1 otherwise)."""
+    p = tmp_path / "mixed.sks"
+    out = _store_mixed(facade_bin, p, 0)
+    assert out.split() == ["sets", "3", "sizes", "65/1", "0/0", "30/0"]
+    data = p.read_bytes()
+    assert data[:8] == b"SKSKETCH" and struct.unpack_from("<I", data, 8)[0] == 2
+    n, total, _nb, groups = struct.unpack_from("<QQQQ", data, 64)
+    assert (n, total, groups) == (3, 95, 3)
+    assert struct.unpack_from("<I", data, 12)[0] == 2  # a 40-wide group: two words per element
+    # the group table: (set, window, mask) in set order
+    o = 96 + ((3 * 4 + 7) & ~7) + 8 * 3
+    recs = [struct.unpack_from("<IiQQQ", data, o + 32 * i) for i in range(3)]
+    assert [(r[0], r[1], r[4]) for r in recs] == [(0, 31, 40), (0, 31, 25), (2, 40, 30)]
+    assert recs[0][2] | recs[0][3] << 64 == O.mask(31, 21, 0)
+    assert recs[1][2] | recs[1][3] << 64 == O.mask(31, 21, 5)
+    assert recs[2][2] | recs[2][3] << 64 == O.mask(40, 30, 1)
+    # one mask plus an empty set: still version 1, readable by the independent parser
+    p1 = tmp_path / "one.sks"
+    out = _store_mixed(facade_bin, p1, 1)
+    assert out.split() == ["sets", "3", "sizes", "40/0", "0/0", "7/0"]
+    f = parse_sksketch(p1.read_bytes())
+    assert f["sizes"] == [40, 0, 7] and f["mask"] == O.mask(31, 21, 0)
+    # the facade's plain loader reads both versions
+    r = subprocess.run([facade_bin, "load", str(p)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+
+
+@pytest.mark.gpu
+def test_store_mixed_masks_intersections(facade_bin, gpu, tmp_path):
+    """Loaded mixed-mask sets intersect like the originals (per shared mask);
+    the C ABI, whose device sets hold one mask, refuses a version-2 file by name."""
+    import sksffi
+    p = tmp_path / "mixed.sks"
+    _store_mixed(facade_bin, p, 0, gpu=True)
+    _torch, ctx = gpu
+    with pytest.raises(sksffi.SksError, match="version 2"):
+        ctx.load_sketches(p)
