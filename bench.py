@@ -84,6 +84,13 @@ def collective():
     return dist.is_available() and dist.is_initialized()
 
 
+def backend_label():
+    """What the collectives run on, from the process group itself."""
+    import torch.distributed as dist
+    b = dist.get_backend()
+    return {"nccl": "RCCL over xGMI", "gloo": "gloo, via host memory"}.get(b, b)
+
+
 def barrier(world):
     if collective():
         import torch.distributed as dist
@@ -680,8 +687,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
                    "pair_sharding": "block-aligned genomes per rank; upper-triangle 64x64 "
                                     "join tiles split over ranks",
                    "collective": ("all_gather_into_tensor join layouts + all_reduce counts "
-                                  + ("(RCCL)" if dev == "cuda" else "(gloo, via host)")
-                                  if collective() else "none")},
+                                  f"({backend_label()})" if collective() else "none")},
         "cpu_baseline": cpu,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
         "ms_end_to_end": (t_sketch + t_pairs) * 1e3,
@@ -773,8 +779,8 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
                    "seeds": C5_SEEDS, "s": C4_S, "w": W, "k": K,
                    "sharding": "seeds over ranks", "consensus": "mean ANI over seeds",
                    "seeds_in_flight": max(1, lanes_n),
-                   "collective": ("all_reduce of ANI sums (RCCL)" if collective() and dev == "cuda"
-                                  else ("all_reduce (gloo)" if collective() else "none"))},
+                   "collective": (f"all_reduce of ANI sums ({backend_label()})"
+                                  if collective() else "none")},
     }
 
 
@@ -790,6 +796,23 @@ def latest_traffic_json():
         if m:
             found.append((int(m.group(1)), f))
     return max(found)[1] if found else ""
+
+
+def traffic_for_current_scan(path):
+    """(bytes per launch, source file, note): the PMC traffic of a profile only
+    while it was measured on the scan kernel's current sources; else None with
+    the reason."""
+    import srchash
+    if not path or not os.path.exists(path):
+        return None, None, "no profiles/rNN/traffic.json"
+    src = os.path.relpath(path, ROOT)
+    with open(path) as f:
+        t = json.load(f)
+    want, got = srchash.scan_hash(), t.get("scan_source_hash")
+    if got != want:
+        return None, src, (f"stale: measured on scan sources {got}, these are {want} "
+                           "(re-run tools/profile_round.sh)")
+    return t.get("scan_hbm_bytes_per_launch"), src, f"PMC on scan sources {want}"
 
 
 def main():
@@ -865,11 +888,7 @@ def main():
     scan_avg_ms = float(np.mean(scan_ms))
     alg_bytes = n_bytes + 8 * float(np.mean(survivors))
     achieved = alg_bytes / (scan_avg_ms * 1e-3) / 1e9
-    traffic = traffic_src = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        with open(args.traffic_json) as f:
-            traffic = json.load(f).get("scan_hbm_bytes_per_launch")
-        traffic_src = os.path.relpath(args.traffic_json, ROOT)
+    traffic, traffic_src, traffic_note = traffic_for_current_scan(args.traffic_json)
 
     c2 = None
     if not args.no_c2:
@@ -917,7 +936,7 @@ def main():
                          "kernel": "scan_kernel<frac, boost-mix, pre-filter>", "kernel_ms": scan_avg_ms,
                          "kernel_ms_median": float(np.median(scan_ms)),
                          "algorithmic_bytes_per_launch": alg_bytes,
-                         "traffic_source": traffic_src,
+                         "traffic_source": traffic_src, "traffic_note": traffic_note,
                          "timing": "hipEvents around each scan launch of the serial pass "
                                    "(the --steps builds after --warmup)"},
             "cpu_baseline": cpu,

@@ -32,39 +32,12 @@ struct PinnedStage {
   void* p = nullptr;
   size_t bytes = 0;
 };
-// never freed: a thread_local destructor could run after the HIP runtime has
-// been torn down at process exit
-thread_local PinnedStage t_stage;
 
-hipError_t stage_reserve(size_t bytes) {
-  if (bytes <= t_stage.bytes) return hipSuccess;
-  if (t_stage.p) (void)hipHostFree(t_stage.p);
-  t_stage.p = nullptr;
-  t_stage.bytes = 0;
-  size_t nb = std::max<size_t>(bytes, size_t(1) << 16);
-  nb = (nb + 4095) & ~size_t(4095);
-  hipError_t e = hipHostMalloc(&t_stage.p, nb, hipHostMallocDefault);
-  if (e == hipSuccess) t_stage.bytes = nb;
-  return e;
-}
-}  // namespace
-
-hipError_t pinned_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (!bytes) return hipSuccess;
-  hipError_t e;
-  if ((e = stage_reserve(bytes)) != hipSuccess) return e;
-  if ((e = hipMemcpyAsync(t_stage.p, src, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-  std::memcpy(dst, t_stage.p, bytes);
-  return hipSuccess;
-}
-
-// Host -> device copies of small metadata go through a per-thread pinned ring
-// and do not wait: the bytes are copied into the ring at once (the caller's
-// buffer may go away), the DMA is queued on `s`, and an event marks when that
-// part of the ring may be rewritten.  A build used to synchronise its stream
-// after every metadata upload (a dozen round trips for one 5 Mb genome).
-namespace {
+// Host -> device copies of small metadata go through a pinned ring and do not
+// wait: the bytes are copied into the ring at once (the caller's buffer may go
+// away), the DMA is queued on `s`, and an event marks when that part of the
+// ring may be rewritten.  A build used to synchronise its stream after every
+// metadata upload (a dozen round trips for one 5 Mb genome).
 struct RingUse {
   size_t off, len;
   int device;
@@ -76,7 +49,55 @@ struct PinnedRing {
   std::vector<RingUse> pending;
   std::vector<std::pair<int, hipEvent_t>> spare;  // (device, event) ready for reuse
 };
-thread_local PinnedRing t_ring;  // never freed (see t_stage)
+
+// A thread's pinned staging (the d2h stage and the h2d ring).  Threads borrow
+// one from a process-wide pool on first use and give it back when they exit,
+// so the pinned memory is bounded by the largest number of threads staging at
+// once, not by how many threads a long-running caller has started (the
+// facade's parallel_* entry points start fresh threads on every call).  Pool
+// entries are never freed: nothing touches HIP at thread or process exit
+// (thread_local destructors of the main thread run before static ones, and
+// could otherwise run after the HIP runtime is gone).
+struct PinnedSlots {
+  PinnedStage stage;
+  PinnedRing ring;
+};
+std::mutex g_slots_mu;
+std::vector<PinnedSlots*>* g_slots_pool = new std::vector<PinnedSlots*>();  // never freed
+
+struct SlotsHandle {
+  PinnedSlots* s = nullptr;
+  PinnedSlots& get() {
+    if (!s) {
+      std::lock_guard<std::mutex> lk(g_slots_mu);
+      if (!g_slots_pool->empty()) {
+        s = g_slots_pool->back();
+        g_slots_pool->pop_back();
+      } else {
+        s = new PinnedSlots();
+      }
+    }
+    return *s;
+  }
+  ~SlotsHandle() {
+    if (!s) return;
+    std::lock_guard<std::mutex> lk(g_slots_mu);
+    g_slots_pool->push_back(s);  // pending ring copies stay tracked by their events
+  }
+};
+thread_local SlotsHandle t_slots;
+
+hipError_t stage_reserve(PinnedStage& st, size_t bytes) {
+  if (bytes <= st.bytes) return hipSuccess;
+  if (st.p) (void)hipHostFree(st.p);
+  st.p = nullptr;
+  st.bytes = 0;
+  size_t nb = std::max<size_t>(bytes, size_t(1) << 16);
+  nb = (nb + 4095) & ~size_t(4095);
+  hipError_t e = hipHostMalloc(&st.p, nb, hipHostMallocDefault);
+  if (e == hipSuccess) st.bytes = nb;
+  return e;
+}
 
 void ring_retire(PinnedRing& R, size_t i) {
   R.spare.emplace_back(R.pending[i].device, R.pending[i].ev);
@@ -84,9 +105,25 @@ void ring_retire(PinnedRing& R, size_t i) {
 }
 }  // namespace
 
+size_t pinned_pool_size() {
+  std::lock_guard<std::mutex> lk(g_slots_mu);
+  return g_slots_pool->size();
+}
+
+hipError_t pinned_d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  PinnedStage& st = t_slots.get().stage;
+  hipError_t e;
+  if ((e = stage_reserve(st, bytes)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(st.p, src, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  std::memcpy(dst, st.p, bytes);
+  return hipSuccess;
+}
+
 hipError_t pinned_h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return hipSuccess;
-  PinnedRing& R = t_ring;
+  PinnedRing& R = t_slots.get().ring;
   hipError_t e;
   int dev = 0;
   if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
@@ -393,6 +430,27 @@ void free_passes(std::vector<PassOut>& passes) {
   passes.clear();
 }
 
+}  // namespace
+
+namespace sks {
+hipError_t cache_alloc(void** p, size_t bytes) { return dev_alloc(p, bytes); }
+
+void cache_release_after(void* p, size_t bytes, hipStream_t s) {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(ev, s) != hipSuccess) {
+    // no event: wait for the stream, then park the block as idle
+    if (ev) (void)hipEventDestroy(ev);
+    ev = nullptr;
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(s);
+  }
+  dev_release(p, bytes, ev);
+}
+}  // namespace sks
+
+namespace {
+
 int alloc_u64(uint64_t** p, uint64_t words, size_t* bytes_out = nullptr) {
   const size_t bytes = std::max<uint64_t>(words, 1) * sizeof(uint64_t);
   SKS_HIP(dev_alloc(reinterpret_cast<void**>(p), bytes));
@@ -498,6 +556,11 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
   if (!c) return sks::fail(SKS_E_NOMEM, "sks_ctx_create: out of memory");
   c->device = device;
   c->stream = reinterpret_cast<hipStream_t>(stream);
+  // every scratch buffer is used on the context's stream only
+  for (sks::Scratch* sc : {&c->ingress, &c->tmp, &c->rec[0], &c->rec[1], &c->rec[2], &c->flag,
+                           &c->pos, &c->meta, &c->iwork})
+    sc->owner = &c->stream;
+  for (auto& b : c->buf) b.owner = &c->stream;
   if (hipEventCreate(&c->ev_begin) != hipSuccess || hipEventCreate(&c->ev_end) != hipSuccess ||
       hipEventCreate(&c->ev_s0) != hipSuccess || hipEventCreate(&c->ev_s1) != hipSuccess ||
       hipEventCreate(&c->ev_i0) != hipSuccess || hipEventCreate(&c->ev_i1) != hipSuccess) {
@@ -535,6 +598,12 @@ int sks_ctx_device(const sks_ctx* c) { return c ? c->device : -1; }
 
 int sks_ctx_set_stream(sks_ctx* c, void* stream) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_set_stream: null ctx");
+  // scratch blocks are released in the order of the context's stream: let the
+  // old stream's work finish before the order changes
+  if (c->stream != reinterpret_cast<hipStream_t>(stream)) {
+    DeviceGuard g(c->device);
+    SKS_HIP(hipStreamSynchronize(c->stream));
+  }
   c->stream = reinterpret_cast<hipStream_t>(stream);
   return SKS_OK;
 }

@@ -405,6 +405,7 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
   if (o > work.bytes) {
     // keep the span offsets across the reallocation
     Scratch grown;
+    grown.owner = work.owner;
     SKS_CK(grown.reserve(o));
     SKS_CK(hipMemcpyAsync(grown.ptr, work.ptr, o_lines, hipMemcpyDeviceToDevice, s));
     SKS_CK(hipStreamSynchronize(s));

@@ -21,15 +21,20 @@ namespace sks {
 hipError_t Scratch::reserve(size_t n) {
   if (n <= bytes) return hipSuccess;
   // queued work may still read the old buffer (metadata uploads do not wait
-  // for their stream): let it finish before the buffer goes (growth is rare)
+  // for their stream): it is reused only after the owner stream's queued work;
+  // an ownerless buffer waits for the device (growth is rare)
   if (ptr) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(ptr);
+    if (owner) {
+      cache_release_after(ptr, bytes, *owner);
+    } else {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(ptr);
+    }
   }
   ptr = nullptr;
   bytes = 0;
   size_t want = std::max<size_t>(n, 1 << 20);
-  hipError_t e = hipMalloc(&ptr, want);
+  hipError_t e = owner ? cache_alloc(&ptr, want) : hipMalloc(&ptr, want);
   if (e == hipSuccess) bytes = want;
   return e;
 }

@@ -15,6 +15,15 @@ namespace sks {
 // (--hip-trace), serialising the concurrent builds.
 hipError_t pinned_d2h(void* dst, const void* src, size_t bytes, hipStream_t s);
 hipError_t pinned_h2d(void* dst, const void* src, size_t bytes, hipStream_t s);
+// Staging buffers parked by exited threads, ready for reuse (diagnostics).
+size_t pinned_pool_size();
+
+// The process's device block cache (api.cpp): a parked block of at least
+// `bytes` on the current device, or a fresh hipMalloc; and a stream-ordered
+// release (the block is handed out again only once `s` has passed the point of
+// the call).  Neither waits for the device.
+hipError_t cache_alloc(void** p, size_t bytes);
+void cache_release_after(void* p, size_t bytes, hipStream_t s);
 
 constexpr int kModeFrac = 0;
 constexpr int kModeBottom = 1;
@@ -54,10 +63,14 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
                        hipStream_t stream, int grid_override);
 
 // ---- post-processing (post.hip) -------------------------------------------------
-// Grow-only device scratch owned by a context.
+// Grow-only device scratch owned by a context.  With `owner` set (the
+// context's stream; every use of the buffer is ordered on it) a grown buffer's
+// old block goes back to the block cache after the stream's queued work, with
+// no device-wide wait; without it, growth waits for the whole device.
 struct Scratch {
   void* ptr = nullptr;
   size_t bytes = 0;
+  const hipStream_t* owner = nullptr;
   hipError_t reserve(size_t n);
   void release();
 };

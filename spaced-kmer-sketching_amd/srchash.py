@@ -20,14 +20,23 @@ def files():
     return sorted(out)
 
 
-def source_hash():
+# the sources the fused scan kernel is compiled from (profiles/rNN/traffic.json
+# records this hash; bench.py uses a traffic figure only when it still matches)
+SCAN_FILES = ["csrc/scan.hip", "csrc/sks_hash.hpp", "csrc/sks_internal.hpp"]
+
+
+def source_hash(rels=None):
     h = hashlib.sha256()
-    for rel in files():
+    for rel in (files() if rels is None else sorted(rels)):
         h.update(rel.encode() + b"\0")
         with open(os.path.join(PKG, rel), "rb") as f:
             h.update(f.read())
         h.update(b"\0")
     return h.hexdigest()[:16]
+
+
+def scan_hash():
+    return source_hash(SCAN_FILES)
 
 
 if __name__ == "__main__":

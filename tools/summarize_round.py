@@ -6,7 +6,8 @@
                             bench line's own hipEvent kernel time of the same run
   traffic.json              HBM bytes per timed launch from PMC: FETCH_SIZE x 2 (the
                             gfx950 correction, MI355X_MICROARCH.md HBM) + WRITE_SIZE,
-                            KiB units, median over the same dispatch indices
+                            KiB units, median over the same dispatch indices, and the
+                            scan kernel's source hash (srchash.scan_hash) it was measured on
   scan_counters.txt / pair_counters.txt   SQ counter averages per kernel
     python tools/summarize_round.py <round_dir> <dst> <warmup> <steps>"""
 import csv
@@ -20,6 +21,10 @@ from contextlib import redirect_stdout
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import pmc_by_kernel  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "spaced-kmer-sketching_amd"))
+import srchash  # noqa: E402
 
 SCAN = "scan_kernel<0, 0, 1>"  # FracMinHash, flavour B, low-bits pre-filter (config 3)
 
@@ -78,7 +83,9 @@ def main(src, dst, warmup, steps):
                "fetch_size_kib_median": fk, "write_size_kib_median": wk,
                "scan_hbm_bytes_per_launch": (2 * fk + wk) * 1024,
                "correction": "FETCH_SIZE x 2 (gfx950 counts 128-B requests at 64 B, MI355X_MICROARCH.md HBM)",
-               "dispatches_seen": [len(fetch), len(write)]}
+               "dispatches_seen": [len(fetch), len(write)],
+               # bench.py reports this traffic only while the scan's sources hash the same
+               "scan_source_hash": srchash.scan_hash()}
     with open(os.path.join(dst, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     for sub, name, kernels in (("sq", "scan_counters.txt", ["scan_kernel"]),
