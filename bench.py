@@ -351,7 +351,8 @@ def cpu_baseline_c3(mask, budget_bases):
     return {"value": windows / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
             "sample": f"first {budget_bases / 1e6:.0f} Mb of config-3 contig 0 "
                       f"({windows} windows, FracMinHash 1/{C3_FRAC}, set size {size}), "
-                      f"oracle/ref_port.cpp, {dt:.1f} s"}
+                      f"oracle/ref_port.cpp, {dt:.1f} s",
+            "host": host_info(1)}
 
 
 def run_c3_sharded(ctx, world, rank, mask, buf, steps, warmup):
@@ -407,12 +408,81 @@ def run_c3_sharded(ctx, world, rank, mask, buf, steps, warmup):
 
 def cpu_threads():
     """Host cores this process may use (the GPU box gives a share of a larger
-    machine: os.cpu_count() shows all of it), capped at 16."""
+    machine: os.cpu_count() shows all of it), capped at 16 — the share a
+    one-GPU box grants (MAX_JOBS / OMP_NUM_THREADS are 16 there)."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
     return max(1, min(16, n))
+
+
+def host_info(threads):
+    """What a CPU baseline ran on (cores and CPU model with every result)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    return {"threads_used": threads, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "cpu_model": model, "thread_cap": "min(16, affinity): the box's CPU share"}
+
+
+def _codes_lens(seq_bytes):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    runs = pyoracle.cut_runs(seq_bytes)
+    codes = np.frombuffer(b"".join(runs), dtype=np.uint8)
+    lens = np.array([len(r) for r in runs], dtype=np.uint64)
+    windows = int(sum(max(0, int(L) - W + 1) for L in lens))
+    return codes, lens, windows
+
+
+def cpu_baseline_c2(host_genome, mask, gpu_sketch):
+    """Config 2 on the host: the reference-style port (oracle/ref_port.cpp:
+    heap bitsets, per-window kmer, std::function predicate, with the bottom-s
+    kept in std::set / unordered_map — the reference has no bottom-s) over the
+    whole 5 Mb genome on one core (one genome = one cilk worker,
+    kmer_set.cpp:124).  The set is checked equal to the GPU's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    codes, lens, windows = _codes_lens(host_genome)
+    t0 = time.perf_counter()
+    s = pyoracle.refport_bottom_codes(codes, lens, W, mask, C2_S)
+    dt = time.perf_counter() - t0
+    assert np.array_equal(s.elems(), gpu_sketch), "config-2 CPU set differs from the GPU's"
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": f"the whole config-2 genome ({windows} windows, bottom-s {C2_S}), "
+                      f"oracle/ref_port.cpp bottom_runs, {dt:.2f} s; set equal to the GPU's",
+            "host": host_info(1)}
+
+
+def cpu_sketch_many(host_genomes, mask, kind, param, threads):
+    """Reference-style port over genomes, `threads` workers over genomes (the
+    reference's cilk_for over files, kmer_set.cpp:112-133). Returns (sets, windows, s)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from concurrent.futures import ThreadPoolExecutor
+    prepared = [_codes_lens(g) for g in host_genomes]
+
+    def one(i):
+        codes, lens, _ = prepared[i]
+        if kind == "bottom":
+            return pyoracle.refport_bottom_codes(codes, lens, W, mask, param)
+        return pyoracle.refport_sketch_codes(codes, lens, W, mask, param)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        sets = list(ex.map(one, range(len(prepared))))
+    dt = time.perf_counter() - t0
+    return sets, sum(p[2] for p in prepared), dt
 
 
 def cpu_crosscheck_c3(ctx, buf, mask, sample_bytes):
@@ -447,14 +517,15 @@ def cpu_crosscheck_c3(ctx, buf, mask, sample_bytes):
     return {"value": windows / dt, "unit": "k-mers/s", "cores": T, "kind": "port (optimised)",
             "sample": f"first {sample_bytes / 1e6:.0f} MB of the config-3 genome, {T} chunks with "
                       f"(w-1) halos, oracle/sks_oracle.cpp u128 rolling window, "
-                      f"{dt:.1f} s; set equal to the GPU's"}
+                      f"{dt:.1f} s; set equal to the GPU's",
+            "host": host_info(T)}
 
 
 # ---- config 2 ------------------------------------------------------------------------
 C2_LEN, C2_SEED, C2_S, C2_BATCH = 5_000_000, 2, 10000, 64
 
 
-def run_c2(ctx, mask, steps, warmup, inflight=2):
+def run_c2(ctx, mask, steps, warmup, inflight=2, cpu=False):
     """Config 2 of BASELINE.json: one 5 Mb bacterial-scale genome (synthetic,
     seed 2), w=31/k=21 spaced seed, bottom-s s=10000.  One such build is
     launch/latency-bound (a few hundred microseconds of GPU work spread over a
@@ -546,6 +617,9 @@ def run_c2(ctx, mask, steps, warmup, inflight=2):
     t_batch = (time.perf_counter() - t0) / reps
     bscan = bt["scan_ms"]
     balg = seg[-1] + 16 * bt["survivors"]
+    cpu_b = None
+    if cpu:
+        cpu_b = cpu_baseline_c2(buf[:C2_LEN].cpu().numpy().tobytes(), mask, ref)
     del buf
     return {
         "metric": "k-mers hashed/s, config 2", "unit": "k-mers/s", "steps": steps,
@@ -561,6 +635,7 @@ def run_c2(ctx, mask, steps, warmup, inflight=2):
                            "scan kernel alone by hipEvents"},
         "inflight": {"builds_in_flight": len(ctxs), "kmers_per_s": windows / t_inflight,
                      "ms_per_build": t_inflight * 1e3},
+        "cpu_baseline": cpu_b,
         "batched": {"genomes_per_build": C2_BATCH, "kmers_per_s": C2_BATCH * windows / t_batch,
                     "ms_per_build": t_batch * 1e3, "scan_kernel_ms": bscan,
                     "scan_roofline_frac": balg / (bscan * 1e-3) / 1e9 / HBM_PEAK_GBS},
@@ -593,7 +668,27 @@ def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100):
     return {"value": n_sets * n_sets / dt, "unit": "ordered pairs/s", "cores": T, "kind": "port",
             "sample": f"all {n_sets}x{n_sets} ordered pairs of the first {n_sets} genomes "
                       f"(s={C4_S}), oracle/ref_port.cpp, {T} threads over pairs, {dt:.2f} s; "
-                      f"counts equal the GPU's"}
+                      f"counts equal the GPU's",
+            "host": host_info(T)}
+
+
+def cpu_baseline_c4_sketch(ctx, buf, seg, mask):
+    """Config 4's sketch phase on the host: the reference-style port over a
+    bounded sample of the genomes, one worker thread per host core over genomes
+    (the reference's cilk_for over files, kmer_set.cpp:112-133); every sampled
+    set is checked equal to the GPU's."""
+    T = cpu_threads()
+    n = min(len(seg) - 1, 4 * T)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[n], seg[:n + 1], W, mask, sksffi.SKS_BOTTOM_S, C4_S)
+    host = [buf[seg[i]:seg[i + 1]].cpu().numpy().tobytes() for i in range(n)]
+    sets, windows, dt = cpu_sketch_many(host, mask, "bottom", C4_S, T)
+    for i in range(n):
+        assert np.array_equal(sets[i].elems(), ss.sketch(i)), f"config-4 CPU set {i} differs"
+    return {"value": windows / dt, "unit": "k-mers/s", "cores": T, "kind": "port",
+            "sample": f"{n} of the {C4_GENOMES} config-4 genomes (5 Mb each, {windows} windows, "
+                      f"bottom-s {C4_S}), oracle/ref_port.cpp bottom_runs, {T} threads over "
+                      f"genomes, {dt:.2f} s; sets equal to the GPU's",
+            "host": host_info(T)}
 
 
 def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
@@ -661,9 +756,10 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
     if rank == 0:
         assert (counts == counts.T).all() and counts[0, 1] > 0
         assert (sizes[g0:g1] == local_sizes[:n_local]).all()
-    cpu = None
+    cpu = cpu_sk = None
     if cpu_pairs and rank == 0 and world == 1:
         cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
+        cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask)
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s", "scaling": "strong",
@@ -689,13 +785,59 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
                    "collective": ("all_gather_into_tensor join layouts + all_reduce counts "
                                   f"({backend_label()})" if collective() else "none")},
         "cpu_baseline": cpu,
+        "cpu_baseline_sketch_phase": cpu_sk,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
         "ms_end_to_end": (t_sketch + t_pairs) * 1e3,
     }
 
 
 # ---- config 5 ------------------------------------------------------------------------
-def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
+def cpu_baseline_c5(ctx, buf, seg, masks, ones):
+    """Config 5 on the host over a bounded sample: 2 of the 8 seeds x the first
+    G genomes; per seed the reference-style port sketches the genomes (threads
+    over genomes, kmer_set.cpp:112-133), counts all G x G ordered pairs
+    (threads over pairs, kmer_set.cpp:167-184) and computes containment and ANI
+    (ani_estimation.cpp:24-42, the oracle's restatement); the timed region is
+    the whole per-seed pipeline, like a GPU sweep step.  Seed 0's counts are
+    checked against the GPU's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    T = cpu_threads()
+    G = min(len(seg) - 1, 2 * T)
+    seeds = [0, 1]
+    host = [buf[seg[i]:seg[i + 1]].cpu().numpy().tobytes() for i in range(G)]
+    t_all = 0.0
+    windows = 0
+    counts0 = None
+    for sd in seeds:
+        sets, nw, dt = cpu_sketch_many(host, masks[sd], "bottom", C4_S, T)
+        t0 = time.perf_counter()
+        counts = pyoracle.refport_all_pairs(sets, threads=T)
+        sizes = np.diag(counts)
+        ani = [pyoracle.binomial_estimator(pyoracle.containment(int(counts[i, j]), int(sizes[i])),
+                                           ones[sd]) for i in range(G) for j in range(G)]
+        t_all += dt + time.perf_counter() - t0
+        windows += nw
+        if sd == 0:
+            counts0 = counts
+        del ani
+    seg0 = seg[:G + 1]
+    ss = ctx.sketch_build(buf.data_ptr(), seg0[-1], seg0, W, masks[0], sksffi.SKS_BOTTOM_S, C4_S)
+    out = torch.zeros((G, G), dtype=torch.int32, device="cuda")
+    d, st, sz = ss.device_ptrs()
+    ctx.intersect_all(d, st, sz, 1, G, 0, G, out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), counts0), "config-5 CPU counts differ from the GPU's"
+    return {"value": len(seeds) * G * G / t_all, "unit": "ordered (pair, seed) ANIs/s", "cores": T,
+            "kind": "port", "sketch_kmers_per_s": windows / t_all,
+            "sample": f"{len(seeds)} of the {C5_SEEDS} seeds x the first {G} genomes "
+                      f"({G * G} ordered pairs per seed, bottom-s {C4_S}): sketch (threads over "
+                      f"genomes) + all pairs (threads over pairs) + containment/ANI, "
+                      f"oracle/ref_port.cpp, {t_all:.2f} s; seed-0 counts equal the GPU's",
+            "host": host_info(T)}
+
+
+def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2, cpu=False):
     """Config 5: 8 spaced seeds (w=31/k=21, mask seeds 0..7) over the first 200
     genomes of config 4, bottom-s s=10000; per seed: sketch all genomes, count
     all 200 x 200 ordered pairs (symmetric tiles), containment + ANI on the host
@@ -769,6 +911,7 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
     pool.shutdown()
     t = total / max(timed, 1)
     c = cons.numpy()
+    cpu_b = cpu_baseline_c5(ctx, buf, seg, masks, ones) if cpu else None
     return {
         "metric": "seed-sweep genome-pairs ANI/s", "value": C5_SEEDS * n * n / t,
         "unit": "ordered (pair, seed) ANIs/s", "scaling": "strong", "ms_per_sweep": t * 1e3,
@@ -781,6 +924,7 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2):
                    "seeds_in_flight": max(1, lanes_n),
                    "collective": (f"all_reduce of ANI sums ({backend_label()})"
                                   if collective() else "none")},
+        "cpu_baseline": cpu_b,
     }
 
 
@@ -892,7 +1036,8 @@ def main():
 
     c2 = None
     if not args.no_c2:
-        c2 = run_c2(ctx, mask, steps=max(4, args.steps), warmup=2, inflight=args.inflight)
+        c2 = run_c2(ctx, mask, steps=max(4, args.steps), warmup=2, inflight=args.inflight,
+                    cpu=rank == 0 and world == 1 and not args.no_cpu_baseline)
 
     pairs = None
     if not args.no_pairs:
@@ -910,7 +1055,8 @@ def main():
     sweep = None
     if not args.no_sweep:
         sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1,
-                               lanes_n=args.sweep_inflight)
+                               lanes_n=args.sweep_inflight,
+                               cpu=rank == 0 and world == 1 and not args.no_cpu_baseline)
 
     cpu = cpu_x = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -211,6 +211,9 @@ def refport():
         L.rp_sketch_runs.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, u64p,
                                      C.c_uint64, C.c_int64]
         L.rp_sketch_runs.restype = C.c_void_p
+        L.rp_bottom_runs.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, u64p,
+                                     C.c_uint64, C.c_int64]
+        L.rp_bottom_runs.restype = C.c_void_p
         L.rp_sketch_files.argtypes = [C.POINTER(C.c_char_p), C.c_int, C.c_int, u64p, C.c_uint64,
                                       C.c_int64, C.c_int, C.POINTER(C.c_void_p)]
         L.rp_set_from_elems.argtypes = [C.c_void_p, C.c_uint64, C.c_int, u64p]
@@ -258,6 +261,16 @@ def refport_sketch_codes(codes, lens, w, m, c=200, nonce=1, flavour=0):
     lens = np.ascontiguousarray(lens, dtype=np.uint64)
     return RefPortSet(refport().rp_sketch_runs(codes.ctypes.data, lens.ctypes.data, len(lens),
                                                w, _mask_arr(m), c, nonce))
+
+
+def refport_bottom_codes(codes, lens, w, m, s, nonce=1, flavour=0):
+    """Reference-style bottom-s (ref_port.cpp bottom_runs): the s distinct k-mers
+    with the smallest (fmh, k-mer)."""
+    refport().rp_set_flavour(flavour)
+    codes = np.ascontiguousarray(codes, dtype=np.uint8)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    return RefPortSet(refport().rp_bottom_runs(codes.ctypes.data, lens.ctypes.data, len(lens),
+                                               w, _mask_arr(m), s, nonce))
 
 
 def refport_set_from_elems(elems, w, m):

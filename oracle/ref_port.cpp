@@ -27,6 +27,7 @@
 #include <functional>
 #include <numeric>
 #include <random>
+#include <set>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -190,6 +191,59 @@ kmer_set* sketch_runs(const uint8_t* codes, const uint64_t* lens, uint64_t n_run
   return s;
 }
 
+// Bottom-s in the reference's style (the reference has no bottom-s; this is
+// what its API expresses it with): the same per-window loop and kmer objects,
+// and a std::function predicate that keeps the s distinct k-mers with the
+// smallest (fmh, masked bits) in a std::set plus an unordered_map for
+// membership — the reference's own containers — and returns false, so the
+// window list stays empty.  The kmer_set is then built from the kept k-mers.
+kmer_set* bottom_runs(const uint8_t* codes, const uint64_t* lens, uint64_t n_runs,
+                      const Sketcher& sk, uint64_t s) {
+  const frac_min_hash fmh = sk.fmh;
+  struct Key {
+    uint64_t f, hi, lo;
+    bool operator<(const Key& o) const {
+      return f != o.f ? f < o.f : (hi != o.hi ? hi < o.hi : lo < o.lo);
+    }
+  };
+  std::set<Key> kept;                  // the s smallest so far
+  std::unordered_map<kmer, int, kmer_hash> member;
+  std::function<bool(const kmer)> cond = [&](const kmer k) {
+    if (s == 0) return false;
+    const Key key{fmh(k), k.masked_bits.b[1], k.masked_bits.b[0]};
+    if (kept.size() >= s && !(key < *kept.rbegin())) return false;
+    if (member.find(k) != member.end()) return false;
+    kept.insert(key);
+    member[k] = 1;
+    if (kept.size() > s) {
+      const Key last = *kept.rbegin();
+      kept.erase(std::prev(kept.end()));
+      kmer gone{k.window_length, kbits(), k.mask, kbits()};
+      gone.masked_bits.b[0] = last.lo;
+      gone.masked_bits.b[1] = last.hi;
+      member.erase(gone);
+    }
+    return false;
+  };
+  std::vector<kmer> ks;
+  uint64_t off = 0;
+  for (uint64_t r = 0; r < n_runs; ++r) {
+    nucleotide_string_to_kmers(ks, codes + off, (int64_t)lens[r], sk.mask, sk.w, cond);
+    off += lens[r];
+  }
+  std::vector<kmer> sel;
+  for (const Key& key : kept) {
+    kmer k{sk.w, kbits(), sk.mask, kbits()};
+    k.masked_bits.b[0] = key.lo;
+    k.masked_bits.b[1] = key.hi;
+    k.kmer_bits = k.masked_bits;
+    sel.push_back(k);
+  }
+  kmer_set* out = new kmer_set();
+  out->insert_kmers(sel);
+  return out;
+}
+
 int kmer_set_intersection(const kmer_set& a, const kmer_set& b) {
   if (a.kmer_set_size() < b.kmer_set_size()) return kmer_set_intersection(b, a);
   int n = 0;
@@ -265,6 +319,13 @@ void* rp_sketch_runs(const uint8_t* codes, const uint64_t* lens, uint64_t n_runs
                      const uint64_t* mask, uint64_t c, int64_t nonce) {
   rp::Sketcher sk(mask[0], mask[1], w, nonce, c);
   return rp::sketch_runs(codes, lens, n_runs, sk);
+}
+
+// One genome (as runs) -> bottom-s kmer_set handle (see bottom_runs).
+void* rp_bottom_runs(const uint8_t* codes, const uint64_t* lens, uint64_t n_runs, int w,
+                     const uint64_t* mask, uint64_t s, int64_t nonce) {
+  rp::Sketcher sk(mask[0], mask[1], w, nonce, 1);
+  return rp::bottom_runs(codes, lens, n_runs, sk, s);
 }
 
 // Files -> kmer_set handles, `threads` workers over files (cilk_for stand-in).

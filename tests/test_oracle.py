@@ -94,6 +94,23 @@ def test_refport_matches_oracle_spaced_and_wide():
             assert np.array_equal(want, got), (w, k, flavour)
 
 
+def test_refport_bottom_s_matches_oracle():
+    """The reference-style bottom-s port (the CPU baseline of the bottom-s
+    configs) keeps the same set as the oracle's bottom-s definition."""
+    seq = synth.bases(40000, seed=13)
+    seq[1000:1030] = ord("N")
+    runs = O.cut_runs(seq.tobytes())
+    codes = np.frombuffer(b"".join(runs), dtype=np.uint8)
+    lens = np.array([len(r) for r in runs], dtype=np.uint64)
+    assert O.refport_bottom_codes(codes, lens, 31, O.mask(31, 21, 2), 0).size() == 0
+    for (w, k, s) in [(31, 21, 300), (21, 21, 1), (40, 30, 500), (31, 21, 100000)]:
+        m = O.mask(w, k, 2)
+        for flavour in (0, 1):
+            want, _ = O.sketch(runs, w, m, "bottom", s, 1, flavour)
+            got = O.refport_bottom_codes(codes, lens, w, m, s, 1, flavour).elems()
+            assert np.array_equal(want, got), (w, k, s, flavour)
+
+
 def test_refport_intersection_matches_merge():
     runs_a = O.cut_runs(synth.bases(30000, seed=21).tobytes())
     runs_b = O.cut_runs(synth.bases(30000, seed=21, mut_seed=5, mut_rate=0.01).tobytes())
