@@ -630,7 +630,7 @@ int sks_ctx_set_scan_grid(sks_ctx* c, int grid) {
 
 int sks_ctx_set_intersect_kernel(sks_ctx* c, int kind) {
   if (!c) return sks::fail(SKS_E_ARG, "null ctx");
-  if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_GLOBAL)
+  if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_POSTINGS)
     return sks::fail(SKS_E_ARG, "sks_ctx_set_intersect_kernel: unknown kernel");
   c->intersect_algo = kind;
   return SKS_OK;

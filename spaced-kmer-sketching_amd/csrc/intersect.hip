@@ -1231,6 +1231,51 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
 
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) total += h_sizes[i];
+  const bool sep_rows_any = !sym && (row_begin % kTile) != 0;
+  if ((algo == kIntersectAuto || algo == kIntersectPostings) && total < (1ull << 32)) {
+    // block postings + MFMA counts (postings.hip).  The layout is checked after
+    // the join (its stat is read back with the counts); a build whose group
+    // outgrew the place kernel or whose bucket outgrew the join table is
+    // redone with twice the buckets, and past 2^14 the older kernels take over
+    const uint32_t rn = row_end - row_begin;
+    uint64_t r_total = 0;
+    if (sep_rows_any)
+      for (uint32_t i = row_begin; i < row_end; ++i) r_total += h_sizes[i];
+    for (uint32_t log_b = postings_log_b(max_size); log_b <= kJMaxLogB; ++log_b) {
+      const size_t oc = postings_bytes(n, log_b, total);
+      const size_t orr = sep_rows_any ? postings_bytes(rn, log_b, r_total) : 0;
+      const size_t tmp = std::max(postings_temp_bytes(n, log_b, total),
+                                  sep_rows_any ? postings_temp_bytes(rn, log_b, r_total) : 0);
+      const size_t o_r = align16(oc), o_st = o_r + align16(orr), o_tmp = o_st + 256;
+      if ((e = work.reserve(o_tmp + tmp)) != hipSuccess) return e;
+      char* w = static_cast<char*>(work.ptr);
+      uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_st);
+      if ((e = hipMemsetAsync(stat, 0, 8, s)) != hipSuccess) return e;
+      PostingsLayout cl{}, rl{};
+      if ((e = postings_build(data, starts, sizes, h_sizes.data(), 0, n, log_b, w, w + o_tmp, stat, &cl,
+                              s)) != hipSuccess)
+        return e;
+      rl = cl;
+      if (sep_rows_any &&
+          (e = postings_build(data, starts, sizes, h_sizes.data(), row_begin, rn, log_b, w + o_r,
+                              w + o_tmp, stat, &rl, s)) != hipSuccess)
+        return e;
+      const uint32_t r_blk0 = sep_rows_any ? 0 : (sym ? 0 : row_begin / kTile);
+      if ((e = postings_join(rl, r_blk0, cl, n, log_b, sym, row_begin, row_end, tile_begin, tile_end,
+                             nullptr, false, out, s)) != hipSuccess)
+        return e;
+      uint32_t h_stat[2] = {0, 0};
+      if ((e = pinned_d2h(h_stat, stat, 8, s)) != hipSuccess) return e;
+      if (dbg)
+        fprintf(stderr, "[sks intersect] postings n=%u log_b=%u max bucket %u group overflow %u\n", n,
+                log_b, h_stat[0], h_stat[1]);
+      if (h_stat[1] == 0 && h_stat[0] <= postings_max_distinct()) {
+        *used_tiles = true;
+        return hipSuccess;
+      }
+      if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
+    }
+  }
   // the join's per-(block, bucket, slot) counting arrays take 8 B x 64 x B per
   // block; beyond a few GB of them (very many sketches) the merge tiles are used
   const bool join_fits = total < (1ull << 32) &&

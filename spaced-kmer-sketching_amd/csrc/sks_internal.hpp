@@ -155,6 +155,7 @@ constexpr int kIntersectAuto = 0;    // join when the bucket sizes allow, else m
 constexpr int kIntersectMerge = 1;   // k_tiles (pairwise LDS merges)
 constexpr int kIntersectJoin = 2;    // k_join (LDS hash join), merge tiles if infeasible
 constexpr int kIntersectGlobal = 3;  // one wavefront per pair from global memory
+constexpr int kIntersectPostings = 4;  // block postings join + MFMA counts (postings.hip)
 uint64_t intersect_sym_tiles(uint32_t n);
 
 // Join layout (input of k_join, intersect.hip): blocks of 64 consecutive
@@ -183,6 +184,35 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t n,
                        uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, int32_t* out, hipStream_t s);
+
+// Block postings (postings.hip): per 64-sketch block and hash bucket, the
+// distinct values with a 64-bit mask of the block's sketches holding each,
+// every bucket with a precomputed linear-probing table position per posting.
+struct PostingsLayout {
+  const uint64_t* ent;     // {value, mask} pairs
+  const uint16_t* pos;     // slot of each posting in its bucket's table (2 slots per posting)
+  const uint32_t* bkt;     // [blk][B][2] = {first posting relative to bstart[blk], count}
+  const uint64_t* bstart;  // [n_blk + 1] first posting slot of each block
+};
+uint32_t postings_log_b(uint32_t max_size);
+uint32_t postings_max_distinct();  // largest bucket (postings) the join takes
+size_t postings_bytes(uint32_t count, uint32_t log_b, uint64_t total);       // the layout
+size_t postings_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total);  // build scratch
+// Layout of sketches [first, first + count) (h_sizes: host copy of all sizes)
+// into `out` (postings_bytes); d_stat[0] is raised to the largest bucket,
+// d_stat[1] to the largest (block, group) element count when one exceeded the
+// build's capacity (then the layout is invalid: raise log_b).
+hipError_t postings_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                          const uint32_t* h_sizes, uint32_t first, uint32_t count, uint32_t log_b,
+                          void* out, void* temp, uint32_t* d_stat, PostingsLayout* L, hipStream_t s);
+// Tiles of the n x n (sym) or rows x n matrix, or the explicit (I, J) list
+// d_tiles[2t], d_tiles[2t + 1] for t in [tile_begin, tile_end) (written to
+// both halves, like sym); packed: out = [tile - tile_begin][64][64] partial
+// counts instead of the matrix.  `out` must be zeroed.
+hipError_t postings_join(const PostingsLayout& rows, uint32_t r_blk0, const PostingsLayout& cols,
+                         uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
+                         uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles,
+                         bool packed, int32_t* out, hipStream_t s);
 
 // ---- device FASTA ingress (ingress.hip) -------------------------------------------------
 // strings_from_fasta on the device: writes the host parser's record stream

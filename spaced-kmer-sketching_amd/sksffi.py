@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("SKS_LIB") or os.path.join(PKG_DIR, "lib", "libsks.so"
 
 SKS_FRAC_MOD = 0
 SKS_BOTTOM_S = 1
-INTERSECT_AUTO, INTERSECT_MERGE, INTERSECT_JOIN, INTERSECT_GLOBAL = 0, 1, 2, 3
+INTERSECT_AUTO, INTERSECT_MERGE, INTERSECT_JOIN, INTERSECT_GLOBAL, INTERSECT_POSTINGS = 0, 1, 2, 3, 4
 FLAVOUR_BOOST_MIX = 0
 FLAVOUR_BOOST_LEGACY = 1
 
@@ -321,7 +321,7 @@ class Context:
                                              tile_end, C.c_void_p(out)))
 
     def set_intersect_kernel(self, kind):
-        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL (sks.h); all give identical counts."""
+        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL / _POSTINGS (sks.h); all give identical counts."""
         check(lib().sks_ctx_set_intersect_kernel(self.h, kind))
         self._intersect_kernel = kind
 

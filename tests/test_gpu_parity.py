@@ -481,7 +481,7 @@ def test_argument_errors(torch_cuda, ctx):
 
 
 KERNELS = [sksffi.INTERSECT_AUTO, sksffi.INTERSECT_MERGE, sksffi.INTERSECT_JOIN,
-           sksffi.INTERSECT_GLOBAL]
+           sksffi.INTERSECT_GLOBAL, sksffi.INTERSECT_POSTINGS]
 
 
 @pytest.fixture

@@ -38,7 +38,12 @@ def main():
     data, starts, sizes = ss.device_ptrs()
     T = sksffi.intersect_sym_tiles(n)
     ref = None
-    for name, k in (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN)):
+    kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN),
+               ("postings", sksffi.INTERSECT_POSTINGS))
+    only = os.environ.get("SKS_BENCH_KERNELS")
+    if only:
+        kernels = tuple(x for x in kernels if x[0] in only.split(","))
+    for name, k in kernels:
         ctx.set_intersect_kernel(k)
         out = torch.empty((n, n), dtype=torch.int32, device="cuda")
         ms = []
