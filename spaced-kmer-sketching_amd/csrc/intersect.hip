@@ -1232,7 +1232,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) total += h_sizes[i];
   const bool sep_rows_any = !sym && (row_begin % kTile) != 0;
-  if ((algo == kIntersectAuto || algo == kIntersectPostings) && total < (1ull << 32)) {
+  if (algo == kIntersectPostings && total < (1ull << 32)) {
     // block postings + MFMA counts (postings.hip).  The layout is checked after
     // the join (its stat is read back with the counts); a build whose group
     // outgrew the place kernel or whose bucket outgrew the join table is

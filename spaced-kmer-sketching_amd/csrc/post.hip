@@ -526,12 +526,16 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     uint64_t* skeys = reinterpret_cast<uint64_t*>(smem);
     uint32_t* sbin = reinterpret_cast<uint32_t*>(smem + kCap * sizeof(uint64_t));
     const int shift = key_bits > kBkLog ? key_bits - kBkLog : 0;
+    // bucket = top kBkLog bits of the packed key; packed keys fit key_bits, the
+    // clamp only keeps a key that did not (a future packing change) inside sbin,
+    // in the last bucket, which keeps the order (larger keys, larger buckets)
+    auto bk_of = [&](uint64_t key) { return (uint32_t)min(key >> shift, (uint64_t)(kBk - 1)); };
 #pragma unroll
     for (uint32_t q = 0; q < kBkPer; ++q) sbin[tid * kBkPer + q] = 0;
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j)
-      if (tid * ITEMS + j < n) atomicAdd(&sbin[(uint32_t)(k[j] >> shift)], 1u);
+      if (tid * ITEMS + j < n) atomicAdd(&sbin[bk_of(k[j])], 1u);
     __syncthreads();
     uint32_t cb[kBkPer], sum = 0, mx = 0;
 #pragma unroll
@@ -572,7 +576,7 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
       __syncthreads();
 #pragma unroll
       for (uint32_t j = 0; j < ITEMS; ++j)
-        if (tid * ITEMS + j < n) skeys[atomicAdd(&sbin[(uint32_t)(k[j] >> shift)], 1u)] = k[j];
+        if (tid * ITEMS + j < n) skeys[atomicAdd(&sbin[bk_of(k[j])], 1u)] = k[j];
       __syncthreads();
       // this thread's buckets are the contiguous range [excl, excl + sum); keys
       // of earlier buckets are smaller, so an insertion sort of the range only

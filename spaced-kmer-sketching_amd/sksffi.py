@@ -288,9 +288,11 @@ class Context:
         check(lib().sks_ctx_create(device, C.c_void_p(stream) if stream else None, C.byref(h)))
         self.h = h
         self.device = device
+        self.stream = stream or 0  # hipStream_t handle the context's work is queued on (0: null)
 
     def set_stream(self, stream):
         check(lib().sks_ctx_set_stream(self.h, C.c_void_p(stream) if stream else None))
+        self.stream = stream or 0
 
     def set_scan_grid(self, grid):
         check(lib().sks_ctx_set_scan_grid(self.h, grid))

@@ -196,6 +196,21 @@ def test_bottom_s_fused_sort_paths(torch_cuda, ctx):
             check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
 
 
+@pytest.mark.parametrize("w,k", [(11, 8), (9, 5), (13, 12)])
+def test_bottom_s_fused_small_k(torch_cuda, ctx, w, k):
+    """k_bottom_fused with packed keys of 2k <= 24 bits: at 2k <= 12 the bucket
+    is the whole key (shift 0), above it the top 12 bits; several genomes so the
+    fused kernel (not the single-genome device-wide path) runs; against the
+    oracle, both flavours."""
+    genomes = [synth.bases(40_000 + 3001 * i, seed=900 + i, mut_seed=950 + i,
+                           mut_rate=0.01 * i).tobytes() for i in range(6)]
+    m = O.mask(w, k, 1)
+    for flavour in (0, 1):
+        for s_ in (50, 3000):
+            ss, _ = build(torch_cuda, ctx, genomes, w, m, "bottom", s_, flavour)
+            check_against_oracle(ss, genomes, w, m, "bottom", s_, flavour)
+
+
 def test_bottom_s_unfused_paths(torch_cuda, ctx, monkeypatch):
     """The per-genome fused post kernel is the default for builds of two or more
     genomes of <= 16384 candidates (a single genome takes the device-wide path);
