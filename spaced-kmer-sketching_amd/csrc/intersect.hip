@@ -21,11 +21,19 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include "join_common.hpp"
 #include "sks_internal.hpp"
 
 namespace sks {
 
 namespace {
+
+using jc::fp_slot;
+using jc::fp_tag;
+using jc::kFFree;
+using jc::kFLog;
+using jc::kFSlots;
+using jc::sym_tile;
 
 constexpr int kB = 256;
 constexpr int kWavesPerBlock = kB / 64;
@@ -221,17 +229,6 @@ __global__ void k_part_stats(const uint32_t* __restrict__ pos, uint32_t n, uint3
   atomicMax(&stats[1], sum);
 }
 
-__device__ __forceinline__ void sym_tile(uint64_t t, uint32_t nb, uint32_t& I, uint32_t& J) {
-  uint32_t i = 0;
-  uint64_t rem = t;
-  while (rem >= nb - i) {  // row i of the upper triangle holds nb - i tiles
-    rem -= nb - i;
-    ++i;
-  }
-  I = i;
-  J = i + (uint32_t)rem;
-}
-
 __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
   // lds[pos * kSlots + slot], pos < a.P (dynamic: sized to the largest part)
   // (the only LDS object, so its base is LDS address 0 and element offsets
@@ -389,14 +386,7 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 #ifndef SKS_JOIN_THREADS
 #define SKS_JOIN_THREADS 512
 #endif
-// 4096 table slots for <= 1024 column elements per chunk (load <= 1/4; 2048
-// slots at load <= 1/2 measured slower: longer probe chains)
-#ifndef SKS_JOIN_LOG_SLOTS
-#define SKS_JOIN_LOG_SLOTS 12
-#endif
 constexpr int kJB = SKS_JOIN_THREADS;       // threads per k_join workgroup
-constexpr int kFLog = SKS_JOIN_LOG_SLOTS;
-constexpr int kFSlots = 1 << kFLog;          // 32-bit table slots
 constexpr int kJCap = 1024;                  // column elements per chunk
 constexpr int kJMade = kJCap / kJB;         // column elements per thread per chunk
 constexpr int kJWin = 256;                  // bucket offsets staged per window
@@ -690,16 +680,7 @@ __device__ unsigned long long g_join_stamps[8];
 // a probe reads 32-bit slots and, on a fingerprint match, the 16-byte entry.
 // Values need no reserved "empty" key (the empty marker lives in the slot), and
 // the entries need no reset: the next chunk's staging overwrites them.
-constexpr uint32_t kFFree = 0xFFFFFFFFu;
 static_assert(kJCap <= 1024, "entry index must fit 10 bits");
-
-__device__ __forceinline__ uint32_t fp_slot(uint64_t v) {
-  return (((uint32_t)v ^ (uint32_t)(v >> 32)) * 0x85EBCA77u) >> (32 - kFLog);
-}
-__device__ __forceinline__ uint32_t fp_tag(uint64_t v) {  // 22 bits, never all ones
-  const uint32_t t = (uint32_t)((v * 0xD6E8FEB86659FD93ull) >> 42);
-  return t == 0x3FFFFFu ? 0x3FFFFEu : t;
-}
 
 __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
 #ifdef SKS_JOIN_STAMPS
@@ -1276,6 +1257,28 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
     }
   }
+  if (algo == kIntersectRange && total < (1ull << 32)) {
+    // range join (rjoin.hip): bounds, positions and column-block bucket starts
+    // only; the join reads the sketches where they lie
+    const uint32_t log_b = join_log_b(max_size), B = 1u << log_b;
+    const size_t o_bnd = 0, o_pos = align16((size_t)(B + 1) * 8);
+    const size_t o_pre = align16(o_pos + (size_t)n * (B + 1) * 4);
+    const size_t o_end = align16(o_pre + (size_t)n_cb * (B + 1) * 4);
+    if ((e = work.reserve(o_end)) != hipSuccess) return e;
+    char* w = static_cast<char*>(work.ptr);
+    uint64_t* bounds = reinterpret_cast<uint64_t*>(w + o_bnd);
+    uint32_t* pos = reinterpret_cast<uint32_t*>(w + o_pos);
+    uint32_t* pre = reinterpret_cast<uint32_t*>(w + o_pre);
+    if (dbg) fprintf(stderr, "[sks intersect] range join n=%u B=%u tiles=%llu\n", n, B, (unsigned long long)tiles);
+    if ((e = rjoin_bounds(data, starts, sizes, n, B, bounds, s)) != hipSuccess) return e;
+    if ((e = rjoin_pos(data, starts, sizes, n, B, bounds, pos, s)) != hipSuccess) return e;
+    if ((e = rjoin_block_prefix(pos, n, B, pre, s)) != hipSuccess) return e;
+    if ((e = rjoin_launch(data, starts, pos, pre, n, B, sym, row_begin, row_end, tile_begin, tile_end,
+                          nullptr, false, out, s)) != hipSuccess)
+      return e;
+    *used_tiles = true;
+    return hipSuccess;
+  }
   // the join's per-(block, bucket, slot) counting arrays take 8 B x 64 x B per
   // block; beyond a few GB of them (very many sketches) the merge tiles are used
   const bool join_fits = total < (1ull << 32) &&
@@ -1375,6 +1378,23 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     }
     B <<= 1;
   }
+}
+
+hipError_t launch_value_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                               uint32_t n, uint32_t B, uint64_t* bounds, hipStream_t s) {
+  hipLaunchKernelGGL(k_bounds, dim3((B + 1 + kB - 1) / kB), dim3(kB), 0, s, data, starts, sizes, n,
+                     std::min<uint32_t>(n, 64), B, bounds);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket_pos(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                             uint32_t n, uint32_t B, const uint64_t* bounds, uint32_t* pos,
+                             hipStream_t s) {
+  const uint64_t items = (uint64_t)n * (B + 1);
+  if (!items) return hipSuccess;
+  hipLaunchKernelGGL(k_bucket_pos, dim3((unsigned)((items + kB - 1) / kB)), dim3(kB), 0, s, data, starts,
+                     sizes, n, B, bounds, pos);
+  return hipGetLastError();
 }
 
 uint64_t intersect_sym_tiles(uint32_t n) {

@@ -1,0 +1,606 @@
+// Kernel 2 (default from round 3) — all-pairs intersection straight from the
+// sorted sketches ("range join").
+//
+// The reference counts |A ∩ B| by probing the larger hash map for every
+// element of the smaller set (kmer_set.cpp:23-41), one pair per cilk_for
+// iteration (kmer_set.cpp:167-184).  As in k_join (intersect.hip), the n x n
+// matrix is cut into 64 x 64 tiles of (row block, column block) and a
+// workgroup joins the two blocks in an LDS hash table: the column elements of
+// a chunk go into a fingerprint table (value -> 64-bit mask of the columns
+// holding it), every row element probes once, and a hit with mask m adds m to
+// the row's bit-sliced counters (a carry chain of LDS atomic XORs).
+//
+// What differs is the input.  k_join reads a hash-bucketed, block-major copy
+// of the sketches that six launches build per call (counts, column sums, scan,
+// offsets, staging, placement: ~0.2 ms for config 4).  Here the sketches are
+// read where they lie: the value range is cut into B buckets by common bounds,
+// and since every sketch is sorted, sketch i's part of bucket b is the
+// contiguous range [pos[i][b], pos[i][b + 1]).  A chunk (whole buckets [bs, be)
+// of the column block holding <= cap elements, or a slice of one larger bucket)
+// is 64 contiguous ranges, one per column sketch, concatenated in sketch order;
+// the row elements of [bs, be) are 64 contiguous ranges too, and a row
+// element's row is the range it came from (no id array).  The whole "layout"
+// is bounds (B + 1 u64), pos (n x (B + 1) u32) and each column block's bucket
+// starts pre[blk][b] = sum over its sketches of pos[i][b]: three small launches.
+//
+// Thread map for the ranges: thread t serves sketch s = t / 8 of the block,
+// lane k = t % 8 takes elements k, k + 8, ... of its range, so each wave reads
+// 8 sketches' ranges as 64-byte runs.  Loads run ahead of their use: waves
+// 0-1 read the bucket positions of the chunk after the next one into
+// registers, and every thread its first two column and row elements of the
+// next chunk, while the current chunk is inserted and probed; the ranges are
+// double-buffered in LDS.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "join_common.hpp"
+#include "sks_internal.hpp"
+
+namespace sks {
+
+namespace {
+
+using jc::fp_slot;
+using jc::fp_tag;
+using jc::kFFree;
+using jc::kFSlots;
+using jc::sym_tile;
+
+constexpr int kRB = 512;              // threads per workgroup (8 waves)
+constexpr int kTile = 64;
+constexpr int kRCap = 1024;           // column elements per chunk (entry index: 10 bits)
+constexpr int kRMade = kRCap / kRB;   // column elements per thread per chunk (insert map)
+constexpr int kRWin = 256;            // bucket starts staged per window
+constexpr int kPlanes = 32;           // bit-sliced counter planes (any int32 count)
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr int kPB = 256;              // threads of the prefix kernel
+constexpr uint64_t kMaxGrid = 1ull << 22;
+static_assert(kRCap <= 1024, "entry index must fit 10 bits");
+
+// pre[blk * (B + 1) + b] = sum of pos[i * (B + 1) + b] over the block's sketches
+__global__ __launch_bounds__(kPB) void k_rj_prefix(const uint32_t* __restrict__ pos, uint32_t n,
+                                                    uint32_t B, uint32_t* __restrict__ pre) {
+  const uint64_t B1 = B + 1;
+  const uint64_t idx = (uint64_t)blockIdx.x * kPB + threadIdx.x;
+  const uint32_t n_blk = (n + kTile - 1) / kTile;
+  if (idx >= (uint64_t)n_blk * B1) return;
+  const uint32_t blk = (uint32_t)(idx / B1), b = (uint32_t)(idx % B1);
+  const uint32_t i0 = blk * kTile, i1 = min(n, i0 + kTile);
+  uint32_t t = 0;
+  for (uint32_t i = i0; i < i1; ++i) t += pos[i * B1 + b];
+  pre[idx] = t;
+}
+
+// Common bucket bounds: bounds[b] = mean over up to 64 sample sketches (spread
+// over the set) of each one's b/B quantile (intersect.hip k_bounds' rule),
+// one wave per bound so the samples are read in parallel.  Any non-decreasing
+// bounds give exact counts: each sample's quantiles are non-decreasing in b,
+// and the same reduction tree for every b keeps the rounded means so.
+__global__ __launch_bounds__(kPB) void k_rj_bounds(const uint64_t* __restrict__ data,
+                                                    const uint64_t* __restrict__ starts,
+                                                    const uint32_t* __restrict__ sizes, uint32_t n,
+                                                    uint32_t B, uint64_t* __restrict__ bounds) {
+  const uint32_t b = blockIdx.x * (kPB / 64) + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (b > B) return;
+  const uint32_t K = min(n, 64u);
+  double x = 0.0, used = 0.0;
+  if (lane < K && b > 0 && b < B) {
+    const uint32_t i = (uint32_t)((uint64_t)lane * n / K);
+    const uint32_t sz = sizes[i];
+    if (sz) {
+      x = (double)data[starts[i] + (uint64_t)b * sz / B];
+      used = 1.0;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    x += __shfl_xor(x, o, 64);
+    used += __shfl_xor(used, o, 64);
+  }
+  if (lane) return;
+  if (b == 0) { bounds[0] = 0; return; }
+  if (b == B) { bounds[B] = ~0ull; return; }
+  const double m = used > 0.0 ? x / used : 0.0;
+  bounds[b] = m >= 18446744073709549568.0 ? ~0ull : (uint64_t)m;
+}
+
+// pos[i][b] = first element of sketch i >= bounds[b] (pos[i][B] = size): one
+// workgroup per sketch, rounds of kPB x kPosItems consecutive elements (thread
+// t takes elements kPosItems t .. of the round, all loaded before any is
+// used).  An element's bucket is the largest b < B with bounds[b] <= v: a
+// binary search over the bounds (LDS when they fit) for the thread's first
+// element, then a forward walk (the sketch is sorted).  Element e fills
+// pos[b] = e for the buckets after its predecessor's, up to its own.
+// O(size + B) per sketch instead of (B + 1) binary searches of it.
+constexpr int kPosItems = 8;
+template <bool LDS_BOUNDS>
+__global__ __launch_bounds__(kPB) void k_rj_pos(const uint64_t* __restrict__ data,
+                                                 const uint64_t* __restrict__ starts,
+                                                 const uint32_t* __restrict__ sizes, uint32_t B,
+                                                 const uint64_t* __restrict__ g_bounds,
+                                                 uint32_t* __restrict__ pos) {
+  extern __shared__ uint64_t s_bnd[];
+  __shared__ uint32_t s_last[kPB];  // bucket of each thread's last element this round
+  __shared__ uint32_t s_carry;
+  const uint32_t i = blockIdx.x, tid = threadIdx.x;
+  const uint32_t sz = sizes[i];
+  const uint64_t* S = data + starts[i];
+  uint32_t* P = pos + (uint64_t)i * (B + 1);
+  const uint64_t* bnd = g_bounds;
+  if constexpr (LDS_BOUNDS) {
+    for (uint32_t b = tid; b <= B; b += kPB) s_bnd[b] = g_bounds[b];
+    bnd = s_bnd;
+  }
+  if (tid == 0) s_carry = 0xFFFFFFFFu;  // bucket of the element before the round (~0: none)
+  __syncthreads();
+  constexpr uint32_t kRound = kPB * kPosItems;
+  for (uint32_t e0 = 0; e0 < sz; e0 += kRound) {
+    const uint32_t eb = e0 + tid * kPosItems;
+    const uint32_t n_mine = eb < sz ? min((uint32_t)kPosItems, sz - eb) : 0;
+    uint64_t v[kPosItems];
+#pragma unroll
+    for (int u = 0; u < kPosItems; ++u) v[u] = (uint32_t)u < n_mine ? S[eb + u] : 0;
+    uint32_t bk[kPosItems];
+    uint32_t cur = 0;
+    if (n_mine) {
+      uint32_t lo = 0, hi = B - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (bnd[mid] <= v[0]) lo = mid; else hi = mid - 1;
+      }
+      cur = lo;
+    }
+#pragma unroll
+    for (int u = 0; u < kPosItems; ++u) {
+      if ((uint32_t)u < n_mine)
+        while (cur + 1 < B && bnd[cur + 1] <= v[u]) ++cur;
+      bk[u] = cur;
+    }
+    s_last[tid] = n_mine ? bk[n_mine - 1] : 0xFFFFFFFFu;
+    __syncthreads();
+    if (n_mine) {
+      uint32_t prev = tid ? s_last[tid - 1] : s_carry;
+#pragma unroll
+      for (int u = 0; u < kPosItems; ++u) {
+        if ((uint32_t)u >= n_mine) break;
+        for (uint32_t b = prev + 1; b <= bk[u]; ++b) P[b] = eb + u;  // prev = ~0: from bucket 0
+        prev = bk[u];
+      }
+    }
+    __syncthreads();
+    if (tid == 0) s_carry = s_last[(min(kRound, sz - e0) - 1) / kPosItems];
+    __syncthreads();
+  }
+  const uint32_t last = s_carry;  // bucket of the last element (~0: empty sketch)
+  for (uint32_t b = tid; b <= B; b += kPB)
+    if (last == 0xFFFFFFFFu || b > last) P[b] = sz;
+}
+
+struct ChunkRegs {
+  uint64_t c[2], r[2];
+};
+
+struct RJoinArgs {
+  const uint64_t* data;
+  const uint64_t* starts;
+  const uint32_t* pos;   // [n][B + 1]
+  const uint32_t* cpre;  // [n_cb][B + 1] column block bucket starts
+  uint32_t B, n, n_col_blocks, n_groups, buckets_per_group;
+  int sym;
+  uint32_t row_begin, row_end;
+  uint64_t tile_begin;
+  const uint32_t* tiles;  // optional (I, J) list, global block indices, sym semantics
+  int32_t* out;
+  uint64_t ld;
+  uint32_t cap;  // column elements per chunk (<= kRCap)
+  int packed;    // out = [tile - tile_begin][64][64]
+};
+
+// 6 waves per SIMD: three workgroups per CU, as the LDS allows (<= 80 VGPRs)
+__global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
+  __shared__ uint32_t s_slot[kFSlots];
+  __shared__ ulonglong2 s_ent[kRCap];                    // {value, mask of the columns holding it}
+  __shared__ unsigned long long s_pl[kPlanes * kTile];  // plane b of row r at [b * 64 + r]
+  __shared__ uint32_t s_coff[kRWin + 1];
+  __shared__ uint16_t s_next[kRWin];
+  // chunk ranges, double-buffered: column sketch s starts at element s_cb, its
+  // elements are [s_cp[s], s_cp[s + 1]) of the chunk's concatenated order; row
+  // sketch s is [s_rb, s_re)
+  __shared__ uint32_t s_cb[2][kTile], s_cp[2][kTile + 1], s_rb[2][kTile], s_re[2][kTile];
+  __shared__ uint32_t s_self[kTile];
+  __shared__ uint32_t s_top;
+
+  const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
+  const uint32_t grp = blockIdx.x % a.n_groups;
+  uint32_t I, J;
+  if (a.tiles) {
+    I = a.tiles[2 * t];
+    J = a.tiles[2 * t + 1];
+  } else if (a.sym) {
+    sym_tile(t, a.n_col_blocks, I, J);
+  } else {
+    I = (uint32_t)(t / a.n_col_blocks);
+    J = (uint32_t)(t % a.n_col_blocks);
+  }
+  const bool rows_mode = !a.sym && !a.tiles;
+  const uint32_t row0 = (rows_mode ? a.row_begin : 0) + I * kTile;
+  const uint32_t row_lim = rows_mode ? a.row_end : a.n;
+  const uint32_t col0 = J * kTile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);
+  const uint32_t c_valid = min<uint32_t>(kTile, a.n - col0);
+  const uint64_t B1 = a.B + 1;
+  const uint32_t* coff = a.cpre + (uint64_t)J * B1;
+  // a tile on the diagonal: its rows are its columns
+  const bool self_tile = row0 == col0;
+
+  // waves 0 / 1: lane s holds column / row sketch s's start and positions row
+  bool my_ok = false;
+  uint32_t my_st = 0;
+  const uint32_t* my_pos = a.pos;
+  if (wave < 2) {
+    const uint32_t i = wave == 0 ? col0 + lane : row0 + lane;
+    my_ok = (uint32_t)lane < (wave == 0 ? c_valid : r_valid);
+    if (my_ok) {
+      my_st = (uint32_t)a.starts[i];
+      my_pos = a.pos + (uint64_t)i * B1;
+    }
+  }
+  // a chunk's ranges: waves 0-1 read pos[bs], pos[be] of their sketch into
+  // registers (pos_load) one chunk before they store them (store_ranges)
+  auto pos_load = [&](uint32_t bs, uint32_t be, uint32_t& pb, uint32_t& pe) {
+    pb = pe = 0;
+    if (my_ok) {
+      pb = my_pos[bs];
+      pe = my_pos[be];
+    }
+  };
+  auto store_ranges = [&](int buf, uint32_t pb, uint32_t pe) {  // waves 0-1, all lanes
+    if (wave == 0) {
+      const uint32_t c = pe - pb;
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += x;
+      }
+      s_cb[buf][lane] = my_st + pb;
+      s_cp[buf][lane] = incl - c;
+      if (lane == 63) s_cp[buf][kTile] = incl;
+    } else {
+      s_rb[buf][lane] = my_st + pb;
+      s_re[buf][lane] = my_st + pe;
+    }
+  };
+
+  for (int i = tid; i < kFSlots / 4; i += kRB)
+    reinterpret_cast<uint4*>(s_slot)[i] = make_uint4(kFFree, kFFree, kFFree, kFFree);
+  for (int i = tid; i < kPlanes * kTile / 2; i += kRB) reinterpret_cast<uint4*>(s_pl)[i] = make_uint4(0, 0, 0, 0);
+  if (tid < kTile) s_self[tid] = 0;
+  if (tid == 0) s_top = 0;
+  uint32_t top = 0;
+  auto add_hits = [&](uint32_t r, unsigned long long m) {
+    if (self_tile && ((m >> r) & 1ull)) {  // (a slice of a large bucket may not hold it)
+      atomicAdd(&s_self[r], 1u);
+      m &= ~(1ull << r);
+    }
+    unsigned long long* p = &s_pl[r];
+    uint32_t b = 0;
+    for (; m && b < kPlanes; ++b) m &= atomicXor(p + b * kTile, m);
+    top = max(top, b);
+  };
+  auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
+    const uint32_t tag = fp_tag(v);
+    for (;;) {
+      if (x == kFFree) return 0ull;
+      if ((x >> 10) == tag) {
+        const ulonglong2 e = s_ent[x & 1023u];
+        if (e.x == v) return e.y;
+      }
+      h = (h + 1) & (kFSlots - 1);
+      x = s_slot[h];
+    }
+  };
+
+  const int rs_s = tid >> 3, rs_k = tid & 7;  // range map: sketch, lane within it
+  // first two elements of this thread's share of a chunk's column range (chunk
+  // order [c0, c1)) and row range, from the ranges in buffer `rb`
+  auto fetch_first = [&](int rb, uint32_t c0, uint32_t c1, bool rows, ChunkRegs& o) {
+    o.c[0] = o.c[1] = o.r[0] = o.r[1] = 0;
+    if ((uint32_t)rs_s < c_valid) {
+      const uint32_t p0 = s_cp[rb][rs_s], p1 = s_cp[rb][rs_s + 1];
+      const uint32_t x = max(p0, c0) + rs_k, hi = min(p1, c1);
+      const uint64_t* src = a.data + s_cb[rb][rs_s] - p0;
+      if (x < hi) o.c[0] = src[x];
+      if (x + 8 < hi) o.c[1] = src[x + 8];
+    }
+    if (rows && (uint32_t)rs_s < r_valid) {
+      const uint32_t j = s_rb[rb][rs_s] + rs_k, re = s_re[rb][rs_s];
+      if (j < re) o.r[0] = a.data[j];
+      if (j + 8 < re) o.r[1] = a.data[j + 8];
+    }
+  };
+  uint32_t made[kRMade];  // slots this thread created in the current chunk
+#pragma unroll
+  for (int u = 0; u < kRMade; ++u) made[u] = kNoSlot;
+  int buf = 0;
+
+  const uint32_t b0 = grp * a.buckets_per_group;
+  const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
+  for (uint32_t wb = b0; wb < b1; wb += kRWin) {
+    const uint32_t we = min(b1, wb + kRWin);
+    __syncthreads();  // previous window fully consumed
+    for (uint32_t i = tid; i <= we - wb; i += kRB) s_coff[i] = coff[wb + i];
+    __syncthreads();
+    for (uint32_t i = tid; i < we - wb; i += kRB) {
+      const uint32_t cs = s_coff[i];
+      uint32_t lo = i + 1, hi = we - wb;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_coff[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
+      }
+      s_next[i] = (uint16_t)lo;
+    }
+    __syncthreads();
+    auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
+    // the chunk after (bs, be, cs, ce): the next slice of an oversized bucket,
+    // or the next whole buckets (bs == we: none)
+    auto advance = [&](uint32_t bs, uint32_t be, uint32_t ce, uint32_t& nbs, uint32_t& nbe, uint32_t& ncs,
+                       uint32_t& nce) {
+      if (ce < s_coff[be - wb]) {
+        nbs = bs;
+        nbe = be;
+        ncs = ce;
+      } else {
+        nbs = be;
+        nbe = nbs < we ? chunk_end(nbs) : nbs;
+        ncs = s_coff[nbs - wb];
+      }
+      nce = min(s_coff[nbe - wb], ncs + a.cap);
+    };
+    uint32_t bs = wb, be = chunk_end(wb);
+    uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
+    uint32_t qb = 0, qe = 0;  // waves 0-1: pos of the chunk after the current one
+    if (wave < 2) {
+      uint32_t pb, pe;
+      pos_load(bs, be, pb, pe);
+      store_ranges(buf, pb, pe);
+      uint32_t x0, x1, x2, x3;
+      advance(bs, be, ce, x0, x1, x2, x3);
+      if (x0 < we) pos_load(x0, x1, qb, qe);
+    }
+    __syncthreads();
+    // the first two elements of this thread's column / row range of a chunk,
+    // loaded one chunk ahead (the row ones only when the chunk probes)
+    ChunkRegs cur, nxt;
+    fetch_first(buf, cs - s_coff[0], ce - s_coff[0], !(self_tile && ce == s_coff[be - wb]), cur);
+    while (bs < we) {
+      uint32_t nbs, nbe, ncs, nce;
+      advance(bs, be, ce, nbs, nbe, ncs, nce);
+      const bool has_next = nbs < we;
+      const uint32_t cbase = s_coff[bs - wb];  // chunk order: [cs - cbase, ce - cbase)
+      const bool whole = cs == cbase && ce == s_coff[be - wb];
+      // the next chunk's ranges, from registers (its buffer was last read
+      // before the barrier that ended the previous chunk)
+      if (has_next && wave < 2) store_ranges(buf ^ 1, qb, qe);
+
+      // 0) free the previous chunk's slots and stage this chunk's column
+      //    elements as entries {value, column bit}
+#pragma unroll
+      for (int u = 0; u < kRMade; ++u) {
+        if (made[u] != kNoSlot) s_slot[made[u]] = kFFree;
+        made[u] = kNoSlot;
+      }
+      if ((uint32_t)rs_s < c_valid) {
+        const uint32_t c0 = cs - cbase, c1 = ce - cbase;
+        const uint32_t p0 = s_cp[buf][rs_s], p1 = s_cp[buf][rs_s + 1];
+        const uint32_t lo = max(p0, c0), hi = min(p1, c1);
+        const uint64_t* src = a.data + s_cb[buf][rs_s] - p0;
+        const unsigned long long bit = 1ull << rs_s;
+        uint32_t x = lo + rs_k;
+        if (x < hi) s_ent[x - c0] = make_ulonglong2(cur.c[0], bit);
+        if (x + 8 < hi) s_ent[x + 8 - c0] = make_ulonglong2(cur.c[1], bit);
+        for (x += 16; x < hi; x += 8) s_ent[x - c0] = make_ulonglong2(src[x], bit);
+      }
+      __syncthreads();
+      // in flight during the insert and probe: the positions of the chunk after
+      // the next (waves 0-1) and the next chunk's first elements
+      if (has_next && wave < 2) {
+        uint32_t x0, x1, x2, x3;
+        advance(nbs, nbe, nce, x0, x1, x2, x3);
+        if (x0 < we) pos_load(x0, x1, qb, qe);
+      }
+      if (has_next)
+        fetch_first(buf ^ 1, ncs - s_coff[nbs - wb], nce - s_coff[nbs - wb],
+                    !(self_tile && ncs == s_coff[nbs - wb] && nce == s_coff[nbe - wb]), nxt);
+      // 1) insert: one 32-bit compare-swap per element; a value already
+      //    present adds its column bit to the entry the slot names
+      const uint32_t ne = ce - cs;
+      uint32_t hs[kRMade], prev[kRMade], tags[kRMade], ent[kRMade], cid[kRMade];
+      uint64_t cv[kRMade];
+#pragma unroll
+      for (int u = 0; u < kRMade; ++u) {
+        hs[u] = kNoSlot;
+        ent[u] = 0;
+        cid[u] = kTile;
+        const uint32_t e = tid + kRB * u;
+        if (e < ne) {
+          const ulonglong2 en = s_ent[e];  // nothing ORs into e before its own slot exists
+          cv[u] = en.x;
+          cid[u] = (uint32_t)__builtin_ctzll(en.y);
+          hs[u] = fp_slot(cv[u]);
+          tags[u] = fp_tag(cv[u]);
+          prev[u] = atomicCAS(&s_slot[hs[u]], kFFree, (tags[u] << 10) | e);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kRMade; ++u) {
+        if (hs[u] == kNoSlot) continue;
+        const uint64_t v = cv[u];
+        const uint32_t e = tid + kRB * u;
+        uint32_t h = hs[u], x = prev[u];
+        for (;;) {
+          if (x == kFFree) {
+            made[u] = h;
+            ent[u] = e;
+            break;
+          }
+          if ((x >> 10) == tags[u] && s_ent[x & 1023u].x == v) {
+            atomicOr(&s_ent[x & 1023u].y, 1ull << cid[u]);
+            ent[u] = x & 1023u;
+            break;
+          }
+          h = (h + 1) & (kFSlots - 1);
+          x = atomicCAS(&s_slot[h], kFFree, (tags[u] << 10) | e);
+        }
+      }
+      __syncthreads();
+      // 2) probe.  A diagonal tile's chunk of whole buckets has its column
+      //    elements as its row elements: each one's hits are the final mask of
+      //    the entry it created or joined
+      if (self_tile && whole) {
+#pragma unroll
+        for (int u = 0; u < kRMade; ++u) {
+          const uint32_t r = cid[u];
+          if (hs[u] == kNoSlot || r >= r_valid) continue;
+          add_hits(r, s_ent[ent[u]].y);
+        }
+      } else if ((uint32_t)rs_s < r_valid) {
+        const uint32_t re = s_re[buf][rs_s];
+        const uint32_t j0 = s_rb[buf][rs_s] + rs_k;
+        const bool ok0 = j0 < re, ok1 = j0 + 8 < re;
+        const uint32_t h0 = fp_slot(cur.r[0]), h1 = fp_slot(cur.r[1]);
+        const uint32_t x0 = ok0 ? s_slot[h0] : kFFree, x1 = ok1 ? s_slot[h1] : kFFree;
+        const unsigned long long m0 = lookup(cur.r[0], h0, x0);
+        if (m0) add_hits(rs_s, m0);
+        const unsigned long long m1 = lookup(cur.r[1], h1, x1);
+        if (m1) add_hits(rs_s, m1);
+        for (uint32_t j = j0 + 16; j < re; j += 8) {
+          const uint64_t v = a.data[j];
+          const uint32_t h = fp_slot(v);
+          const unsigned long long m = lookup(v, h, s_slot[h]);
+          if (m) add_hits(rs_s, m);
+        }
+      }
+      __syncthreads();
+      buf ^= 1;
+      cur = nxt;
+      bs = nbs;
+      be = nbe;
+      cs = ncs;
+      ce = nce;
+    }
+  }
+  __syncthreads();
+  // planes the carry chains reached (unrelated tiles: none or one)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) top = max(top, (uint32_t)__shfl_xor(top, o, 64));
+  if (lane == 0 && top) atomicMax(&s_top, top);
+  __syncthreads();
+  const int np = (int)s_top;
+  for (uint32_t r = tid >> 6; r < kTile; r += kRB / 64) {  // a wave per row, a lane per column
+    const uint32_t c = lane;
+    uint32_t cnt = 0;
+    for (int b = 0; b < np; ++b) cnt |= (uint32_t)((s_pl[b * kTile + r] >> c) & 1ull) << b;
+    if (self_tile && c == r) cnt += s_self[r];
+    if (!cnt) continue;
+    const uint32_t gr = row0 + r, gc = col0 + c;
+    if (gr >= row_lim || gc >= a.n) continue;
+    if (a.packed) {
+      atomicAdd(&a.out[(t - a.tile_begin) * (kTile * kTile) + r * kTile + c], (int32_t)cnt);
+      continue;
+    }
+    const uint64_t orow = rows_mode ? gr - a.row_begin : gr;
+    atomicAdd(&a.out[orow * a.ld + gc], (int32_t)cnt);
+    if (!rows_mode && I != J) atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
+  }
+}
+
+}  // namespace
+
+hipError_t rjoin_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes, uint32_t n,
+                        uint32_t B, uint64_t* bounds, hipStream_t s) {
+  hipLaunchKernelGGL(k_rj_bounds, dim3((B + 1 + kPB / 64 - 1) / (kPB / 64)), dim3(kPB), 0, s, data, starts,
+                     sizes, n, B, bounds);
+  return hipGetLastError();
+}
+
+hipError_t rjoin_pos(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes, uint32_t n,
+                     uint32_t B, const uint64_t* bounds, uint32_t* pos, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const size_t lds = (size_t)(B + 1) * 8;
+  if (lds <= 32 * 1024 + 8) {
+    hipLaunchKernelGGL(k_rj_pos<true>, dim3(n), dim3(kPB), lds, s, data, starts, sizes, B, bounds, pos);
+  } else {
+    hipLaunchKernelGGL(k_rj_pos<false>, dim3(n), dim3(kPB), 0, s, data, starts, sizes, B, bounds, pos);
+  }
+  return hipGetLastError();
+}
+
+hipError_t rjoin_block_prefix(const uint32_t* pos, uint32_t n, uint32_t B, uint32_t* pre, hipStream_t s) {
+  const uint64_t cells = (uint64_t)((n + kTile - 1) / kTile) * (B + 1);
+  if (!cells) return hipSuccess;
+  hipLaunchKernelGGL(k_rj_prefix, dim3((unsigned)((cells + kPB - 1) / kPB)), dim3(kPB), 0, s, pos, n, B, pre);
+  return hipGetLastError();
+}
+
+hipError_t rjoin_launch(const uint64_t* data, const uint64_t* starts, const uint32_t* pos,
+                        const uint32_t* pre, uint32_t n, uint32_t B, bool sym, uint32_t row_begin,
+                        uint32_t row_end, uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles,
+                        bool packed, int32_t* out, hipStream_t s) {
+  const uint32_t n_cb = (n + kTile - 1) / kTile;
+  const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
+  if (!d_tiles) {
+    const uint64_t all = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
+    if (!sym) {
+      tile_begin = 0;
+      tile_end = all;
+    }
+    tile_end = std::min(tile_end, all);
+  }
+  if (tile_begin >= tile_end) return hipSuccess;
+  const uint64_t tiles = tile_end - tile_begin;
+  RJoinArgs ra{};
+  ra.data = data;
+  ra.starts = starts;
+  ra.pos = pos;
+  ra.cpre = pre;
+  ra.B = B;
+  ra.n = n;
+  ra.n_col_blocks = n_cb;
+  ra.sym = (sym || d_tiles) ? 1 : 0;
+  ra.row_begin = row_begin;
+  ra.row_end = row_end;
+  ra.tiles = d_tiles;
+  ra.out = out;
+  ra.ld = n;
+  ra.cap = join_cap();
+  ra.packed = packed ? 1 : 0;
+  // bucket groups per tile as for k_join: ~64 buckets per workgroup while the
+  // grid is small, >= ~1024 workgroups in all, >= 16 buckets each
+  // (SKS_RJOIN_WGS, diagnostics: the total)
+  static const uint64_t wgs_env = getenv("SKS_RJOIN_WGS") ? strtoull(getenv("SKS_RJOIN_WGS"), 0, 10) : 0;
+  uint64_t want = wgs_env ? (wgs_env + tiles - 1) / tiles
+                          : std::max<uint64_t>(std::min<uint64_t>((B + 63) / 64, (65536 + tiles - 1) / tiles),
+                                               (1024 + tiles - 1) / tiles);
+  if (!wgs_env) want = std::min<uint64_t>(want, std::max<uint32_t>(1, B / 16));
+  const uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, want));
+  ra.buckets_per_group = (B + groups - 1) / groups;
+  ra.n_groups = (B + ra.buckets_per_group - 1) / ra.buckets_per_group;
+  const uint64_t per = std::max<uint64_t>(1, kMaxGrid / ra.n_groups);
+  for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += per) {
+    const uint64_t nt = std::min(per, tile_end - t0);
+    ra.tile_begin = t0;
+    if (packed) ra.out = out + (t0 - tile_begin) * (uint64_t)(kTile * kTile);
+    hipLaunchKernelGGL(k_rjoin, dim3((unsigned)(nt * ra.n_groups)), dim3(kRB), 0, s, ra);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace sks

@@ -157,6 +157,35 @@ constexpr int kIntersectJoin = 2;    // k_join (LDS hash join), merge tiles if i
 constexpr int kIntersectGlobal = 3;  // one wavefront per pair from global memory
 constexpr int kIntersectPostings = 4;  // block postings join + MFMA counts (postings.hip)
 uint64_t intersect_sym_tiles(uint32_t n);
+constexpr int kIntersectRange = 5;     // k_rjoin: LDS hash join straight from the sorted sketches
+// Common value-range bucket bounds[0..B] (quantiles averaged over up to 64
+// sample sketches; any non-decreasing bounds give exact counts) and
+// pos[i][b] = first element of sketch i that is >= bounds[b] (pos[i][B] = size).
+hipError_t launch_value_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                               uint32_t n, uint32_t B, uint64_t* bounds, hipStream_t s);
+hipError_t launch_bucket_pos(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                             uint32_t n, uint32_t B, const uint64_t* bounds, uint32_t* pos,
+                             hipStream_t s);
+
+// ---- range join (rjoin.hip) ---------------------------------------------------------------
+// Its "layout" is only the bucket positions of the sorted sketches: pos (above)
+// and, per 64-sketch column block, pre[blk][b] = sum of pos[i][b] over the
+// block's sketches (where bucket b starts in the block's concatenated order).
+// Rows are read through pos alone, so a row range need not be block-aligned.
+hipError_t rjoin_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes, uint32_t n,
+                        uint32_t B, uint64_t* bounds, hipStream_t s);
+hipError_t rjoin_pos(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes, uint32_t n,
+                     uint32_t B, const uint64_t* bounds, uint32_t* pos, hipStream_t s);
+hipError_t rjoin_block_prefix(const uint32_t* pos, uint32_t n, uint32_t B, uint32_t* pre, hipStream_t s);
+// Tiles of the n x n matrix (sym: upper-triangle tiles [tile_begin, tile_end),
+// or with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
+// written) or rows [row_begin, row_end) x n (sym false, d_tiles null).
+// packed: out = [tile - tile_begin][64][64] instead of the matrix.  Counts are
+// added: `out` must be zeroed.  All element offsets (starts + pos) < 2^32.
+hipError_t rjoin_launch(const uint64_t* data, const uint64_t* starts, const uint32_t* pos,
+                        const uint32_t* pre, uint32_t n, uint32_t B, bool sym, uint32_t row_begin,
+                        uint32_t row_end, uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles,
+                        bool packed, int32_t* out, hipStream_t s);
 
 // Join layout (input of k_join, intersect.hip): blocks of 64 consecutive
 // sketches, elements hash-bucketed into B = 2^log_b buckets and stored block-major.

@@ -329,3 +329,222 @@ def sketch_genome_sharded(n_bytes, w, world, rank, build_chunk, union, device="c
     t = torch.tensor([nw], dtype=torch.int64, device=device)
     dist.all_reduce(t)
     return union(g[keep]), int(t.item())
+
+
+# ---- all-vs-all over the range join: packed tiles, overlap, one receiving rank ------------
+# The range join (sks_intersect_range, rjoin.hip) reads the sorted sketches
+# where they lie, so the exchange is the sketches themselves (8 B per element,
+# padded to the largest rank's total) and nothing is built before it.  Each
+# rank counts a fixed plan of upper-triangle 64x64 tiles (tile_plan): the tiles
+# of its own blocks first — from its own sketches, while the gather is in
+# flight — then its half of every cross-rank block pair.  Counts stay packed
+# ([tile][64][64] int32, 16 KB per tile) and go to ONE rank (dst), where the
+# n x n matrix is assembled: no rank holds a matrix it does not need and no
+# collective carries n^2 words (the dense all-reduce of all_vs_all_join moved
+# 2 (N-1)/N n^2 words through every rank).
+
+def _ctx_waits_for_torch(ctx):
+    """Order the context's HIP stream after work queued so far on torch's current
+    stream (no-op when they are the same stream)."""
+    s = _ctx_torch_stream(ctx)
+    if s is not None:
+        s.wait_stream(torch.cuda.current_stream())
+
+
+def _torch_waits_for_ctx(ctx):
+    s = _ctx_torch_stream(ctx)
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
+def _ctx_torch_stream(ctx):
+    h = getattr(ctx, "stream", 0) or 0
+    cur = torch.cuda.current_stream()
+    if h == cur.cuda_stream:
+        return None
+    return torch.cuda.default_stream() if h == 0 else torch.cuda.ExternalStream(h)
+
+
+def tile_plan(n_genomes, world, rank):
+    """(local, remote) int64 arrays [T, 2] of the upper-triangle tiles (I, J) that
+    `rank` counts.  local: both blocks in the rank's own block range
+    (block_shard), countable from its own sketches; remote: for every other rank
+    q, half of the tiles pairing the two ranks' blocks (row-major over the pair,
+    the lower rank takes the first half).  Every tile of the n x n upper
+    triangle is in exactly one rank's plan; per-rank counts differ by at most
+    one tile per rank pair (plus a short last rank)."""
+    import numpy as np
+    nb = (n_genomes + TILE - 1) // TILE
+    bpr = block_shard(n_genomes, world, rank)[0]
+
+    def blocks(q):
+        return np.arange(min(nb, q * bpr), min(nb, (q + 1) * bpr), dtype=np.int64)
+
+    mine = blocks(rank)
+    I, J = np.meshgrid(mine, mine, indexing="ij")
+    keep = I <= J
+    local = np.stack([I[keep], J[keep]], axis=1) if mine.size else np.zeros((0, 2), np.int64)
+    remote = [np.zeros((0, 2), np.int64)]
+    for q in range(world):
+        if q == rank:
+            continue
+        a, b = min(rank, q), max(rank, q)
+        ba, bb = blocks(a), blocks(b)
+        if not ba.size or not bb.size:
+            continue
+        I, J = np.meshgrid(ba, bb, indexing="ij")
+        pairs = np.stack([I.reshape(-1), J.reshape(-1)], axis=1)
+        h = (len(pairs) + 1) // 2
+        remote.append(pairs[:h] if rank == a else pairs[h:])
+    return local.reshape(-1, 2), np.concatenate(remote).reshape(-1, 2)
+
+
+def _max_over_many(xs, world, device):
+    if _solo(world):
+        return [int(x) for x in xs]
+    t = torch.tensor([int(x) for x in xs], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [int(v) for v in t.tolist()]
+
+
+def _gather_start(ts, world):
+    """Starts the all-gathers of flat tensors (rank-major); returns a function
+    that waits for them and returns the gathered tensors.  With RCCL the
+    gathers run on the collective stream while the caller queues other work."""
+    if dist.get_backend() == "nccl":
+        outs, works = [], []
+        for t in ts:
+            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+            works.append(dist.all_gather_into_tensor(out, t.contiguous(), async_op=True))
+            outs.append(out)
+
+        def finish():
+            for w in works:
+                w.wait()
+            return outs
+        return finish
+    res = _gather_many(ts, world)  # gloo: through host memory, synchronously
+    return lambda: res
+
+
+def _gather_tiles(parts, world, dst):
+    """parts: int32 [Tmax, 64, 64] (padded) of this rank -> [world, Tmax, 64, 64]
+    on dst (None elsewhere), or on every rank when dst is None."""
+    if dst is None:
+        return _gather_flat(parts.reshape(-1), world).view((world,) + tuple(parts.shape))
+    nccl = dist.get_backend() == "nccl"
+    src = parts if nccl else parts.cpu()
+    lst = [torch.empty_like(src) for _ in range(world)] if dist.get_rank() == dst else None
+    dist.gather(src, gather_list=lst, dst=dst)
+    if lst is None:
+        return None
+    return torch.stack(lst).to(parts.device)
+
+
+def place_tiles(mat, tiles, parts, n, chunk=8192):
+    """Writes packed tile counts into the n x n matrix: tile (I, J) at rows
+    64 I.., columns 64 J.., and mirrored when I != J (a diagonal tile holds both
+    triangles)."""
+    dev = mat.device
+    flat = mat.view(-1)
+    ar = torch.arange(TILE, device=dev, dtype=torch.int64)
+    tiles = torch.as_tensor(tiles, dtype=torch.int64, device=dev).reshape(-1, 2)
+    for a in range(0, tiles.shape[0], chunk):
+        t = tiles[a:a + chunk]
+        p = parts[a:a + chunk].to(dev)
+        gr = (t[:, 0:1] * TILE + ar.view(1, -1)).view(-1, TILE, 1).expand(-1, TILE, TILE)
+        gc = (t[:, 1:2] * TILE + ar.view(1, -1)).view(-1, 1, TILE).expand(-1, TILE, TILE)
+        ok = (gr < n) & (gc < n)
+        flat[(gr * n + gc)[ok]] = p[ok]
+        off = (t[:, 0] != t[:, 1]).view(-1, 1, 1) & ok
+        flat[(gc * n + gr)[off]] = p[off]
+    return mat
+
+
+def all_vs_all_ranged(n_genomes, world, rank, data, starts, sizes, max_size, count, device="cpu",
+                      dst=0, out=None):
+    """n x n int32 intersection matrix on rank `dst` (None on the others; on every
+    rank when dst is None).
+
+    data / starts / sizes: this rank's sketches (block_shard's genome range):
+    int64 values (each sketch sorted, unique), int64 starts, int32 sizes.
+    max_size: its largest sketch.  count(data, starts, sizes, n, log_b, tiles,
+    out) adds the counts of `tiles` (int64 [T, 2] block indices into that
+    sketch numbering) to the packed int32 out [T, 64, 64]; it is called first
+    with the local sketches, then with the gathered ones, and must use one set
+    of bucket bounds across its calls (sks_intersect_range's contract)."""
+    bpr, g0, g1 = block_shard(n_genomes, world, rank)
+    nl = g1 - g0
+    solo = _solo(world)
+    local, remote = tile_plan(n_genomes, world, rank)
+    T = len(local) + len(remote)
+    tot = int(sizes.to(torch.int64).sum()) if nl else 0
+    gmax, cap_e = _max_over_many([max_size, tot], world, device)
+    import sksffi
+    log_b = sksffi.range_log_b(max(gmax, 1))
+    parts = torch.zeros((max(T, 1), TILE, TILE), dtype=torch.int32, device=device)
+    if solo:
+        if T:
+            count(data, starts, sizes, nl, log_b, local, parts[:len(local)])
+        tiles, got = local, parts[:T]
+    else:
+        per = bpr * TILE
+        cap_e = max(cap_e, 1)
+        send_d = torch.zeros(cap_e, dtype=torch.int64, device=device)
+        send_s = torch.zeros(per, dtype=torch.int64, device=device)
+        send_z = torch.zeros(per, dtype=torch.int32, device=device)
+        if nl:
+            send_d[:tot] = data[:tot]
+            send_s[:nl] = starts[:nl]
+            send_z[:nl] = sizes[:nl]
+        finish = _gather_start([send_d, send_s, send_z], world)
+        if len(local):  # the rank's own tiles while the sketches travel
+            count(data, starts, sizes, nl, log_b, local - g0 // TILE, parts[:len(local)])
+        g_d, g_s, g_z = finish()
+        g_s = (g_s.view(world, per) + torch.arange(world, device=g_s.device, dtype=torch.int64).view(world, 1)
+               * cap_e).reshape(-1)
+        if len(remote):
+            count(g_d, g_s, g_z, world * per, log_b, remote, parts[len(local):T])
+        tmax = max(sum(len(x) for x in tile_plan(n_genomes, world, q)) for q in range(world))
+        pad = torch.zeros((max(tmax, 1), TILE, TILE), dtype=torch.int32, device=device)
+        pad[:T] = parts[:T]
+        gathered = _gather_tiles(pad, world, dst)
+        if gathered is None:
+            return None
+        import numpy as np
+        plans = [tile_plan(n_genomes, world, q) for q in range(world)]
+        tiles = np.concatenate([np.concatenate(p) for p in plans]).reshape(-1, 2)
+        got = torch.cat([gathered[q, :sum(len(x) for x in plans[q])] for q in range(world)])
+    if out is None:
+        out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+    else:
+        out.zero_()
+    return place_tiles(out, tiles, got, n_genomes)
+
+
+def range_count_fn(ctx):
+    """count() of all_vs_all_ranged on the GPU (sks_range_bounds once, from the
+    first call's sketches, then sks_intersect_range per call).  Tensors may be
+    on the CPU (gloo): they are staged to the GPU and the counts copied back.
+    The context's stream is ordered after torch's current stream before its
+    kernels and torch's after them (any ctx stream works)."""
+    state = {}
+
+    def count(data, starts, sizes, n, log_b, tiles, out):
+        d, st, sz = (t.to("cuda").contiguous() for t in (data, starts, sizes))
+        tl = torch.as_tensor(tiles, dtype=torch.int32).reshape(-1, 2).to("cuda").contiguous()
+        tgt = out if out.is_cuda else torch.zeros(out.shape, dtype=out.dtype, device="cuda")
+        _ctx_waits_for_torch(ctx)
+        if "bounds" not in state:
+            b = torch.empty((1 << log_b) + 1, dtype=torch.int64, device="cuda")
+            ctx.range_bounds(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, log_b, b.data_ptr())
+            state["bounds"], state["log_b"] = b, log_b
+        assert state["log_b"] == log_b
+        ctx.intersect_range(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, log_b,
+                            state["bounds"].data_ptr(), tl.data_ptr(), 0, tl.shape[0], True,
+                            tgt.data_ptr())
+        _torch_waits_for_ctx(ctx)
+        state["keep"] = (d, st, sz, tl)  # alive until the next call queues behind them
+        if tgt is not out:
+            out.copy_(tgt.cpu())
+    return count

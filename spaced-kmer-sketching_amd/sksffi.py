@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("SKS_LIB") or os.path.join(PKG_DIR, "lib", "libsks.so"
 SKS_FRAC_MOD = 0
 SKS_BOTTOM_S = 1
 INTERSECT_AUTO, INTERSECT_MERGE, INTERSECT_JOIN, INTERSECT_GLOBAL, INTERSECT_POSTINGS = 0, 1, 2, 3, 4
+INTERSECT_RANGE = 5
 FLAVOUR_BOOST_MIX = 0
 FLAVOUR_BOOST_LEGACY = 1
 
@@ -59,6 +60,7 @@ EXPORTED = [
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
     "sks_sketch_set_name", "sks_sketch_set_save", "sks_sketch_set_load", "sks_sketch_set_concat",
+    "sks_range_log_b", "sks_range_bounds", "sks_intersect_range",
 ]
 
 _lib = None
@@ -121,6 +123,11 @@ def lib():
                                         C.POINTER(C.c_uint32)]
     L.sks_intersect_sym_layout.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint64,
                                            C.c_uint64, vp]
+    L.sks_range_log_b.argtypes = [C.c_uint32]
+    L.sks_range_log_b.restype = C.c_uint32
+    L.sks_range_bounds.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp]
+    L.sks_intersect_range.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, C.c_uint64,
+                                      C.c_uint64, C.c_int, vp]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_device.argtypes = [vp]
@@ -204,6 +211,10 @@ def join_layout_log_b(max_sketch_size):
 
 def join_layout_capacity():
     return int(lib().sks_join_layout_capacity())
+
+
+def range_log_b(max_sketch_size):
+    return int(lib().sks_range_log_b(max_sketch_size))
 
 
 def intersect_sym_tiles(n):
@@ -322,8 +333,22 @@ class Context:
                                              C.c_void_p(boff), C.c_void_p(bstart), tile_begin,
                                              tile_end, C.c_void_p(out)))
 
+    def range_bounds(self, data, starts, sizes, n, log_b, bounds):
+        """sks_range_bounds (device pointers): value-range bucket bounds of the set."""
+        check(lib().sks_range_bounds(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes), n,
+                                     log_b, C.c_void_p(bounds)))
+
+    def intersect_range(self, data, starts, sizes, n, log_b, bounds, tiles, tile_begin, tile_end,
+                        packed, out):
+        """sks_intersect_range: tile counts ADDED to `out` (n x n both halves, or packed
+        [tile][64][64]); tiles: device pointer of (I, J) u32 pairs, or 0 for the
+        upper-triangle range."""
+        check(lib().sks_intersect_range(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes),
+                                        n, log_b, C.c_void_p(bounds), C.c_void_p(tiles) if tiles else None,
+                                        tile_begin, tile_end, 1 if packed else 0, C.c_void_p(out)))
+
     def set_intersect_kernel(self, kind):
-        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL / _POSTINGS (sks.h); all give identical counts."""
+        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL / _POSTINGS / _RANGE (sks.h); all give identical counts."""
         check(lib().sks_ctx_set_intersect_kernel(self.h, kind))
         self._intersect_kernel = kind
 
@@ -427,6 +452,15 @@ class Context:
                                     pos_offset))
 
 
+class _DeviceArray:
+    """A device buffer described by __cuda_array_interface__ (torch.as_tensor
+    wraps it without a copy)."""
+
+    def __init__(self, ptr, n, typestr):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr,
+                                         "data": (int(ptr), False), "version": 3, "strides": None}
+
+
 class SketchSet:
     def __init__(self, h):
         self.h = h
@@ -511,6 +545,23 @@ class SketchSet:
         L = lib()
         return (L.sks_sketch_set_device_data(self.h), L.sks_sketch_set_device_starts(self.h),
                 L.sks_sketch_set_device_sizes(self.h))
+
+    def device_tensors(self, device=0):
+        """Zero-copy torch views of the set's device arrays (u64 sketches only):
+        (data int64 [total], starts int64 [n], sizes int32 [n]).  The views do
+        not keep the set alive: use them while the set is."""
+        import torch
+        assert self.elem_words == 1, "device_tensors: u64 sketches only"
+        d, st, sz = self.device_ptrs()
+        total = int(self.sizes().astype(np.int64).sum())
+        dev = torch.device("cuda", device)
+
+        def view(ptr, n, typestr, dtype):
+            if n == 0 or not ptr:
+                return torch.zeros(0, dtype=dtype, device=dev)
+            return torch.as_tensor(_DeviceArray(ptr, n, typestr), device=dev)
+        return view(d, total, "<i8", torch.int64), view(st, self.n, "<i8", torch.int64), \
+            view(sz, self.n, "<i4", torch.int32)
 
     def export(self, d_dst_ptr, stride, d_sizes_ptr):
         check(lib().sks_sketch_set_export(self.h, C.c_void_p(d_dst_ptr), stride,

@@ -402,3 +402,112 @@ def test_one_genome_sharded_gloo(world, w, k):
     for _, sk, n in res:
         got = sk.view(np.uint64).reshape(-1, 2) if w > 32 else sk.view(np.uint64)
         assert np.array_equal(got, want if w > 32 else want[:, 0]) and n == nw
+
+
+# ---- all_vs_all_ranged: local tiles before the gather, packed tiles to one rank ----------
+N_RANGED = 200  # four tile blocks, ragged; at world 3 the last rank holds no genome
+
+
+def _ranged_sketches():
+    m = O.mask(21, 21, 0)
+    out = []
+    for g in range(N_RANGED):
+        seq = synth.bases(4000, seed=70 + g % 5, mut_seed=900 + g, mut_rate=0.003 * (g % 7))
+        sk, _ = O.sketch(O.cut_runs(seq.tobytes()), 21, m, "bottom", 150 + (g % 3) * 40)
+        out.append(np.sort(sk[:, 0].astype(np.int64)))
+    if N_RANGED > 77:
+        out[77] = out[77][:0]  # an empty sketch
+    return out
+
+
+def _np_count_tiles(data, starts, sizes, n, log_b, tiles, out):
+    """The tile contract of sks_intersect_range (packed, counts added) by merge."""
+    data, starts, sizes = data.numpy(), starts.numpy(), sizes.numpy()
+    sk = [data[starts[i]:starts[i] + sizes[i]] for i in range(n)]
+    for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
+        for r in range(64):
+            i = I * 64 + r
+            if i >= n:
+                break
+            for c in range(64):
+                j = J * 64 + c
+                if j >= n:
+                    break
+                out[t, r, c] += len(np.intersect1d(sk[i], sk[j], assume_unique=True))
+
+
+def _ranged_worker(rank, world, port, q, dst):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sk = _ranged_sketches()
+    _, g0, g1 = sks_dist.block_shard(N_RANGED, world, rank)
+    mine = sk[g0:g1]
+    sizes = torch.tensor([len(s) for s in mine], dtype=torch.int32)
+    starts = torch.zeros(len(mine), dtype=torch.int64)
+    if len(mine):
+        starts[1:] = torch.cumsum(sizes.to(torch.int64), 0)[:-1]
+    data = torch.from_numpy(np.concatenate(mine)) if mine else torch.zeros(0, dtype=torch.int64)
+    calls = []
+
+    def count(d, st, sz, n, log_b, tiles, out):
+        calls.append((n, len(tiles)))
+        _np_count_tiles(d, st, sz, n, log_b, tiles, out)
+    mx = max((len(s) for s in mine), default=0)
+    mat = sks_dist.all_vs_all_ranged(N_RANGED, world, rank, data, starts, sizes, mx, count, dst=dst)
+    q.put((rank, None if mat is None else mat.numpy(), calls))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dst", [(2, 0), (3, 1), (3, None)])
+def test_all_vs_all_ranged_gloo(world, dst):
+    """Each rank counts its own blocks' tiles from its own sketches (first call,
+    n = its genome count), then its share of the cross-rank tiles over the
+    gathered sketches; the packed tiles go to `dst` (every rank for None), whose
+    matrix equals the single-process merge counts; the others return None."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ranged_worker, args=(r, world, port, q, dst)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {r: (m, c) for r, m, c in (q.get(timeout=240) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sk = _ranged_sketches()
+    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(N_RANGED)]
+                     for i in range(N_RANGED)])
+    for r in range(world):
+        mat, calls = results[r]
+        if dst is None or r == dst:
+            assert np.array_equal(mat, want), r
+        else:
+            assert mat is None
+        loc, rem = sks_dist.tile_plan(N_RANGED, world, r)
+        _, g0, g1 = sks_dist.block_shard(N_RANGED, world, r)
+        expect = ([(g1 - g0, len(loc))] if len(loc) else []) + ([(world * sks_dist.block_shard(
+            N_RANGED, world, r)[0] * 64, len(rem))] if len(rem) else [])
+        assert calls == expect, (r, calls)
+
+
+@pytest.mark.parametrize("n,world", [(1000, 8), (1000, 3), (200, 3), (64, 2), (1, 4), (5000, 7)])
+def test_tile_plan_partitions_upper_triangle(n, world):
+    nb = (n + 63) // 64
+    seen = {}
+    sizes = []
+    for r in range(world):
+        loc, rem = sks_dist.tile_plan(n, world, r)
+        sizes.append(len(loc) + len(rem))
+        bpr, g0, g1 = sks_dist.block_shard(n, world, r)
+        for I, J in loc:
+            assert g0 // 64 <= I <= J < (g1 + 63) // 64
+        for I, J in np.concatenate([loc, rem]):
+            assert 0 <= I <= J < nb
+            assert (I, J) not in seen
+            seen[(I, J)] = r
+    assert len(seen) == nb * (nb + 1) // 2
+    full = [s for r, s in enumerate(sizes) if sks_dist.block_shard(n, world, r)[2] -
+            sks_dist.block_shard(n, world, r)[1] == sks_dist.block_shard(n, world, r)[0] * 64]
+    if full:  # ranks holding whole block ranges get near-equal shares
+        assert max(full) - min(full) <= world

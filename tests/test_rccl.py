@@ -205,3 +205,34 @@ def test_seed_sweep_on_rccl(env):
     assert mine == list(range(seeds)) and cons.is_cuda
     want = sum(per_seed) / seeds
     assert np.allclose(cons.cpu().numpy(), want, rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("side_stream", [False, True])
+def test_ranged_all_vs_all_on_rccl(env, side_stream):
+    """sks_dist.all_vs_all_ranged through the collective branch on RCCL: the
+    scalar all_reduce MAX, the three async sketch gathers (int64 values, int64
+    starts, int32 sizes) with the local tiles counted while they run, the packed
+    tile gather to rank 0 (dist.gather) and the matrix assembly — 130 genomes,
+    a ragged last block, one empty sketch.  With side_stream the context's
+    kernels run on a non-default HIP stream: range_count_fn orders it against
+    torch's stream both ways."""
+    torch, dist, ctx = env
+    import sks_dist
+    n, s = 130, 500
+    genomes = _family(n, 25_000, 7)
+    genomes[40] = b""
+    d, seg = _upload(torch, genomes)
+    mask = sksffi.mask_generate(W, K, 2)
+    ss = ctx.sketch_build(d.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, s)
+    sk = [ss.sketch(i)[:, 0].copy() for i in range(n)]
+    want = _merge_counts(sk)
+    assert want[0, 7] > 0 and want[40].sum() == 0
+    stream = torch.cuda.Stream() if side_stream else None
+    cctx = sksffi.Context(0, stream.cuda_stream) if side_stream else ctx
+    data, starts, sizes = ss.device_tensors()
+    mat = sks_dist.all_vs_all_ranged(n, 1, 0, data, starts, sizes, int(ss.sizes().max()),
+                                     sks_dist.range_count_fn(cctx), device="cuda", dst=0)
+    torch.cuda.synchronize()
+    assert np.array_equal(mat.cpu().numpy().astype(np.int64), want)
+    if side_stream:
+        cctx.close()

@@ -39,7 +39,7 @@ def main():
     T = sksffi.intersect_sym_tiles(n)
     ref = None
     kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN),
-               ("postings", sksffi.INTERSECT_POSTINGS))
+               ("postings", sksffi.INTERSECT_POSTINGS), ("range", sksffi.INTERSECT_RANGE))
     only = os.environ.get("SKS_BENCH_KERNELS")
     if only:
         kernels = tuple(x for x in kernels if x[0] in only.split(","))
