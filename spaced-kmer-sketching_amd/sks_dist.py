@@ -203,7 +203,7 @@ def _gather_many(ts, world):
 
 
 def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity, build, count,
-                    device="cpu", out=None, max_log_b=14):
+                    device="cpu", out=None, max_log_b=14, local_total=None):
     """Full n x n int32 intersection matrix on every rank.
 
     build(log_b, pad) -> (data u64[], ids u8[], boff u32[], bstart u64[], max_block_bucket)
@@ -221,15 +221,24 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity,
     exceeds the join table's `capacity`, up to 2^max_log_b buckets.  That is a
     speed choice, not a correctness one: k_join cuts a bucket above capacity into
     table-sized sub-chunks and probes the bucket's row elements once per
-    sub-chunk, so the counts at max_log_b are exact for any sketch size."""
+    sub-chunk, so the counts at max_log_b are exact for any sketch size.
+
+    local_total: this rank's element count.  The layouts are built straight
+    into padded send buffers of max-over-ranks(local_total) elements (one
+    all-reduce carries it with the largest sketch size); without it the pad is
+    the bound bpr * 64 * (largest sketch), which over-allocates and over-sends
+    when sketch sizes are skewed (FracMinHash of genomes of different lengths)."""
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
-    max_all = _max_over(local_max_size, world, device)
+    if local_total is None:
+        max_all = _max_over(local_max_size, world, device)
+        cap_bound = bpr * TILE * max_all
+    else:
+        max_all, cap_bound = _max_over_many([local_max_size, local_total], world, device)
     log_b = log_b_for(max_all)
     solo = _solo(world)
-    # every rank's layout holds at most bpr * 64 * (largest sketch) elements, so
-    # the layouts are built straight into padded send buffers of that size: no
-    # all-reduce of the layout sizes and no copies before the gather
-    pad = None if solo else (max(1, bpr * TILE * max_all), bpr)
+    # the layouts are built straight into padded send buffers: no all-reduce
+    # of the layout sizes and no copies before the gather
+    pad = None if solo else (max(1, cap_bound), bpr)
     while True:
         data, ids, boff, bstart, mb = build(log_b, pad)
         if mb is None or log_b >= max_log_b:

@@ -276,7 +276,7 @@ def _np_count_layout(n, log_b, data, ids, boff, bstart, t0, t1, out):
                     out[j, i] = c
 
 
-def _join_worker(rank, world, port, q, capacity, max_log_b):
+def _join_worker(rank, world, port, q, capacity, max_log_b, exact=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -290,6 +290,11 @@ def _join_worker(rank, world, port, q, capacity, max_log_b):
         d, i, b, s, mx = _np_layout(mine, lb)
         cap_e, bpr = pad  # the padded send-buffer shape all_vs_all_join gathers
         assert d.numel() <= cap_e and b.numel() <= bpr * ((1 << lb) + 1)
+        if exact:  # the largest rank's element total, not bpr * 64 * largest sketch
+            totals = [sum(len(x) for x in sk[sks_dist.block_shard(N_GENOMES, world, q)[1]:
+                                             sks_dist.block_shard(N_GENOMES, world, q)[2]])
+                      for q in range(world)]
+            assert cap_e == max(totals), (cap_e, totals)
         pd = torch.full((cap_e,), -7, dtype=torch.int64)
         pi = torch.full((cap_e,), 99, dtype=torch.uint8)
         pb = torch.full((bpr * ((1 << lb) + 1),), -3, dtype=torch.int32)
@@ -299,7 +304,8 @@ def _join_worker(rank, world, port, q, capacity, max_log_b):
     mat = sks_dist.all_vs_all_join(
         N_GENOMES, world, rank, max((len(s) for s in mine), default=0),
         lambda m: 1 if capacity < 100 else 3, capacity=capacity, build=build,
-        count=_np_count_layout, max_log_b=max_log_b)
+        count=_np_count_layout, max_log_b=max_log_b,
+        local_total=sum(len(s) for s in mine) if exact else None)
     q.put((rank, mat.numpy(), built))
     dist.destroy_process_group()
 
@@ -307,14 +313,18 @@ def _join_worker(rank, world, port, q, capacity, max_log_b):
 # (capacity, max_log_b): a table that holds everything (no bucket search), and
 # a tiny one that walks log_b 1 -> max_log_b and then counts with block-buckets
 # still above capacity (the kernel's sub-chunk case; counts must stay exact)
-@pytest.mark.parametrize("world,capacity,max_log_b", [(2, 10**9, 14), (3, 10**9, 14), (2, 20, 4)])
-def test_all_vs_all_join_layout_gather_gloo(world, capacity, max_log_b):
+@pytest.mark.parametrize("world,capacity,max_log_b,exact", [(2, 10**9, 14, False), (3, 10**9, 14, False),
+                                                           (2, 20, 4, False), (2, 10**9, 14, True),
+                                                           (3, 10**9, 14, True)])
+def test_all_vs_all_join_layout_gather_gloo(world, capacity, max_log_b, exact):
     """Ranks build layouts of their own block-aligned genomes, all-gather them and
-    count their tile share: every rank ends with the single-process matrix."""
+    count their tile share: every rank ends with the single-process matrix.
+    exact: the send buffers are padded to the largest rank's element total
+    (sketch sizes here vary 100-300 per genome and the last rank is short)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, capacity, max_log_b))
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, capacity, max_log_b, exact))
              for r in range(world)]
     for p in procs:
         p.start()
