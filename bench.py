@@ -711,6 +711,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
 
     t_sketch = t_pairs = 0.0
     timed = 0
+    res = None
     for it in range(warmup + steps):
         barrier(world)
         torch.cuda.synchronize()
@@ -723,18 +724,13 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         local_max = int(local_sizes.max()) if n_local else 0
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        # layouts of this rank's blocks, built into the padded send buffers and
-        # all-gathered; symmetric join tiles of this rank; all-reduce of the
-        # counts.  stat=False: no block-bucket read-back (bucket count from the
-        # largest sketch; counts are exact at any)
-        build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs,
-                                                stat=False)
-        out = mat if dev == "cuda" else torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32)
-        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max, sksffi.join_layout_log_b,
-                                       sksffi.join_layout_capacity(), build, count, device=dev,
-                                       out=out if dev == "cuda" else None)
-        if dev != "cuda":
-            mat.copy_(res)
+        # layouts of this rank's blocks, built into send buffers padded to the
+        # largest rank's total; the rank's own tiles counted while the layouts
+        # are all-gathered, then its cross-rank tiles; packed tiles to rank 0
+        build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs)
+        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max,
+                                       int(local_sizes.astype(np.int64).sum()), sksffi.join_layout_log_b,
+                                       build, count, device=dev, out=mat if dev == "cuda" else None, dst=0)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ts, tp = max_over_ranks(t1 - t0, world), max_over_ranks(t2 - t1, world)
@@ -743,17 +739,21 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
             t_pairs += tp
             timed += 1
         del ss
+    if res is not None and dev != "cuda":
+        mat.copy_(res)
     # containment + ANI for every ordered pair (host, double, from exact counts;
     # kmer-sketching.cpp:195-200 with the first set of the pair as denominator)
-    counts = mat.cpu().numpy()
-    sizes = np.diag(counts).astype(np.int32)  # |S_i ∩ S_i| = |S_i|
-    size_first = np.repeat(sizes, C4_GENOMES)
-    kmer_ones = bin(mask).count("1") // 2
-    _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, kmer_ones)
+    # (the matrix exists on rank 0 only: the packed tiles were gathered there)
     k_ms = ctx.last_intersect_ms()
     t_sketch /= max(timed, 1)
     t_pairs /= max(timed, 1)
+    counts, ani = None, np.zeros(1)
     if rank == 0:
+        counts = mat.cpu().numpy()
+        sizes = np.diag(counts).astype(np.int32)  # |S_i ∩ S_i| = |S_i|
+        size_first = np.repeat(sizes, C4_GENOMES)
+        kmer_ones = bin(mask).count("1") // 2
+        _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, kmer_ones)
         assert (counts == counts.T).all() and counts[0, 1] > 0
         assert (sizes[g0:g1] == local_sizes[:n_local]).all()
     cpu = cpu_sk = None
@@ -764,7 +764,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s", "scaling": "strong",
         "ms_pair_phase": t_pairs * 1e3, "ms_sketch_phase": t_sketch * 1e3,
-        "pair_kernel_ms_rank0": k_ms,
+        "pair_kernel_ms_rank0": k_ms,  # the rank's last join launch (all tiles at N = 1)
         # streamed-equivalent bytes of the pair kernel, 8 B per
         # element of both sets + 4 B per count, for every ordered pair this rank's
         # tiles cover (symmetric tiles give both halves); the join reads each
@@ -780,10 +780,12 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         "ani_mean_all_pairs": float(np.mean(ani)),
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
                    "genome_len": C4_LEN, "s": C4_S, "w": W, "k": K,
-                   "pair_sharding": "block-aligned genomes per rank; upper-triangle 64x64 "
-                                    "join tiles split over ranks",
-                   "collective": ("all_gather_into_tensor join layouts + all_reduce counts "
-                                  f"({backend_label()})" if collective() else "none")},
+                   "pair_sharding": "block-aligned genomes per rank; tile plan: the rank's own "
+                                    "blocks' 64x64 join tiles (counted while the layouts are "
+                                    "gathered) + half of every cross-rank block pair",
+                   "collective": ("all_reduce MAX (largest sketch, element total) + "
+                                  "all_gather_into_tensor join layouts + gather of packed tiles "
+                                  f"to rank 0 ({backend_label()})" if collective() else "none")},
         "cpu_baseline": cpu,
         "cpu_baseline_sketch_phase": cpu_sk,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),

@@ -277,6 +277,22 @@ int sks_intersect_sym_layout(sks_ctx* ctx, uint32_t n, uint32_t log_b, const uin
                              const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
                              uint64_t tile_begin, uint64_t tile_end, int32_t* d_out);
 
+/* Tiles of the n x n matrix over a join layout whose block 0 is global block
+ * blk0 (a rank's own blocks, or a gathered layout with blk0 = 0); every tile's
+ * two blocks must lie in the layout.  Tiles: d_tiles == NULL -> upper-triangle
+ * tiles [tile_begin, tile_end) (row-major, sks_intersect_sym_tiles); else the
+ * list d_tiles[2t] = I, d_tiles[2t + 1] = J (I <= J, global block indices) for
+ * t in [tile_begin, tile_end).  packed == 0: counts are ADDED to the n x n int32
+ * matrix d_out at (i, j) and (j, i); packed != 0: to
+ * d_out[(t - tile_begin) * 4096 + r * 64 + c] for row I*64 + r, column J*64 + c
+ * (a diagonal tile holds both triangles).  The caller zeroes d_out.  A
+ * multi-GPU caller counts the tiles of its own blocks on its own layout while
+ * the others' layouts are still being gathered. */
+int sks_intersect_layout_tiles(sks_ctx* ctx, uint32_t n, uint32_t log_b, const uint64_t* d_data,
+                               const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+                               uint32_t blk0, const uint32_t* d_tiles, uint64_t tile_begin,
+                               uint64_t tile_end, int packed, int32_t* d_out);
+
 /* ---- range join: all-pairs straight from the sorted sketches, across GPUs -----------------
  * Replaces the pair loop of compute_pairwise_kmer_set_intersections
  * (kmer_set.cpp:143-184) over u64 sketches, each count equal to

@@ -1530,7 +1530,8 @@ int sks_intersect_sym_layout(sks_ctx* c, uint32_t n, uint32_t log_b, const uint6
   SKS_HIP(hipMemsetAsync(d_out, 0, (uint64_t)n * n * sizeof(int32_t), c->stream));
   if (n) {
     const sks::JoinLayout L{d_data, d_ids, d_boff, d_bstart};
-    SKS_HIP(sks::join_launch(L, 0, L, n, log_b, true, 0, n, tile_begin, tile_end, d_out, c->stream));
+    SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, true, 0, n, tile_begin, tile_end, nullptr, false, d_out,
+                             c->stream));
   }
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;
@@ -1571,6 +1572,28 @@ int sks_intersect_range(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_st
     SKS_HIP(sks::rjoin_block_prefix(pos, n, B, pre, c->stream));
     SKS_HIP(sks::rjoin_launch(d_data, d_starts, pos, pre, n, B, true, 0, n, tile_begin, tile_end, d_tiles,
                               packed != 0, d_out, c->stream));
+  }
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_intersect_layout_tiles(sks_ctx* c, uint32_t n, uint32_t log_b, const uint64_t* d_data,
+                               const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+                               uint32_t blk0, const uint32_t* d_tiles, uint64_t tile_begin,
+                               uint64_t tile_end, int packed, int32_t* d_out) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: null ctx");
+  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: log_b > 14");
+  if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: bad tile range");
+  if (!d_tiles && tile_end > sks::intersect_sym_tiles(n))
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: tile range beyond the upper triangle");
+  if (tile_end > tile_begin && (!d_boff || !d_bstart || !d_out))
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  if (n && tile_end > tile_begin) {
+    const sks::JoinLayout L{d_data, d_ids, d_boff, d_bstart};
+    SKS_HIP(sks::join_launch(L, 0u - blk0, L, 0u - blk0, n, log_b, true, 0, n, tile_begin, tile_end, d_tiles,
+                             packed != 0, d_out, c->stream));
   }
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;

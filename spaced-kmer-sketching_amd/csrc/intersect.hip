@@ -614,14 +614,16 @@ __global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ st
 
 struct JoinArgs {
   JoinLayout r, c;  // row blocks (tile row I = block r_blk0 + I) and column blocks
-  uint32_t r_blk0;
+  uint32_t r_blk0, c_blk0;  // (tile column J = block c_blk0 + J; uint32 arithmetic, -blk0 works)
   uint32_t B, n, n_col_blocks, n_groups, buckets_per_group;
   int sym;
   uint32_t row_begin, row_end;
   uint64_t tile_begin;
+  const uint32_t* tiles;  // optional (I, J) list (global block indices), sym semantics
   int32_t* out;
   uint64_t ld;
   uint32_t cap;  // column elements per chunk (<= kJCap): table load <= cap / kFSlots
+  int packed;    // out = [tile - tile_begin][64][64]
 };
 
 // Elements of one chunk held in registers: column elements k = cs + tid + kJB * u
@@ -696,24 +698,28 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
   const uint32_t grp = blockIdx.x % a.n_groups;
   uint32_t I, J;
-  if (a.sym) {
+  if (a.tiles) {
+    I = a.tiles[2 * t];
+    J = a.tiles[2 * t + 1];
+  } else if (a.sym) {
     sym_tile(t, a.n_col_blocks, I, J);
   } else {
     I = (uint32_t)(t / a.n_col_blocks);
     J = (uint32_t)(t % a.n_col_blocks);
   }
-  const uint32_t row0 = (a.sym ? 0 : a.row_begin) + I * kTile;
-  const uint32_t row_lim = a.sym ? a.n : a.row_end;
+  const bool rows_mode = !a.sym && !a.tiles;
+  const uint32_t row0 = (rows_mode ? a.row_begin : 0) + I * kTile;
+  const uint32_t row_lim = rows_mode ? a.row_end : a.n;
   const uint32_t col0 = J * kTile;
   const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t rblk = a.r_blk0 + I;
-  const uint64_t rb = a.r.bstart[rblk], cb = a.c.bstart[J];
+  const uint32_t rblk = a.r_blk0 + I, cblk = a.c_blk0 + J;
+  const uint64_t rb = a.r.bstart[rblk], cb = a.c.bstart[cblk];
   const uint64_t* rdata = a.r.data + rb;
   const uint8_t* rids = a.r.ids + rb;
   const uint64_t* cdata = a.c.data + cb;
   const uint8_t* cids = a.c.ids + cb;
   const uint32_t* roff = a.r.boff + (uint64_t)rblk * (a.B + 1);
-  const uint32_t* coff = a.c.boff + (uint64_t)J * (a.B + 1);
+  const uint32_t* coff = a.c.boff + (uint64_t)cblk * (a.B + 1);
   const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);
 
   for (int i = tid; i < kFSlots / 4; i += kJB)
@@ -935,9 +941,13 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
     if (!cnt) continue;
     const uint32_t gr = row0 + r, gc = col0 + c;
     if (gr >= row_lim || gc >= a.n) continue;
-    const uint64_t orow = a.sym ? gr : (gr - a.row_begin);
+    if (a.packed) {
+      atomicAdd(&a.out[(t - a.tile_begin) * (kTile * kTile) + r * kTile + c], (int32_t)cnt);
+      continue;
+    }
+    const uint64_t orow = rows_mode ? (gr - a.row_begin) : gr;
     atomicAdd(&a.out[orow * a.ld + gc], (int32_t)cnt);
-    if (a.sym && I != J) atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
+    if (!rows_mode && I != J) atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
   }
 #ifdef SKS_JOIN_STAMPS
   JSTAMP(4);
@@ -1074,14 +1084,17 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   return hipGetLastError();
 }
 
-hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t n,
-                       uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
-                       uint64_t tile_begin, uint64_t tile_end, int32_t* out, hipStream_t s) {
+hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
+                       uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
+                       uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
+                       int32_t* out, hipStream_t s) {
   const uint32_t n_cb = (n + kTile - 1) / kTile;
   const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
-  const uint64_t all_tiles = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
-  if (!sym) { tile_begin = 0; tile_end = all_tiles; }
-  tile_end = std::min(tile_end, all_tiles);
+  if (!d_tiles) {
+    const uint64_t all_tiles = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
+    if (!sym) { tile_begin = 0; tile_end = all_tiles; }
+    tile_end = std::min(tile_end, all_tiles);
+  }
   if (tile_begin >= tile_end) return hipSuccess;
   const uint64_t tiles = tile_end - tile_begin;
   const uint32_t B = 1u << log_b;
@@ -1089,10 +1102,13 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.r = rows;
   ja.c = cols;
   ja.r_blk0 = r_blk0;
+  ja.c_blk0 = c_blk0;
+  ja.tiles = d_tiles;
+  ja.packed = packed ? 1 : 0;
   ja.B = B;
   ja.n = n;
   ja.n_col_blocks = n_cb;
-  ja.sym = sym ? 1 : 0;
+  ja.sym = (sym || d_tiles) ? 1 : 0;
   ja.row_begin = row_begin;
   ja.row_end = row_end;
   ja.tile_begin = tile_begin;
@@ -1121,6 +1137,7 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
     const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
     ja.tile_begin = t0;
+    if (packed) ja.out = out + (t0 - tile_begin) * (uint64_t)(kTile * kTile);
     hipLaunchKernelGGL(k_join, dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1314,18 +1331,17 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       JoinLayout rl = cl;
       uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
       if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
-      if ((e = join_layout_build(data, starts, sizes, 0, n, total, log_b, const_cast<uint64_t*>(cl.data),
-                                 const_cast<uint8_t*>(cl.ids), const_cast<uint32_t*>(cl.boff),
-                                 const_cast<uint64_t*>(cl.bstart), stat, w + o_tmp, tmp_c, s)) != hipSuccess)
-        return e;
+      auto build_layout = [&](uint32_t first, uint32_t cnt, uint64_t tot, const JoinLayout& L,
+                              size_t tmp_bytes) -> hipError_t {
+        return join_layout_build(data, starts, sizes, first, cnt, tot, log_b, const_cast<uint64_t*>(L.data),
+                                 const_cast<uint8_t*>(L.ids), const_cast<uint32_t*>(L.boff),
+                                 const_cast<uint64_t*>(L.bstart), stat, w + o_tmp, tmp_bytes, s);
+      };
+      if ((e = build_layout(0, n, total, cl, tmp_c)) != hipSuccess) return e;
       if (sep_rows) {
         rl = JoinLayout{reinterpret_cast<uint64_t*>(w + o_rdat), reinterpret_cast<uint8_t*>(w + o_rids),
                         reinterpret_cast<uint32_t*>(w + o_rbof), reinterpret_cast<uint64_t*>(w + o_rbst)};
-        if ((e = join_layout_build(data, starts, sizes, row_begin, rn, r_total, log_b,
-                                   const_cast<uint64_t*>(rl.data), const_cast<uint8_t*>(rl.ids),
-                                   const_cast<uint32_t*>(rl.boff), const_cast<uint64_t*>(rl.bstart),
-                                   stat, w + o_tmp, tmp_r, s)) != hipSuccess)
-          return e;
+        if ((e = build_layout(row_begin, rn, r_total, rl, tmp_r)) != hipSuccess) return e;
       }
       uint32_t h_stat = 0;
       if ((e = pinned_d2h(&h_stat, stat, 4, s)) != hipSuccess) return e;
@@ -1337,7 +1353,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       // buckets are tried first while the count matrix allows
       if (h_stat <= join_cap() || log_b >= kJMaxLogB) {
         const uint32_t r_blk0 = sep_rows ? 0 : (sym ? 0 : row_begin / kTile);
-        if ((e = join_launch(rl, r_blk0, cl, n, log_b, sym, row_begin, row_end, tile_begin, tile_end,
+        if ((e = join_launch(rl, r_blk0, cl, 0, n, log_b, sym, row_begin, row_end, tile_begin, tile_end, nullptr, false,
                              out, s)) != hipSuccess)
           return e;
         *used_tiles = true;

@@ -52,7 +52,6 @@ using jc::sym_tile;
 constexpr int kRB = 512;              // threads per workgroup (8 waves)
 constexpr int kTile = 64;
 constexpr int kRCap = 1024;           // column elements per chunk (entry index: 10 bits)
-constexpr int kRMade = kRCap / kRB;   // column elements per thread per chunk (insert map)
 constexpr int kRWin = 256;            // bucket starts staged per window
 constexpr int kPlanes = 32;           // bit-sliced counter planes (any int32 count)
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
@@ -180,9 +179,26 @@ __global__ __launch_bounds__(kPB) void k_rj_pos(const uint64_t* __restrict__ dat
     if (last == 0xFFFFFFFFu || b > last) P[b] = sz;
 }
 
+// One thread's share of a chunk, read from the LDS ranges once: column
+// elements at chunk-order positions x = clo, clo + 8, ... < chi, element x at
+// data[csrc + x]; row elements at data[j], j = rlo, rlo + 8, ... < rhi; and the
+// first two of each, loaded ahead.
 struct ChunkRegs {
+  uint32_t clo, chi, csrc, rlo, rhi;
   uint64_t c[2], r[2];
 };
+
+// inclusive prefix sum over the 64 lanes of a wave (DPP row shifts, then the
+// row broadcasts of lanes 15 and 31; no LDS)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
 
 struct RJoinArgs {
   const uint64_t* data;
@@ -262,12 +278,7 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
   auto store_ranges = [&](int buf, uint32_t pb, uint32_t pe) {  // waves 0-1, all lanes
     if (wave == 0) {
       const uint32_t c = pe - pb;
-      uint32_t incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t x = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += x;
-      }
+      const uint32_t incl = wave_incl_scan(c);
       s_cb[buf][lane] = my_st + pb;
       s_cp[buf][lane] = incl - c;
       if (lane == 63) s_cp[buf][kTile] = incl;
@@ -307,26 +318,48 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
   };
 
   const int rs_s = tid >> 3, rs_k = tid & 7;  // range map: sketch, lane within it
-  // first two elements of this thread's share of a chunk's column range (chunk
-  // order [c0, c1)) and row range, from the ranges in buffer `rb`
+  // this thread's share of a chunk (chunk order [c0, c1)) from the ranges in
+  // buffer `rb`, with its first two column and row elements
   auto fetch_first = [&](int rb, uint32_t c0, uint32_t c1, bool rows, ChunkRegs& o) {
+    o.clo = o.chi = o.rlo = o.rhi = 0;
+    o.csrc = 0;
     o.c[0] = o.c[1] = o.r[0] = o.r[1] = 0;
     if ((uint32_t)rs_s < c_valid) {
       const uint32_t p0 = s_cp[rb][rs_s], p1 = s_cp[rb][rs_s + 1];
-      const uint32_t x = max(p0, c0) + rs_k, hi = min(p1, c1);
-      const uint64_t* src = a.data + s_cb[rb][rs_s] - p0;
-      if (x < hi) o.c[0] = src[x];
-      if (x + 8 < hi) o.c[1] = src[x + 8];
+      o.clo = max(p0, c0) + rs_k;
+      o.chi = min(p1, c1);
+      o.csrc = s_cb[rb][rs_s] - p0;
+      if (o.clo < o.chi) o.c[0] = a.data[o.csrc + o.clo];
+      if (o.clo + 8 < o.chi) o.c[1] = a.data[o.csrc + o.clo + 8];
+      o.clo -= c0;  // chunk-relative: the entry index of the first element
+      o.chi = o.chi > c0 ? o.chi - c0 : 0;
+      o.csrc += c0;
     }
     if (rows && (uint32_t)rs_s < r_valid) {
-      const uint32_t j = s_rb[rb][rs_s] + rs_k, re = s_re[rb][rs_s];
-      if (j < re) o.r[0] = a.data[j];
-      if (j + 8 < re) o.r[1] = a.data[j + 8];
+      o.rlo = s_rb[rb][rs_s] + rs_k;
+      o.rhi = s_re[rb][rs_s];
+      if (o.rlo < o.rhi) o.r[0] = a.data[o.rlo];
+      if (o.rlo + 8 < o.rhi) o.r[1] = a.data[o.rlo + 8];
     }
   };
-  uint32_t made[kRMade];  // slots this thread created in the current chunk
-#pragma unroll
-  for (int u = 0; u < kRMade; ++u) made[u] = kNoSlot;
+  // insert value v as entry e of column rs_s: one 32-bit compare-swap; a value
+  // already present adds the column bit to the entry its slot names.  The entry
+  // is written before its slot can name it (a wave's LDS operations complete
+  // in order), so no barrier separates staging from inserting.  Returns the
+  // entry now holding v.
+  // resolve an insert whose first compare-swap at slot h returned x
+  auto insert_chain = [&](uint64_t v, uint32_t e, uint32_t tag, uint32_t h, uint32_t x) -> uint32_t {
+    const unsigned long long bit = 1ull << rs_s;
+    for (;;) {
+      if (x == kFFree) return e;
+      if ((x >> 10) == tag && s_ent[x & 1023u].x == v) {
+        atomicOr(&s_ent[x & 1023u].y, bit);
+        return x & 1023u;
+      }
+      h = (h + 1) & (kFSlots - 1);
+      x = atomicCAS(&s_slot[h], kFFree, (tag << 10) | e);
+    }
+  };
   int buf = 0;
 
   const uint32_t b0 = grp * a.buckets_per_group;
@@ -374,10 +407,8 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
       if (x0 < we) pos_load(x0, x1, qb, qe);
     }
     __syncthreads();
-    // the first two elements of this thread's column / row range of a chunk,
-    // loaded one chunk ahead (the row ones only when the chunk probes)
     ChunkRegs cur, nxt;
-    fetch_first(buf, cs - s_coff[0], ce - s_coff[0], !(self_tile && ce == s_coff[be - wb]), cur);
+    fetch_first(buf, 0, ce - cs, !(self_tile && ce == s_coff[be - wb]), cur);
     while (bs < we) {
       uint32_t nbs, nbe, ncs, nce;
       advance(bs, be, ce, nbs, nbe, ncs, nce);
@@ -385,30 +416,14 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
       const uint32_t cbase = s_coff[bs - wb];  // chunk order: [cs - cbase, ce - cbase)
       const bool whole = cs == cbase && ce == s_coff[be - wb];
       // the next chunk's ranges, from registers (its buffer was last read
-      // before the barrier that ended the previous chunk)
+      // before the barrier that ended the previous chunk); the previous
+      // chunk's table entries all go (cheaper than tracking who made which)
       if (has_next && wave < 2) store_ranges(buf ^ 1, qb, qe);
-
-      // 0) free the previous chunk's slots and stage this chunk's column
-      //    elements as entries {value, column bit}
-#pragma unroll
-      for (int u = 0; u < kRMade; ++u) {
-        if (made[u] != kNoSlot) s_slot[made[u]] = kFFree;
-        made[u] = kNoSlot;
-      }
-      if ((uint32_t)rs_s < c_valid) {
-        const uint32_t c0 = cs - cbase, c1 = ce - cbase;
-        const uint32_t p0 = s_cp[buf][rs_s], p1 = s_cp[buf][rs_s + 1];
-        const uint32_t lo = max(p0, c0), hi = min(p1, c1);
-        const uint64_t* src = a.data + s_cb[buf][rs_s] - p0;
-        const unsigned long long bit = 1ull << rs_s;
-        uint32_t x = lo + rs_k;
-        if (x < hi) s_ent[x - c0] = make_ulonglong2(cur.c[0], bit);
-        if (x + 8 < hi) s_ent[x + 8 - c0] = make_ulonglong2(cur.c[1], bit);
-        for (x += 16; x < hi; x += 8) s_ent[x - c0] = make_ulonglong2(src[x], bit);
-      }
+      for (int i = tid; i < kFSlots / 4; i += kRB)
+        reinterpret_cast<uint4*>(s_slot)[i] = make_uint4(kFFree, kFFree, kFFree, kFFree);
       __syncthreads();
-      // in flight during the insert and probe: the positions of the chunk after
-      // the next (waves 0-1) and the next chunk's first elements
+      // in flight during the inserts and probes: the positions of the chunk
+      // after the next (waves 0-1) and the next chunk's first elements
       if (has_next && wave < 2) {
         uint32_t x0, x1, x2, x3;
         advance(nbs, nbe, nce, x0, x1, x2, x3);
@@ -417,69 +432,53 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
       if (has_next)
         fetch_first(buf ^ 1, ncs - s_coff[nbs - wb], nce - s_coff[nbs - wb],
                     !(self_tile && ncs == s_coff[nbs - wb] && nce == s_coff[nbe - wb]), nxt);
-      // 1) insert: one 32-bit compare-swap per element; a value already
-      //    present adds its column bit to the entry the slot names
-      const uint32_t ne = ce - cs;
-      uint32_t hs[kRMade], prev[kRMade], tags[kRMade], ent[kRMade], cid[kRMade];
-      uint64_t cv[kRMade];
-#pragma unroll
-      for (int u = 0; u < kRMade; ++u) {
-        hs[u] = kNoSlot;
-        ent[u] = 0;
-        cid[u] = kTile;
-        const uint32_t e = tid + kRB * u;
-        if (e < ne) {
-          const ulonglong2 en = s_ent[e];  // nothing ORs into e before its own slot exists
-          cv[u] = en.x;
-          cid[u] = (uint32_t)__builtin_ctzll(en.y);
-          hs[u] = fp_slot(cv[u]);
-          tags[u] = fp_tag(cv[u]);
-          prev[u] = atomicCAS(&s_slot[hs[u]], kFFree, (tags[u] << 10) | e);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kRMade; ++u) {
-        if (hs[u] == kNoSlot) continue;
-        const uint64_t v = cv[u];
-        const uint32_t e = tid + kRB * u;
-        uint32_t h = hs[u], x = prev[u];
-        for (;;) {
-          if (x == kFFree) {
-            made[u] = h;
-            ent[u] = e;
-            break;
-          }
-          if ((x >> 10) == tags[u] && s_ent[x & 1023u].x == v) {
-            atomicOr(&s_ent[x & 1023u].y, 1ull << cid[u]);
-            ent[u] = x & 1023u;
-            break;
-          }
-          h = (h + 1) & (kFSlots - 1);
-          x = atomicCAS(&s_slot[h], kFFree, (tags[u] << 10) | e);
+      // 1) stage + insert this thread's column elements
+      uint32_t ent0 = kNoSlot, ent1 = kNoSlot;
+      {
+        // the two register elements: both entries written and both first
+        // compare-swaps issued before either chain is resolved
+        const bool in0 = cur.clo < cur.chi, in1 = cur.clo + 8 < cur.chi;
+        const unsigned long long bit = 1ull << rs_s;
+        const uint32_t t0 = fp_tag(cur.c[0]), t1 = fp_tag(cur.c[1]);
+        const uint32_t h0 = fp_slot(cur.c[0]), h1 = fp_slot(cur.c[1]);
+        uint32_t x0 = kFFree, x1 = kFFree;
+        if (in0) s_ent[cur.clo] = make_ulonglong2(cur.c[0], bit);
+        if (in1) s_ent[cur.clo + 8] = make_ulonglong2(cur.c[1], bit);
+        if (in0) x0 = atomicCAS(&s_slot[h0], kFFree, (t0 << 10) | cur.clo);
+        if (in1) x1 = atomicCAS(&s_slot[h1], kFFree, (t1 << 10) | (cur.clo + 8));
+        if (in0) ent0 = insert_chain(cur.c[0], cur.clo, t0, h0, x0);
+        if (in1) ent1 = insert_chain(cur.c[1], cur.clo + 8, t1, h1, x1);
+        for (uint32_t x = cur.clo + 16; x < cur.chi; x += 8) {
+          const uint64_t v = a.data[cur.csrc + x];
+          s_ent[x] = make_ulonglong2(v, bit);
+          const uint32_t tg = fp_tag(v), hh = fp_slot(v);
+          insert_chain(v, x, tg, hh, atomicCAS(&s_slot[hh], kFFree, (tg << 10) | x));
         }
       }
       __syncthreads();
       // 2) probe.  A diagonal tile's chunk of whole buckets has its column
       //    elements as its row elements: each one's hits are the final mask of
-      //    the entry it created or joined
+      //    the entry it created or joined (the first two in registers; any
+      //    further ones look their value up like a row element)
       if (self_tile && whole) {
-#pragma unroll
-        for (int u = 0; u < kRMade; ++u) {
-          const uint32_t r = cid[u];
-          if (hs[u] == kNoSlot || r >= r_valid) continue;
-          add_hits(r, s_ent[ent[u]].y);
+        if ((uint32_t)rs_s < r_valid) {
+          if (ent0 != kNoSlot) add_hits(rs_s, s_ent[ent0].y);
+          if (ent1 != kNoSlot) add_hits(rs_s, s_ent[ent1].y);
+          for (uint32_t x = cur.clo + 16; x < cur.chi; x += 8) {
+            const uint64_t v = a.data[cur.csrc + x];
+            const uint32_t h = fp_slot(v);
+            add_hits(rs_s, lookup(v, h, s_slot[h]));
+          }
         }
       } else if ((uint32_t)rs_s < r_valid) {
-        const uint32_t re = s_re[buf][rs_s];
-        const uint32_t j0 = s_rb[buf][rs_s] + rs_k;
-        const bool ok0 = j0 < re, ok1 = j0 + 8 < re;
+        const bool ok0 = cur.rlo < cur.rhi, ok1 = cur.rlo + 8 < cur.rhi;
         const uint32_t h0 = fp_slot(cur.r[0]), h1 = fp_slot(cur.r[1]);
         const uint32_t x0 = ok0 ? s_slot[h0] : kFFree, x1 = ok1 ? s_slot[h1] : kFFree;
         const unsigned long long m0 = lookup(cur.r[0], h0, x0);
         if (m0) add_hits(rs_s, m0);
         const unsigned long long m1 = lookup(cur.r[1], h1, x1);
         if (m1) add_hits(rs_s, m1);
-        for (uint32_t j = j0 + 16; j < re; j += 8) {
+        for (uint32_t j = cur.rlo + 16; j < cur.rhi; j += 8) {
           const uint64_t v = a.data[j];
           const uint32_t h = fp_slot(v);
           const unsigned long long m = lookup(v, h, s_slot[h]);

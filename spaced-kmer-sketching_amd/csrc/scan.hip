@@ -126,12 +126,16 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s)
 // without overlapping), and validity of all 4 bytes is one v_sad_u8 against
 // the expected lower-case letters.  Only a 16-base word holding a non-ACGT
 // byte pays for the exact per-byte invalid bits (encode4).
+// ALIGNED: the tile's bytes start on a dword boundary (sb == 0, wave-uniform;
+// a genome starting at a 4-byte multiple, e.g. config 3), so the dwords are
+// used as they are and the four alignbits go.
+template <bool ALIGNED>
 __device__ __forceinline__ void pack16(const uint32_t (&x)[5], uint32_t sb, uint32_t& le,
                                        uint32_t& inv) {
   uint32_t w[4], g[4], sad = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    w[k] = funnel(x[k + 1], x[k], sb);  // alignbit by 0 returns x[k]
+    w[k] = ALIGNED ? x[k] : funnel(x[k + 1], x[k], sb);
     const uint32_t low = w[k] | 0x20202020u;
     const uint32_t code = ((low >> 1) ^ (low >> 2)) & 0x03030303u;
     const uint32_t expect = __builtin_amdgcn_perm(0u, 0x74676361u, code);
@@ -333,17 +337,23 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
     __syncthreads();
 
     // 2) pack: word i covers bases [16 i, 16 i + 16) of the tile
-    for (int i = tid; i < kWords; i += kBlock) {
-      const uint32_t b0 = 16 * i + shift;  // byte offset in s_raw
-      const uint32_t wi = b0 >> 2, sb = (b0 & 3) * 8;
-      uint32_t x[5];
+    {
+      const uint32_t sb = (shift & 3) * 8;  // wave-uniform
+      auto pack_words = [&](auto aligned) {
+        for (int i = tid; i < kWords; i += kBlock) {
+          const uint32_t wi = (16 * i + shift) >> 2;  // dword offset in s_raw
+          uint32_t x[5];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) x[k] = s_raw[wi + k];
-      uint32_t le, inv;
-      pack16(x, sb, le, inv);
-      s_be[kBeOff + i] = rev_pairs(le);
-      s_lc[i] = ~le;
-      s_inv[i] = inv;
+          for (int k = 0; k < 5; ++k) x[k] = (decltype(aligned)::value && k == 4) ? 0u : s_raw[wi + k];
+          uint32_t le, inv;
+          pack16<decltype(aligned)::value>(x, sb, le, inv);
+          s_be[kBeOff + i] = rev_pairs(le);
+          s_lc[i] = ~le;
+          s_inv[i] = inv;
+        }
+      };
+      if (sb == 0) pack_words(std::true_type{});
+      else pack_words(std::false_type{});
     }
     __syncthreads();
 
@@ -588,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
 #pragma unroll
       for (int k = 0; k < 5; ++k) x[k] = s_raw[wi + k];
       uint32_t le, inv;
-      pack16(x, sb, le, inv);
+      pack16<false>(x, sb, le, inv);
       s_be[i] = rev_pairs(le);
       s_lc[i] = ~le;
       s_inv[i] = inv;

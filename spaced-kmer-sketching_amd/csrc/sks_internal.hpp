@@ -210,9 +210,16 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
                              uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
                              uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
                              hipStream_t s);
-hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t n,
-                       uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
-                       uint64_t tile_begin, uint64_t tile_end, int32_t* out, hipStream_t s);
+// Tiles of the n x n (sym: upper-triangle range [tile_begin, tile_end), or
+// with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
+// written) or rows x n matrix; tile (I, J) reads row block r_blk0 + I of
+// `rows` and column block c_blk0 + J of `cols` (uint32 arithmetic: 0 - blk0
+// maps global block indices onto a layout whose block 0 is blk0).  packed:
+// out = [tile - tile_begin][64][64].  Counts are added to `out`.
+hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
+                       uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
+                       uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
+                       int32_t* out, hipStream_t s);
 
 // Block postings (postings.hip): per 64-sketch block and hash bucket, the
 // distinct values with a 64-bit mask of the block's sketches holding each,

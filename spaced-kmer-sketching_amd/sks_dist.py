@@ -10,6 +10,7 @@ pairs (kmer_set.cpp:179) inside one process.  Here:
 The functions take the count kernel as a callable so the same orchestration is
 exercised on CPU with gloo in tests/test_dist_cpu.py.
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -151,206 +152,14 @@ def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
     return acc, mine
 
 
-# ---- all-vs-all over gathered join layouts ------------------------------------------------
-# The join kernel's input (sks_join_layout_build) is built per 64-sketch block,
-# so each rank builds the layout of its OWN block-aligned genome range and the
-# ranks all-gather layouts instead of raw sketches: nothing is rebuilt on every
-# rank, and the gathered bytes (9 B per element + bucket starts) are about the
-# same as the padded sketches.  Block k of the gathered layout is block
-# k - r*bpr of rank r, so its start is shifted by r * (padded layout size).
-
-def block_shard(n_genomes, world, rank):
-    """(blocks per rank, g0, g1): genome range of `rank`, whole 64-sketch blocks."""
-    n_blk = (n_genomes + TILE - 1) // TILE
-    bpr = max(1, (n_blk + world - 1) // world)
-    g0 = min(n_genomes, rank * bpr * TILE)
-    return bpr, g0, min(n_genomes, g0 + bpr * TILE)
-
-
-def _max_over(x, world, device):
-    if _solo(world):
-        return int(x)
-    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return int(t.item())
-
-
-def _gather_flat(t, world):
-    return _gather_many([t], world)[0]
-
-
-def _gather_many(ts, world):
-    """All-gather of flat tensors, rank-major; with RCCL the gathers are queued
-    together (async) and waited on once, so their latencies overlap."""
-    if _solo(world):
-        return list(ts)
-    if dist.get_backend() == "nccl":
-        outs, works = [], []
-        for t in ts:
-            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
-            works.append(dist.all_gather_into_tensor(out, t.contiguous(), async_op=True))
-            outs.append(out)
-        for w in works:
-            w.wait()
-        return outs
-    res = []
-    for t in ts:
-        host = t.cpu()
-        parts = [torch.empty_like(host) for _ in range(world)]
-        dist.all_gather(parts, host)
-        res.append(torch.cat(parts).to(t.device))
-    return res
-
-
-def all_vs_all_join(n_genomes, world, rank, local_max_size, log_b_for, capacity, build, count,
-                    device="cpu", out=None, max_log_b=14, local_total=None):
-    """Full n x n int32 intersection matrix on every rank.
-
-    build(log_b, pad) -> (data u64[], ids u8[], boff u32[], bstart u64[], max_block_bucket)
-    builds the layout of this rank's block-aligned genomes (block_shard).  pad is
-    None for one rank without a process group; otherwise (cap_e, bpr) and the
-    buffers must have exactly cap_e data / id entries, bpr * (B + 1) bucket starts
-    and bpr + 1 block starts (entries past the rank's own blocks are never read:
-    those blocks lie beyond n), so they are all-gathered as they are.
-    max_block_bucket may be None (the build skipped that read-back).
-    count(n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out) fills `out`
-    (zeroed first) with the counts of upper-triangle tiles [tile_begin, tile_end), both halves
-    — the contract of sks_intersect_sym_layout.
-
-    The bucket count is raised while the largest block-bucket (over all ranks)
-    exceeds the join table's `capacity`, up to 2^max_log_b buckets.  That is a
-    speed choice, not a correctness one: k_join cuts a bucket above capacity into
-    table-sized sub-chunks and probes the bucket's row elements once per
-    sub-chunk, so the counts at max_log_b are exact for any sketch size.
-
-    local_total: this rank's element count.  The layouts are built straight
-    into padded send buffers of max-over-ranks(local_total) elements (one
-    all-reduce carries it with the largest sketch size); without it the pad is
-    the bound bpr * 64 * (largest sketch), which over-allocates and over-sends
-    when sketch sizes are skewed (FracMinHash of genomes of different lengths)."""
-    bpr, g0, g1 = block_shard(n_genomes, world, rank)
-    if local_total is None:
-        max_all = _max_over(local_max_size, world, device)
-        cap_bound = bpr * TILE * max_all
-    else:
-        max_all, cap_bound = _max_over_many([local_max_size, local_total], world, device)
-    log_b = log_b_for(max_all)
-    solo = _solo(world)
-    # the layouts are built straight into padded send buffers: no all-reduce
-    # of the layout sizes and no copies before the gather
-    pad = None if solo else (max(1, cap_bound), bpr)
-    while True:
-        data, ids, boff, bstart, mb = build(log_b, pad)
-        if mb is None or log_b >= max_log_b:
-            break
-        if (mb if solo else _max_over(mb, world, device)) <= capacity:
-            break
-        log_b += 1
-    t0, t1 = tile_shard(sym_tiles(n_genomes), world, rank)
-    if out is None:
-        out = torch.empty((n_genomes, n_genomes), dtype=torch.int32, device=device)
-    if solo:  # the local layout is the whole layout
-        count(n_genomes, log_b, data, ids, boff, bstart, t0, t1, out)
-        return out
-    cap_e = pad[0]
-    g_data, g_ids, g_boff, g_bst = _gather_many([data, ids, boff, bstart], world)
-    # block k of rank r starts at r * cap_e in the gathered data
-    g_bst = g_bst.view(world, bpr + 1)[:, :bpr] + \
-        torch.arange(world, device=g_bst.device, dtype=torch.int64).view(world, 1) * cap_e
-    g_bst = torch.cat([g_bst.reshape(-1),
-                       torch.full((1,), world * cap_e, dtype=torch.int64, device=g_bst.device)])
-    count(n_genomes, log_b, g_data, g_ids, g_boff, g_bst, t0, t1, out)
-    sum_matrix(out)
-    return out
-
-
-def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None, stat=True):
-    """The build / count callables of all_vs_all_join for this rank's sketches
-    on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
-    `local_sizes` its sizes (numpy).  build(log_b, pad) runs sks_join_layout_build
-    into device buffers (kept in `cache` across calls of the same shape) and
-    returns them on `device`; count(...) runs sks_intersect_sym_layout (on the
-    GPU, staging through `device` tensors when that is the CPU, as with gloo).
-    stat=False: the build does not read back its largest block-bucket (mb is
-    None), so nothing waits between the layout and the count; the bucket count
-    is then the first one tried (a speed choice only: counts are exact at any)."""
-    n_local = len(local_sizes)
-    nb_local = (n_local + TILE - 1) // TILE
-    data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
-    tot = int(local_sizes.astype("int64").sum()) if n_local else 0
-    cache = {} if cache is None else cache
-
-    def build(log_b, pad=None):
-        B1 = (1 << log_b) + 1
-        # padded (all_vs_all_join with a process group): the send buffers
-        # themselves, cap_e elements and bpr blocks, gathered as they are
-        cap_e, nb = pad if pad is not None else (max(tot, 1), max(nb_local, 1))
-        key = (cap_e, log_b, nb)
-        if key not in cache:  # layout buffers persist across steps
-            cache.clear()
-            cache[key] = (torch.empty(cap_e, dtype=torch.int64, device="cuda"),
-                          torch.empty(cap_e, dtype=torch.uint8, device="cuda"),
-                          torch.zeros(nb * B1, dtype=torch.int32, device="cuda"),
-                          torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
-        out = cache[key]
-        mx = ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out),
-                                   stat=stat)
-        return tuple(t.to(device) for t in out) + (mx,)
-
-    def count(n, log_b, d, i, b, s, t0, t1, out):
-        lay = [t.to("cuda") for t in (d, i, b, s)]
-        tgt = out if out.is_cuda else torch.empty(out.shape, dtype=out.dtype, device="cuda")
-        ctx.intersect_sym_layout(n, log_b, *(t.data_ptr() for t in lay), t0, t1, tgt.data_ptr())
-        if tgt is not out:
-            out.copy_(tgt.cpu())
-    return build, count
-
-
-# ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------
-# FracMinHash keeps a k-mer on its own hash, so the sketch of a genome is the
-# union of the sketches of chunks cut with (w-1)-base halos: rank r scans the
-# windows that start in [r*n/world, (r+1)*n/world), the chunk sets are
-# all-gathered (padded to the largest) and every rank forms the sorted union.
-
-def genome_chunk(n_bytes, w, world, rank):
-    a = n_bytes * rank // world
-    b = n_bytes * (rank + 1) // world
-    return a, min(n_bytes, b + w - 1) if b > a else b
-
-
-def sketch_genome_sharded(n_bytes, w, world, rank, build_chunk, union, device="cpu"):
-    """build_chunk(a, b) -> (int64 tensor of the chunk's sorted k-mers, windows):
-    shape [k] for w <= 32, [k, 2] (lo, hi) for w > 32; union(t) -> sorted distinct
-    k-mers of t (same shape convention).  Returns (sketch, total windows) on
-    every rank."""
-    a, b = genome_chunk(n_bytes, w, world, rank)
-    vals, nw = build_chunk(a, b)
-    if _solo(world):
-        return vals, nw
-    k = vals.shape[0]
-    rest = tuple(vals.shape[1:])
-    kmax = max(1, _max_over(k, world, device))
-    pad = torch.zeros((kmax,) + rest, dtype=torch.int64, device=device)
-    pad[:k] = vals
-    g = _gather_flat(pad.reshape(-1), world).view((world, kmax) + rest)
-    sizes = _gather_flat(torch.tensor([k], dtype=torch.int64, device=device), world)
-    keep = torch.arange(kmax, device=device).view(1, kmax) < sizes.view(world, 1)
-    t = torch.tensor([nw], dtype=torch.int64, device=device)
-    dist.all_reduce(t)
-    return union(g[keep]), int(t.item())
-
-
-# ---- all-vs-all over the range join: packed tiles, overlap, one receiving rank ------------
-# The range join (sks_intersect_range, rjoin.hip) reads the sorted sketches
-# where they lie, so the exchange is the sketches themselves (8 B per element,
-# padded to the largest rank's total) and nothing is built before it.  Each
-# rank counts a fixed plan of upper-triangle 64x64 tiles (tile_plan): the tiles
-# of its own blocks first — from its own sketches, while the gather is in
+# ---- tile plan, packed tiles, one receiving rank ------------------------------------------
+# Each rank counts a fixed plan of upper-triangle 64x64 tiles (tile_plan): the
+# tiles of its own blocks first — from its own data, while the exchange is in
 # flight — then its half of every cross-rank block pair.  Counts stay packed
 # ([tile][64][64] int32, 16 KB per tile) and go to ONE rank (dst), where the
 # n x n matrix is assembled: no rank holds a matrix it does not need and no
-# collective carries n^2 words (the dense all-reduce of all_vs_all_join moved
-# 2 (N-1)/N n^2 words through every rank).
+# collective carries n^2 words (a dense all-reduce moves 2 (N-1)/N n^2 words
+# through every rank).
 
 def _ctx_waits_for_torch(ctx):
     """Order the context's HIP stream after work queued so far on torch's current
@@ -382,7 +191,6 @@ def tile_plan(n_genomes, world, rank):
     the lower rank takes the first half).  Every tile of the n x n upper
     triangle is in exactly one rank's plan; per-rank counts differ by at most
     one tile per rank pair (plus a short last rank)."""
-    import numpy as np
     nb = (n_genomes + TILE - 1) // TILE
     bpr = block_shard(n_genomes, world, rank)[0]
 
@@ -450,80 +258,151 @@ def _gather_tiles(parts, world, dst):
     return torch.stack(lst).to(parts.device)
 
 
-def place_tiles(mat, tiles, parts, n, chunk=8192):
+_PLACE_CACHE = {}
+
+
+def place_tiles(mat, tiles, parts, n):
     """Writes packed tile counts into the n x n matrix: tile (I, J) at rows
     64 I.., columns 64 J.., and mirrored when I != J (a diagonal tile holds both
-    triangles)."""
+    triangles).  The index maps depend only on (tiles, n): built once per
+    process and device, then every step is two gathers and two scatters."""
     dev = mat.device
-    flat = mat.view(-1)
-    ar = torch.arange(TILE, device=dev, dtype=torch.int64)
-    tiles = torch.as_tensor(tiles, dtype=torch.int64, device=dev).reshape(-1, 2)
-    for a in range(0, tiles.shape[0], chunk):
-        t = tiles[a:a + chunk]
-        p = parts[a:a + chunk].to(dev)
+    tiles = np.asarray(tiles, dtype=np.int64).reshape(-1, 2)
+    key = (tiles.tobytes(), n, str(dev))
+    if key not in _PLACE_CACHE:
+        if len(_PLACE_CACHE) > 4:
+            _PLACE_CACHE.clear()
+        t = torch.as_tensor(tiles, device=dev)
+        ar = torch.arange(TILE, device=dev, dtype=torch.int64)
         gr = (t[:, 0:1] * TILE + ar.view(1, -1)).view(-1, TILE, 1).expand(-1, TILE, TILE)
         gc = (t[:, 1:2] * TILE + ar.view(1, -1)).view(-1, 1, TILE).expand(-1, TILE, TILE)
-        ok = (gr < n) & (gc < n)
-        flat[(gr * n + gc)[ok]] = p[ok]
-        off = (t[:, 0] != t[:, 1]).view(-1, 1, 1) & ok
-        flat[(gc * n + gr)[off]] = p[off]
+        ok = ((gr < n) & (gc < n)).reshape(-1)
+        off = ((t[:, 0] != t[:, 1]).view(-1, 1, 1).expand(-1, TILE, TILE).reshape(-1)) & ok
+        src_up = torch.nonzero(ok).view(-1)
+        src_lo = torch.nonzero(off).view(-1)
+        flat_up = (gr * n + gc).reshape(-1)[src_up]
+        flat_lo = (gc * n + gr).reshape(-1)[src_lo]
+        _PLACE_CACHE[key] = (src_up, flat_up, src_lo, flat_lo)
+    src_up, flat_up, src_lo, flat_lo = _PLACE_CACHE[key]
+    vals = parts.reshape(-1).to(dev)
+    flat = mat.view(-1)
+    flat[flat_up] = vals[src_up]
+    flat[flat_lo] = vals[src_lo]
     return mat
 
 
-def all_vs_all_ranged(n_genomes, world, rank, data, starts, sizes, max_size, count, device="cpu",
-                      dst=0, out=None):
-    """n x n int32 intersection matrix on rank `dst` (None on the others; on every
-    rank when dst is None).
+# ---- all-vs-all over gathered join layouts ------------------------------------------------
+# The join kernel's input (sks_join_layout_build) is built per 64-sketch block,
+# so each rank builds the layout of its OWN block-aligned genome range, counts
+# the tiles of its own blocks on it while the ranks all-gather their layouts
+# (9 B per element + bucket starts, about the padded sketches' bytes; nothing
+# is rebuilt on every rank), then counts its cross-rank tiles on the gathered
+# layout.  Block k of the gathered layout is block k - r*bpr of rank r, so its
+# start is shifted by r * (padded layout size).
 
-    data / starts / sizes: this rank's sketches (block_shard's genome range):
-    int64 values (each sketch sorted, unique), int64 starts, int32 sizes.
-    max_size: its largest sketch.  count(data, starts, sizes, n, log_b, tiles,
-    out) adds the counts of `tiles` (int64 [T, 2] block indices into that
-    sketch numbering) to the packed int32 out [T, 64, 64]; it is called first
-    with the local sketches, then with the gathered ones, and must use one set
-    of bucket bounds across its calls (sks_intersect_range's contract)."""
+def block_shard(n_genomes, world, rank):
+    """(blocks per rank, g0, g1): genome range of `rank`, whole 64-sketch blocks."""
+    n_blk = (n_genomes + TILE - 1) // TILE
+    bpr = max(1, (n_blk + world - 1) // world)
+    g0 = min(n_genomes, rank * bpr * TILE)
+    return bpr, g0, min(n_genomes, g0 + bpr * TILE)
+
+
+def _max_over(x, world, device):
+    if _solo(world):
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
+def _gather_flat(t, world):
+    return _gather_many([t], world)[0]
+
+
+def _gather_many(ts, world):
+    """All-gather of flat tensors, rank-major; with RCCL the gathers are queued
+    together (async) and waited on once, so their latencies overlap."""
+    if _solo(world):
+        return list(ts)
+    if dist.get_backend() == "nccl":
+        outs, works = [], []
+        for t in ts:
+            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+            works.append(dist.all_gather_into_tensor(out, t.contiguous(), async_op=True))
+            outs.append(out)
+        for w in works:
+            w.wait()
+        return outs
+    res = []
+    for t in ts:
+        host = t.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host)
+        res.append(torch.cat(parts).to(t.device))
+    return res
+
+
+def all_vs_all_join(n_genomes, world, rank, local_max_size, local_total, log_b_for, build, count,
+                    device="cpu", out=None, dst=0):
+    """n x n int32 intersection matrix on rank `dst` (None on the others; on
+    every rank when dst is None).
+
+    build(log_b, pad) -> (data u64[], ids u8[], boff u32[], bstart u64[]): the
+    join layout of this rank's block-aligned genomes (block_shard).  pad is None
+    for one rank without a process group; otherwise (cap_e, bpr), and the
+    buffers must have exactly cap_e data / id entries, bpr * (B + 1) bucket
+    starts and bpr + 1 block starts (entries past the rank's own blocks are never
+    read), so they are all-gathered as they are.  cap_e is the largest rank's
+    element total (one all-reduce carries it with the largest sketch size).
+    count(n, log_b, layout, blk0, tiles, out) adds the counts of `tiles` (int64
+    [T, 2] global block indices, I <= J) to out — the packed int32 [T, 64, 64],
+    or the n x n int32 matrix (both halves) when out is 2-D — reading a layout
+    whose block 0 is global block blk0: the contract of
+    sks_intersect_layout_tiles.  One rank without a process group counts every
+    tile straight into the matrix.
+
+    The rank counts its tile_plan: its own blocks' tiles from its own layout
+    while the layouts are being gathered, then its share of the cross-rank
+    tiles; the packed tiles go to dst, which assembles the matrix.  The bucket
+    count comes from the largest sketch (counts are exact at any: k_join cuts a
+    bucket above its table into sub-chunks)."""
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
-    nl = g1 - g0
     solo = _solo(world)
+    max_all, cap_e = _max_over_many([local_max_size, local_total], world, device)
+    log_b = log_b_for(max(max_all, 1))
     local, remote = tile_plan(n_genomes, world, rank)
     T = len(local) + len(remote)
-    tot = int(sizes.to(torch.int64).sum()) if nl else 0
-    gmax, cap_e = _max_over_many([max_size, tot], world, device)
-    import sksffi
-    log_b = sksffi.range_log_b(max(gmax, 1))
-    parts = torch.zeros((max(T, 1), TILE, TILE), dtype=torch.int32, device=device)
+    lay = build(log_b, None if solo else (max(1, cap_e), bpr))
     if solo:
+        if out is None:
+            out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+        else:
+            out.zero_()
         if T:
-            count(data, starts, sizes, nl, log_b, local, parts[:len(local)])
-        tiles, got = local, parts[:T]
-    else:
-        per = bpr * TILE
-        cap_e = max(cap_e, 1)
-        send_d = torch.zeros(cap_e, dtype=torch.int64, device=device)
-        send_s = torch.zeros(per, dtype=torch.int64, device=device)
-        send_z = torch.zeros(per, dtype=torch.int32, device=device)
-        if nl:
-            send_d[:tot] = data[:tot]
-            send_s[:nl] = starts[:nl]
-            send_z[:nl] = sizes[:nl]
-        finish = _gather_start([send_d, send_s, send_z], world)
-        if len(local):  # the rank's own tiles while the sketches travel
-            count(data, starts, sizes, nl, log_b, local - g0 // TILE, parts[:len(local)])
-        g_d, g_s, g_z = finish()
-        g_s = (g_s.view(world, per) + torch.arange(world, device=g_s.device, dtype=torch.int64).view(world, 1)
-               * cap_e).reshape(-1)
-        if len(remote):
-            count(g_d, g_s, g_z, world * per, log_b, remote, parts[len(local):T])
-        tmax = max(sum(len(x) for x in tile_plan(n_genomes, world, q)) for q in range(world))
-        pad = torch.zeros((max(tmax, 1), TILE, TILE), dtype=torch.int32, device=device)
-        pad[:T] = parts[:T]
-        gathered = _gather_tiles(pad, world, dst)
-        if gathered is None:
-            return None
-        import numpy as np
-        plans = [tile_plan(n_genomes, world, q) for q in range(world)]
-        tiles = np.concatenate([np.concatenate(p) for p in plans]).reshape(-1, 2)
-        got = torch.cat([gathered[q, :sum(len(x) for x in plans[q])] for q in range(world)])
+            count(n_genomes, log_b, lay, 0, local, out)
+        return out
+    plans = [tile_plan(n_genomes, world, q) for q in range(world)]
+    sizes = [len(pl[0]) + len(pl[1]) for pl in plans]
+    # the rank's packed tiles, padded to the largest plan: the gather's send buffer
+    parts = torch.zeros((max(max(sizes), 1), TILE, TILE), dtype=torch.int32, device=device)
+    cap_e = max(1, cap_e)
+    finish = _gather_start(list(lay), world)
+    if len(local):  # the rank's own tiles while the layouts travel
+        count(n_genomes, log_b, lay, g0 // TILE, local, parts[:len(local)])
+    g_data, g_ids, g_boff, g_bst = finish()
+    # block k of rank r starts at r * cap_e in the gathered data
+    g_bst = g_bst.view(world, bpr + 1)[:, :bpr] + \
+        torch.arange(world, device=g_bst.device, dtype=torch.int64).view(world, 1) * cap_e
+    g_bst = torch.cat([g_bst.reshape(-1),
+                       torch.full((1,), world * cap_e, dtype=torch.int64, device=g_bst.device)])
+    if len(remote):
+        count(n_genomes, log_b, (g_data, g_ids, g_boff, g_bst), 0, remote, parts[len(local):T])
+    gathered = _gather_tiles(parts, world, dst)
+    if gathered is None:
+        return None
+    tiles = np.concatenate([np.concatenate(pl) for pl in plans]).reshape(-1, 2)
+    got = torch.cat([gathered[q, :sizes[q]] for q in range(world)])
     if out is None:
         out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
     else:
@@ -531,29 +410,91 @@ def all_vs_all_ranged(n_genomes, world, rank, data, starts, sizes, max_size, cou
     return place_tiles(out, tiles, got, n_genomes)
 
 
-def range_count_fn(ctx):
-    """count() of all_vs_all_ranged on the GPU (sks_range_bounds once, from the
-    first call's sketches, then sks_intersect_range per call).  Tensors may be
-    on the CPU (gloo): they are staged to the GPU and the counts copied back.
-    The context's stream is ordered after torch's current stream before its
-    kernels and torch's after them (any ctx stream works)."""
-    state = {}
+def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
+    """The build / count callables of all_vs_all_join for this rank's sketches
+    on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
+    `local_sizes` its sizes (numpy).  build(log_b, pad) runs
+    sks_join_layout_build into device buffers (kept in `cache` across calls of
+    the same shape) and returns them on `device`; count(...) runs
+    sks_intersect_layout_tiles (on the GPU, staging through `device` tensors
+    when that is the CPU, as with gloo).  The context's stream is ordered after
+    torch's current stream before its kernels and torch's after them, so a
+    context on any stream works with the collectives on torch's."""
+    n_local = len(local_sizes)
+    nb_local = (n_local + TILE - 1) // TILE
+    data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
+    tot = int(local_sizes.astype("int64").sum()) if n_local else 0
+    cache = {} if cache is None else cache
+    tile_cache = cache.setdefault("_tiles", {}) if isinstance(cache, dict) else {}
+    keep = {}
 
-    def count(data, starts, sizes, n, log_b, tiles, out):
-        d, st, sz = (t.to("cuda").contiguous() for t in (data, starts, sizes))
-        tl = torch.as_tensor(tiles, dtype=torch.int32).reshape(-1, 2).to("cuda").contiguous()
+    def build(log_b, pad=None):
+        B1 = (1 << log_b) + 1
+        # padded (all_vs_all_join with a process group): the send buffers
+        # themselves, cap_e elements and bpr blocks, gathered as they are
+        cap_e, nb = pad if pad is not None else (max(tot, 1), max(nb_local, 1))
+        key = (cap_e, log_b, nb)
+        if key not in cache:  # layout buffers persist across steps
+            for k in [k for k in cache if k != "_tiles"]:
+                del cache[k]
+            cache[key] = (torch.empty(cap_e, dtype=torch.int64, device="cuda"),
+                          torch.empty(cap_e, dtype=torch.uint8, device="cuda"),
+                          torch.zeros(nb * B1, dtype=torch.int32, device="cuda"),
+                          torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
+        out = cache[key]
+        _ctx_waits_for_torch(ctx)  # the buffers' previous readers (gathers, joins)
+        ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out), stat=False)
+        _torch_waits_for_ctx(ctx)
+        return tuple(t.to(device) for t in out)
+
+    def count(n, log_b, lay, blk0, tiles, out):
+        lay = [t.to("cuda") for t in lay]
+        key = ("tiles", tiles.tobytes())  # the plan repeats every step: upload it once
+        if key not in tile_cache:
+            if len(tile_cache) > 8:
+                tile_cache.clear()
+            tile_cache[key] = torch.as_tensor(tiles, dtype=torch.int32).reshape(-1, 2).to("cuda").contiguous()
+        tl = tile_cache[key]
         tgt = out if out.is_cuda else torch.zeros(out.shape, dtype=out.dtype, device="cuda")
         _ctx_waits_for_torch(ctx)
-        if "bounds" not in state:
-            b = torch.empty((1 << log_b) + 1, dtype=torch.int64, device="cuda")
-            ctx.range_bounds(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, log_b, b.data_ptr())
-            state["bounds"], state["log_b"] = b, log_b
-        assert state["log_b"] == log_b
-        ctx.intersect_range(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, log_b,
-                            state["bounds"].data_ptr(), tl.data_ptr(), 0, tl.shape[0], True,
-                            tgt.data_ptr())
+        ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in lay), blk0, tl.data_ptr(), 0,
+                                   tl.shape[0], out.dim() == 3, tgt.data_ptr())
         _torch_waits_for_ctx(ctx)
-        state["keep"] = (d, st, sz, tl)  # alive until the next call queues behind them
+        keep["last"] = (lay, tl)  # alive until torch's stream is past the kernel
         if tgt is not out:
             out.copy_(tgt.cpu())
-    return count
+    return build, count
+
+
+# ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------
+# FracMinHash keeps a k-mer on its own hash, so the sketch of a genome is the
+# union of the sketches of chunks cut with (w-1)-base halos: rank r scans the
+# windows that start in [r*n/world, (r+1)*n/world), the chunk sets are
+# all-gathered (padded to the largest) and every rank forms the sorted union.
+
+def genome_chunk(n_bytes, w, world, rank):
+    a = n_bytes * rank // world
+    b = n_bytes * (rank + 1) // world
+    return a, min(n_bytes, b + w - 1) if b > a else b
+
+
+def sketch_genome_sharded(n_bytes, w, world, rank, build_chunk, union, device="cpu"):
+    """build_chunk(a, b) -> (int64 tensor of the chunk's sorted k-mers, windows):
+    shape [k] for w <= 32, [k, 2] (lo, hi) for w > 32; union(t) -> sorted distinct
+    k-mers of t (same shape convention).  Returns (sketch, total windows) on
+    every rank."""
+    a, b = genome_chunk(n_bytes, w, world, rank)
+    vals, nw = build_chunk(a, b)
+    if _solo(world):
+        return vals, nw
+    k = vals.shape[0]
+    rest = tuple(vals.shape[1:])
+    kmax = max(1, _max_over(k, world, device))
+    pad = torch.zeros((kmax,) + rest, dtype=torch.int64, device=device)
+    pad[:k] = vals
+    g = _gather_flat(pad.reshape(-1), world).view((world, kmax) + rest)
+    sizes = _gather_flat(torch.tensor([k], dtype=torch.int64, device=device), world)
+    keep = torch.arange(kmax, device=device).view(1, kmax) < sizes.view(world, 1)
+    t = torch.tensor([nw], dtype=torch.int64, device=device)
+    dist.all_reduce(t)
+    return union(g[keep]), int(t.item())

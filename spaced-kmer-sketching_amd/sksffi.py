@@ -60,7 +60,7 @@ EXPORTED = [
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
     "sks_sketch_set_name", "sks_sketch_set_save", "sks_sketch_set_load", "sks_sketch_set_concat",
-    "sks_range_log_b", "sks_range_bounds", "sks_intersect_range",
+    "sks_range_log_b", "sks_range_bounds", "sks_intersect_range", "sks_intersect_layout_tiles",
 ]
 
 _lib = None
@@ -123,6 +123,8 @@ def lib():
                                         C.POINTER(C.c_uint32)]
     L.sks_intersect_sym_layout.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint64,
                                            C.c_uint64, vp]
+    L.sks_intersect_layout_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp,
+                                             C.c_uint64, C.c_uint64, C.c_int, vp]
     L.sks_range_log_b.argtypes = [C.c_uint32]
     L.sks_range_log_b.restype = C.c_uint32
     L.sks_range_bounds.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp]
@@ -346,6 +348,16 @@ class Context:
         check(lib().sks_intersect_range(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes),
                                         n, log_b, C.c_void_p(bounds), C.c_void_p(tiles) if tiles else None,
                                         tile_begin, tile_end, 1 if packed else 0, C.c_void_p(out)))
+
+    def intersect_layout_tiles(self, n, log_b, data, ids, boff, bstart, blk0, tiles, tile_begin, tile_end,
+                               packed, out):
+        """sks_intersect_layout_tiles: join tiles over a layout whose block 0 is
+        global block blk0; counts ADDED to `out` (n x n both halves, or packed
+        [tile][64][64]); tiles: device pointer of (I, J) u32 pairs, or 0."""
+        check(lib().sks_intersect_layout_tiles(self.h, n, log_b, C.c_void_p(data), C.c_void_p(ids),
+                                               C.c_void_p(boff), C.c_void_p(bstart), blk0,
+                                               C.c_void_p(tiles) if tiles else None, tile_begin, tile_end,
+                                               1 if packed else 0, C.c_void_p(out)))
 
     def set_intersect_kernel(self, kind):
         """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL / _POSTINGS / _RANGE (sks.h); all give identical counts."""

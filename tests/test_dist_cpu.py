@@ -253,96 +253,99 @@ def _np_layout(sketches, log_b):
             torch.tensor(boff, dtype=torch.int32), as_t(bstart, torch.int64), mx)
 
 
-def _np_count_layout(n, log_b, data, ids, boff, bstart, t0, t1, out):
-    """Counts from a gathered layout (decodes block k's sketches by id)."""
-    out.zero_()
+def _np_count_tiles_layout(n, log_b, lay, blk0, tiles, out):
+    """The contract of sks_intersect_layout_tiles (packed, counts added), from a
+    layout whose block 0 is global block blk0 (decodes block k's sketches by id)."""
+    data, ids, boff, bstart = lay
     B1 = (1 << log_b) + 1
     d = data.numpy().view(np.uint64)
 
     def sketches_of(k):
-        a = int(bstart[k])
-        e = a + int(boff[k * B1 + B1 - 1])
+        kk = k - blk0
+        a = int(bstart[kk])
+        e = a + int(boff[kk * B1 + B1 - 1])
         vals, sl = d[a:e], ids[a:e].numpy()
         return [np.sort(vals[sl == i]) for i in range(64)]
-    for t in range(t0, t1):
-        I, J = sks_dist.sym_tile_coords(t, n)
+    for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
         ri, cj = sketches_of(I), sketches_of(J)
         for a in range(64):
             for b in range(64):
                 i, j = I * 64 + a, J * 64 + b
                 if i < n and j < n:
-                    c = np.intersect1d(ri[a], cj[b], assume_unique=True).size
-                    out[i, j] = c
-                    out[j, i] = c
+                    out[t, a, b] += np.intersect1d(ri[a], cj[b], assume_unique=True).size
 
 
-def _join_worker(rank, world, port, q, capacity, max_log_b, exact=False):
+def _join_worker(rank, world, port, q, dst, n_genomes):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    sk = [s.astype(np.uint64) for s in _sketches()]
-    _, g0, g1 = sks_dist.block_shard(N_GENOMES, world, rank)
+    sk = [s.astype(np.uint64) for s in (_sketches() if n_genomes == N_GENOMES else _sketches_200())]
+    _, g0, g1 = sks_dist.block_shard(n_genomes, world, rank)
     mine = sk[g0:g1]
-    built = []
+    built, calls = [], []
 
     def build(lb, pad):
-        built.append(lb)
-        d, i, b, s, mx = _np_layout(mine, lb)
+        built.append((lb, pad))
+        d, i, b, s, _ = _np_layout(mine, lb)
+        if pad is None:
+            return d, i, b, s
         cap_e, bpr = pad  # the padded send-buffer shape all_vs_all_join gathers
         assert d.numel() <= cap_e and b.numel() <= bpr * ((1 << lb) + 1)
-        if exact:  # the largest rank's element total, not bpr * 64 * largest sketch
-            totals = [sum(len(x) for x in sk[sks_dist.block_shard(N_GENOMES, world, q)[1]:
-                                             sks_dist.block_shard(N_GENOMES, world, q)[2]])
-                      for q in range(world)]
-            assert cap_e == max(totals), (cap_e, totals)
+        totals = [sum(len(x) for x in sk[sks_dist.block_shard(n_genomes, world, r)[1]:
+                                         sks_dist.block_shard(n_genomes, world, r)[2]]) for r in range(world)]
+        assert cap_e == max(max(totals), 1), (cap_e, totals)  # the largest rank's total, exactly
         pd = torch.full((cap_e,), -7, dtype=torch.int64)
         pi = torch.full((cap_e,), 99, dtype=torch.uint8)
         pb = torch.full((bpr * ((1 << lb) + 1),), -3, dtype=torch.int32)
         ps = torch.full((bpr + 1,), -5, dtype=torch.int64)  # junk past the own blocks
         pd[:d.numel()], pi[:i.numel()], pb[:b.numel()], ps[:s.numel()] = d, i, b, s
-        return pd, pi, pb, ps, mx
+        return pd, pi, pb, ps
+
+    def count(n, lb, lay, blk0, tiles, out):
+        calls.append((blk0, len(tiles)))
+        _np_count_tiles_layout(n, lb, lay, blk0, tiles, out)
     mat = sks_dist.all_vs_all_join(
-        N_GENOMES, world, rank, max((len(s) for s in mine), default=0),
-        lambda m: 1 if capacity < 100 else 3, capacity=capacity, build=build,
-        count=_np_count_layout, max_log_b=max_log_b,
-        local_total=sum(len(s) for s in mine) if exact else None)
-    q.put((rank, mat.numpy(), built))
+        n_genomes, world, rank, max((len(s) for s in mine), default=0), sum(len(s) for s in mine),
+        lambda m: 3, build, count, dst=dst)
+    q.put((rank, None if mat is None else mat.numpy(), built, calls))
     dist.destroy_process_group()
 
 
-# (capacity, max_log_b): a table that holds everything (no bucket search), and
-# a tiny one that walks log_b 1 -> max_log_b and then counts with block-buckets
-# still above capacity (the kernel's sub-chunk case; counts must stay exact)
-@pytest.mark.parametrize("world,capacity,max_log_b,exact", [(2, 10**9, 14, False), (3, 10**9, 14, False),
-                                                           (2, 20, 4, False), (2, 10**9, 14, True),
-                                                           (3, 10**9, 14, True)])
-def test_all_vs_all_join_layout_gather_gloo(world, capacity, max_log_b, exact):
-    """Ranks build layouts of their own block-aligned genomes, all-gather them and
-    count their tile share: every rank ends with the single-process matrix.
-    exact: the send buffers are padded to the largest rank's element total
-    (sketch sizes here vary 100-300 per genome and the last rank is short)."""
+@pytest.mark.parametrize("world,dst,n_genomes", [(2, 0, N_GENOMES), (3, None, N_GENOMES), (2, 1, 200),
+                                                 (3, 0, 200)])
+def test_all_vs_all_join_layout_gather_gloo(world, dst, n_genomes):
+    """Ranks build layouts of their own block-aligned genomes into send buffers
+    padded to the largest rank's element total, count their own blocks' tiles
+    on their own layout (first call, blk0 = their first block) while the layouts
+    are gathered, then their share of the cross-rank tiles on the gathered
+    layout; the packed tiles go to dst (every rank for None), whose matrix equals
+    the single-process merge counts; the others return None.  n = 200 at world 3
+    leaves the last rank without genomes."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, capacity, max_log_b, exact))
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes))
              for r in range(world)]
     for p in procs:
         p.start()
-    results = {r: (m, b) for r, m, b in (q.get(timeout=240) for _ in range(world))}
+    results = {r: (m, b, c) for r, m, b, c in (q.get(timeout=300) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    sk = _sketches()
-    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(N_GENOMES)]
-                     for i in range(N_GENOMES)])
+    sk = _sketches() if n_genomes == N_GENOMES else _sketches_200()
+    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(n_genomes)]
+                     for i in range(n_genomes)])
     for r in range(world):
-        assert np.array_equal(results[r][0], want)
-        # every rank walks the same log_b sequence (the check is all-reduced)
-        assert results[r][1] == results[0][1]
-    if capacity < 100:
-        assert results[0][1] == list(range(1, max_log_b + 1))
-    else:
-        assert results[0][1] == [3]
+        mat, built, calls = results[r]
+        if dst is None or r == dst:
+            assert np.array_equal(mat, want), r
+        else:
+            assert mat is None
+        assert [lb for lb, _ in built] == [3]
+        loc, rem = sks_dist.tile_plan(n_genomes, world, r)
+        _, g0, _ = sks_dist.block_shard(n_genomes, world, r)
+        expect = ([(g0 // 64, len(loc))] if len(loc) else []) + ([(0, len(rem))] if len(rem) else [])
+        assert calls == expect, (r, calls)
 
 
 def test_block_shard_covers_whole_blocks():
@@ -414,91 +417,20 @@ def test_one_genome_sharded_gloo(world, w, k):
         assert np.array_equal(got, want if w > 32 else want[:, 0]) and n == nw
 
 
-# ---- all_vs_all_ranged: local tiles before the gather, packed tiles to one rank ----------
-N_RANGED = 200  # four tile blocks, ragged; at world 3 the last rank holds no genome
+# ---- tile plan of all_vs_all_join ------------------------------------------------------------
+N_200 = 200  # four tile blocks, ragged; at world 3 the last rank holds no genome
 
 
-def _ranged_sketches():
+def _sketches_200():
     m = O.mask(21, 21, 0)
     out = []
-    for g in range(N_RANGED):
+    for g in range(N_200):
         seq = synth.bases(4000, seed=70 + g % 5, mut_seed=900 + g, mut_rate=0.003 * (g % 7))
         sk, _ = O.sketch(O.cut_runs(seq.tobytes()), 21, m, "bottom", 150 + (g % 3) * 40)
         out.append(np.sort(sk[:, 0].astype(np.int64)))
-    if N_RANGED > 77:
+    if N_200 > 77:
         out[77] = out[77][:0]  # an empty sketch
     return out
-
-
-def _np_count_tiles(data, starts, sizes, n, log_b, tiles, out):
-    """The tile contract of sks_intersect_range (packed, counts added) by merge."""
-    data, starts, sizes = data.numpy(), starts.numpy(), sizes.numpy()
-    sk = [data[starts[i]:starts[i] + sizes[i]] for i in range(n)]
-    for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
-        for r in range(64):
-            i = I * 64 + r
-            if i >= n:
-                break
-            for c in range(64):
-                j = J * 64 + c
-                if j >= n:
-                    break
-                out[t, r, c] += len(np.intersect1d(sk[i], sk[j], assume_unique=True))
-
-
-def _ranged_worker(rank, world, port, q, dst):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    sk = _ranged_sketches()
-    _, g0, g1 = sks_dist.block_shard(N_RANGED, world, rank)
-    mine = sk[g0:g1]
-    sizes = torch.tensor([len(s) for s in mine], dtype=torch.int32)
-    starts = torch.zeros(len(mine), dtype=torch.int64)
-    if len(mine):
-        starts[1:] = torch.cumsum(sizes.to(torch.int64), 0)[:-1]
-    data = torch.from_numpy(np.concatenate(mine)) if mine else torch.zeros(0, dtype=torch.int64)
-    calls = []
-
-    def count(d, st, sz, n, log_b, tiles, out):
-        calls.append((n, len(tiles)))
-        _np_count_tiles(d, st, sz, n, log_b, tiles, out)
-    mx = max((len(s) for s in mine), default=0)
-    mat = sks_dist.all_vs_all_ranged(N_RANGED, world, rank, data, starts, sizes, mx, count, dst=dst)
-    q.put((rank, None if mat is None else mat.numpy(), calls))
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world,dst", [(2, 0), (3, 1), (3, None)])
-def test_all_vs_all_ranged_gloo(world, dst):
-    """Each rank counts its own blocks' tiles from its own sketches (first call,
-    n = its genome count), then its share of the cross-rank tiles over the
-    gathered sketches; the packed tiles go to `dst` (every rank for None), whose
-    matrix equals the single-process merge counts; the others return None."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_ranged_worker, args=(r, world, port, q, dst)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = {r: (m, c) for r, m, c in (q.get(timeout=240) for _ in range(world))}
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    sk = _ranged_sketches()
-    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(N_RANGED)]
-                     for i in range(N_RANGED)])
-    for r in range(world):
-        mat, calls = results[r]
-        if dst is None or r == dst:
-            assert np.array_equal(mat, want), r
-        else:
-            assert mat is None
-        loc, rem = sks_dist.tile_plan(N_RANGED, world, r)
-        _, g0, g1 = sks_dist.block_shard(N_RANGED, world, r)
-        expect = ([(g1 - g0, len(loc))] if len(loc) else []) + ([(world * sks_dist.block_shard(
-            N_RANGED, world, r)[0] * 64, len(rem))] if len(rem) else [])
-        assert calls == expect, (r, calls)
 
 
 @pytest.mark.parametrize("n,world", [(1000, 8), (1000, 3), (200, 3), (64, 2), (1, 4), (5000, 7)])

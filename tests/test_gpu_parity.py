@@ -864,3 +864,51 @@ def test_range_join_tile_lists_and_packed(torch_cuda, ctx):
                         dense.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dense.cpu(), ref)
+
+
+def test_join_layout_tiles_block_offset_and_packed(torch_cuda, ctx):
+    """sks_intersect_layout_tiles on the layout of a rank's own blocks (global
+    blocks 1-3 of 200 sketches, built from the sketch range 64..199, blk0 = 1)
+    with a tile list and packed output, and on the whole layout into the dense
+    matrix: equal to sks_intersect_sym's merge-tile counts."""
+    torch = torch_cuda
+    n = 200
+    genomes = [synth.bases(12000, seed=80 + i % 5, mut_seed=600 + i, mut_rate=0.005 * (i % 7)).tobytes()
+               for i in range(n)]
+    m = O.mask(31, 21, 6)
+    ss, _dev = build(torch, ctx, genomes, 31, m, "bottom", 500)
+    d, st, sz = ss.device_ptrs()
+    ref = torch.zeros((n, n), dtype=torch.int32, device="cuda")
+    ctx.set_intersect_kernel(sksffi.INTERSECT_MERGE)
+    ctx.intersect_sym(d, st, sz, 1, n, 0, sksffi.intersect_sym_tiles(n), ref.data_ptr())
+    ctx.set_intersect_kernel(sksffi.INTERSECT_AUTO)
+    torch.cuda.synchronize()
+    ref = ref.cpu()
+    sizes = ss.sizes().astype(np.int64)
+    log_b = sksffi.join_layout_log_b(int(sizes.max()))
+    B1 = (1 << log_b) + 1
+
+    def layout(first, cnt):
+        tot = int(sizes[first:first + cnt].sum())
+        nb = (cnt + 63) // 64
+        lay = (torch.empty(tot, dtype=torch.int64, device="cuda"), torch.empty(tot, dtype=torch.uint8, device="cuda"),
+               torch.zeros(nb * B1, dtype=torch.int32, device="cuda"), torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
+        ctx.join_layout_build(d, st + 8 * first, sz + 4 * first, cnt, log_b, *(t.data_ptr() for t in lay), stat=False)
+        return lay
+    own = layout(64, n - 64)
+    tiles = [(1, 1), (1, 3), (3, 3), (2, 3), (1, 2), (2, 2)]
+    tl = torch.tensor(tiles, dtype=torch.int32, device="cuda")
+    packed = torch.zeros((len(tiles), 64, 64), dtype=torch.int32, device="cuda")
+    ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in own), 1, tl.data_ptr(), 0, len(tiles), True,
+                               packed.data_ptr())
+    whole = layout(0, n)
+    dense = torch.zeros((n, n), dtype=torch.int32, device="cuda")
+    ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in whole), 0, 0, 0, sksffi.intersect_sym_tiles(n),
+                               False, dense.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dense.cpu(), ref)
+    pk = packed.cpu()
+    for t, (I, J) in enumerate(tiles):
+        blk = ref[I * 64:I * 64 + 64, J * 64:J * 64 + 64]
+        assert torch.equal(pk[t, :blk.shape[0], :blk.shape[1]], blk), (I, J)
+        assert int(pk[t].sum()) == int(blk.sum())

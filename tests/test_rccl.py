@@ -68,16 +68,21 @@ def _merge_counts(sk):
                      for i in range(n)], dtype=np.int64)
 
 
-def test_join_layout_all_vs_all_on_rccl(env):
-    """sks_dist.all_vs_all_join through the collective branch: the capacity check
-    and layout size (all_reduce MAX), the padded layout gather (int64 data, uint8
-    ids, int32 bucket / block starts in one all_gather_into_tensor each, queued
-    together) and the count all_reduce — 130 genomes (3 blocks, a ragged last
-    one), with and without the build's block-bucket read-back."""
+@pytest.mark.parametrize("side_stream", [False, True])
+def test_join_layout_all_vs_all_on_rccl(env, side_stream):
+    """sks_dist.all_vs_all_join through the collective branch on RCCL: the
+    all_reduce MAX of (largest sketch, element total), the padded layout gathers
+    (int64 data, uint8 ids, int32 bucket starts, int64 block starts), queued on
+    the collective stream while the rank's own tiles are counted, the packed
+    tile gather to rank 0 (dist.gather) and the matrix assembly — 130 genomes
+    (3 blocks, a ragged last one, an empty sketch).  With side_stream the
+    context's kernels run on a non-default HIP stream: join_layout_fns orders it
+    against torch's stream both ways."""
     torch, dist, ctx = env
     import sks_dist
     n, s = 130, 600
     genomes = _family(n, 30_000, 9)
+    genomes[40] = b""
     d, seg = _upload(torch, genomes)
     mask = sksffi.mask_generate(W, K, 0)
     ss = ctx.sketch_build(d.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, s)
@@ -87,15 +92,17 @@ def test_join_layout_all_vs_all_on_rccl(env):
         want, _ = O.sketch(O.cut_runs(genomes[g]), W, mask, "bottom", s)
         assert np.array_equal(ss.sketch(g), want)
     want = _merge_counts(sk)
-    assert want[0, 9] > 0
-    for stat in (True, False):
-        build, count = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda", stat=stat)
-        out = torch.full((n, n), -5, dtype=torch.int32, device="cuda")
-        mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), sksffi.join_layout_log_b,
-                                       sksffi.join_layout_capacity(), build, count,
-                                       device="cuda", out=out)
-        torch.cuda.synchronize()
-        assert np.array_equal(mat.cpu().numpy().astype(np.int64), want), stat
+    assert want[0, 9] > 0 and want[40].sum() == 0
+    stream = torch.cuda.Stream() if side_stream else None
+    cctx = sksffi.Context(0, stream.cuda_stream) if side_stream else ctx
+    build, count = sks_dist.join_layout_fns(cctx, ss, sizes, device="cuda")
+    out = torch.full((n, n), -5, dtype=torch.int32, device="cuda")
+    mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), int(sizes.astype(np.int64).sum()),
+                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out)
+    torch.cuda.synchronize()
+    assert np.array_equal(mat.cpu().numpy().astype(np.int64), want), side_stream
+    if side_stream:
+        cctx.close()
 
 
 def test_padded_sketch_all_vs_all_and_rows_on_rccl(env):
@@ -205,34 +212,3 @@ def test_seed_sweep_on_rccl(env):
     assert mine == list(range(seeds)) and cons.is_cuda
     want = sum(per_seed) / seeds
     assert np.allclose(cons.cpu().numpy(), want, rtol=0, atol=1e-15)
-
-
-@pytest.mark.parametrize("side_stream", [False, True])
-def test_ranged_all_vs_all_on_rccl(env, side_stream):
-    """sks_dist.all_vs_all_ranged through the collective branch on RCCL: the
-    scalar all_reduce MAX, the three async sketch gathers (int64 values, int64
-    starts, int32 sizes) with the local tiles counted while they run, the packed
-    tile gather to rank 0 (dist.gather) and the matrix assembly — 130 genomes,
-    a ragged last block, one empty sketch.  With side_stream the context's
-    kernels run on a non-default HIP stream: range_count_fn orders it against
-    torch's stream both ways."""
-    torch, dist, ctx = env
-    import sks_dist
-    n, s = 130, 500
-    genomes = _family(n, 25_000, 7)
-    genomes[40] = b""
-    d, seg = _upload(torch, genomes)
-    mask = sksffi.mask_generate(W, K, 2)
-    ss = ctx.sketch_build(d.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, s)
-    sk = [ss.sketch(i)[:, 0].copy() for i in range(n)]
-    want = _merge_counts(sk)
-    assert want[0, 7] > 0 and want[40].sum() == 0
-    stream = torch.cuda.Stream() if side_stream else None
-    cctx = sksffi.Context(0, stream.cuda_stream) if side_stream else ctx
-    data, starts, sizes = ss.device_tensors()
-    mat = sks_dist.all_vs_all_ranged(n, 1, 0, data, starts, sizes, int(ss.sizes().max()),
-                                     sks_dist.range_count_fn(cctx), device="cuda", dst=0)
-    torch.cuda.synchronize()
-    assert np.array_equal(mat.cpu().numpy().astype(np.int64), want)
-    if side_stream:
-        cctx.close()
