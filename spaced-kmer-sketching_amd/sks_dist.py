@@ -10,6 +10,8 @@ pairs (kmer_set.cpp:179) inside one process.  Here:
 The functions take the count kernel as a callable so the same orchestration is
 exercised on CPU with gloo in tests/test_dist_cpu.py.
 """
+import functools
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -183,6 +185,7 @@ def _ctx_torch_stream(ctx):
     return torch.cuda.default_stream() if h == 0 else torch.cuda.ExternalStream(h)
 
 
+@functools.lru_cache(maxsize=64)
 def tile_plan(n_genomes, world, rank):
     """(local, remote) int64 arrays [T, 2] of the upper-triangle tiles (I, J) that
     `rank` counts.  local: both blocks in the rank's own block range
@@ -213,7 +216,10 @@ def tile_plan(n_genomes, world, rank):
         pairs = np.stack([I.reshape(-1), J.reshape(-1)], axis=1)
         h = (len(pairs) + 1) // 2
         remote.append(pairs[:h] if rank == a else pairs[h:])
-    return local.reshape(-1, 2), np.concatenate(remote).reshape(-1, 2)
+    local, remote = local.reshape(-1, 2), np.concatenate(remote).reshape(-1, 2)
+    local.flags.writeable = False  # cached: shared by every caller
+    remote.flags.writeable = False
+    return local, remote
 
 
 def _max_over_many(xs, world, device):
