@@ -727,10 +727,11 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         # layouts of this rank's blocks, built into send buffers padded to the
         # largest rank's total; the rank's own tiles counted while the layouts
         # are all-gathered, then its cross-rank tiles; packed tiles to rank 0
-        build, count = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs)
+        build, count, bounds = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs)
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max,
                                        int(local_sizes.astype(np.int64).sum()), sksffi.join_layout_log_b,
-                                       build, count, device=dev, out=mat if dev == "cuda" else None, dst=0)
+                                       build, count, device=dev, out=mat if dev == "cuda" else None, dst=0,
+                                       bounds=bounds)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ts, tp = max_over_ranks(t1 - t0, world), max_over_ranks(t2 - t1, world)

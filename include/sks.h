@@ -249,28 +249,40 @@ int sks_sketch_union_wide(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64
 /* ---- join layout: all-vs-all across GPUs ------------------------------------------------
  * The all-pairs join kernel (sks_intersect_all / _sym, SKS_INTERSECT_JOIN) reads
  * a "join layout": blocks of 64 consecutive sketches, their u64 elements
- * hash-bucketed into 2^log_b buckets and stored block-major.  Exposing it lets a
- * multi-GPU caller build the layout of its own sketches only and all-gather
- * layouts instead of raw sketches (no replicated build):
+ * bucketed into 2^log_b buckets and stored block-major.  Buckets are two-level:
+ * G = sks_join_layout_groups(log_b) value groups cut by bounds u64[G + 1]
+ * (non-decreasing, bounds[0] = 0, bounds[G] = 2^64 - 1), each split into 16 (or
+ * 2^log_b when log_b < 4) hash buckets.  Exposing the layout lets a multi-GPU
+ * caller build the layout of its own sketches only and all-gather layouts
+ * instead of raw sketches (no replicated build):
  *   data   u64[total]            elements, block-major (total = sum of sizes)
  *   ids    u8[total]             slot of each element's sketch in its block
  *   boff   u32[nb * (2^log_b+1)] bucket starts inside each block (nb = ceil(n/64))
  *   bstart u64[nb + 1]           first element of each block in data/ids; [nb] = total
  * Layouts of consecutive sketch ranges that each start at a multiple of 64 can
- * be concatenated: append data/ids/boff and add the data offset to bstart. */
+ * be concatenated (append data/ids/boff and add the data offset to bstart) when
+ * they were built with the same bounds. */
 /* log_b for a largest sketch of max_sketch_size elements (all ranks must agree). */
 uint32_t sks_join_layout_log_b(uint32_t max_sketch_size);
 /* Block-bucket population one join chunk holds; larger buckets are joined in
- * sub-chunks (exact, slower), so a caller may raise log_b while the largest
- * block-bucket exceeds it. */
+ * sub-chunks (exact, slower). */
 uint32_t sks_join_layout_capacity(void);
+/* Value groups of a layout with 2^log_b buckets (bounds hold groups + 1 words). */
+uint32_t sks_join_layout_groups(uint32_t log_b);
+/* Group bounds balanced for the set (quantiles averaged over up to 64 sample
+ * sketches), queued on the context stream.  Any bounds give exact counts. */
+int sks_join_layout_bounds(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
+                           const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_bounds);
 /* Builds the layout of sketches (d_data, d_starts, d_sizes)[0, n) (u64 elements)
- * into caller buffers; *max_block_bucket (host) receives the largest
- * block-bucket population (waits for the build); NULL skips that read-back. */
+ * into caller buffers (two launches).  d_bounds: the group bounds (NULL: the
+ * set's own, sks_join_layout_bounds).  *max_block_bucket (host) receives the
+ * largest block-bucket population (waits for the build); NULL skips that
+ * read-back.  total_hint: the n sizes' sum when the caller knows it (the build
+ * then never waits for the stream), UINT64_MAX to have the sizes read back. */
 int sks_join_layout_build(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
-                          const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_out_data,
-                          uint8_t* d_out_ids, uint32_t* d_out_boff, uint64_t* d_out_bstart,
-                          uint32_t* max_block_bucket);
+                          const uint32_t* d_sizes, uint32_t n, uint64_t total_hint, uint32_t log_b,
+                          const uint64_t* d_bounds, uint64_t* d_out_data, uint8_t* d_out_ids,
+                          uint32_t* d_out_boff, uint64_t* d_out_bstart, uint32_t* max_block_bucket);
 /* sks_intersect_sym over a join layout of n sketches: upper-triangle 64x64 tiles
  * [tile_begin, tile_end) into the n x n int32 matrix d_out (zeroed first). */
 int sks_intersect_sym_layout(sks_ctx* ctx, uint32_t n, uint32_t log_b, const uint64_t* d_data,

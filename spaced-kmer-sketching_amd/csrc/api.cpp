@@ -1481,33 +1481,48 @@ int sks_sketch_union_wide(sks_ctx* c, const uint64_t* d_in, uint64_t n, uint64_t
 uint32_t sks_join_layout_log_b(uint32_t max_sketch_size) { return sks::join_log_b(max_sketch_size); }
 uint32_t sks_join_layout_capacity(void) { return sks::join_cap(); }
 
+int sks_join_layout_bounds(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
+                           const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_bounds) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds: null ctx");
+  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds: log_b > 14");
+  if (!d_bounds || (n && (!d_starts || !d_sizes))) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::join_layout_bounds(d_data, d_starts, d_sizes, n, log_b, d_bounds, c->stream));
+  return SKS_OK;
+}
+
+uint32_t sks_join_layout_groups(uint32_t log_b) { return sks::join_layout_groups(log_b); }
+
 int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
-                          const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_out_data,
-                          uint8_t* d_out_ids, uint32_t* d_out_boff, uint64_t* d_out_bstart,
-                          uint32_t* max_block_bucket) {
+                          const uint32_t* d_sizes, uint32_t n, uint64_t total_hint, uint32_t log_b,
+                          const uint64_t* d_bounds, uint64_t* d_out_data, uint8_t* d_out_ids,
+                          uint32_t* d_out_boff, uint64_t* d_out_bstart, uint32_t* max_block_bucket) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_join_layout_build: null ctx");
   if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_join_layout_build: log_b > 14");
   if (!d_out_bstart || (n && (!d_starts || !d_sizes || !d_out_boff)))
     return sks::fail(SKS_E_ARG, "sks_join_layout_build: null argument");
   DeviceGuard g(c->device);
-  uint64_t total = 0;
-  if (n) {  // bucket starts are u32: the layout must hold < 2^32 elements
+  uint64_t total = total_hint;
+  if (n && total == UINT64_MAX) {  // unknown: read the sizes back (waits for the stream)
     std::vector<uint32_t> h_sizes(n);
     SKS_HIP(sks::pinned_d2h(h_sizes.data(), d_sizes, n * sizeof(uint32_t), c->stream));
+    total = 0;
     for (uint32_t v : h_sizes) total += v;
-    if (total >= (1ull << 32))
-      return sks::fail(SKS_E_UNSUPPORTED, "sks_join_layout_build: >= 2^32 elements in one layout");
   }
-  const size_t tmp = sks::join_layout_temp_bytes(n, log_b, total);
-  SKS_HIP(c->iwork.reserve(tmp + 64));
+  if (!n) total = 0;
+  // bucket starts are u32: the layout must hold < 2^32 elements
+  if (total >= (1ull << 32))
+    return sks::fail(SKS_E_UNSUPPORTED, "sks_join_layout_build: >= 2^32 elements in one layout");
+  const size_t o_stat = (sks::join_layout_temp_bytes(n, log_b) + 15) & ~(size_t)15;
+  SKS_HIP(c->iwork.reserve(o_stat + 16));
   char* w = static_cast<char*>(c->iwork.ptr);
-  uint32_t* stat = reinterpret_cast<uint32_t*>(w + ((tmp + 15) & ~(size_t)15));
+  uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
   SKS_HIP(hipMemsetAsync(stat, 0, 4, c->stream));
   if (n == 0) {
     SKS_HIP(hipMemsetAsync(d_out_bstart, 0, 8, c->stream));
   } else {
-    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, 0, n, total, log_b, d_out_data,
-                                   d_out_ids, d_out_boff, d_out_bstart, stat, w, tmp, c->stream));
+    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, d_bounds, w, d_out_data, d_out_ids,
+                                   d_out_boff, d_out_bstart, stat, c->stream));
   }
   if (max_block_bucket) {  // NULL: no read-back, the call does not wait for the build
     uint32_t h = 0;

@@ -30,6 +30,7 @@ namespace {
 
 using jc::fp_slot;
 using jc::fp_tag;
+using jc::join_chain;
 using jc::kFFree;
 using jc::kFLog;
 using jc::kFSlots;
@@ -682,7 +683,7 @@ __device__ unsigned long long g_join_stamps[8];
 // a probe reads 32-bit slots and, on a fingerprint match, the 16-byte entry.
 // Values need no reserved "empty" key (the empty marker lives in the slot), and
 // the entries need no reset: the next chunk's staging overwrites them.
-static_assert(kJCap <= 1024, "entry index must fit 10 bits");
+static_assert(kJCap == 1024, "entry index: 10 bits; join_chain reads entry x & 1023 of any slot word");
 
 __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
 #ifdef SKS_JOIN_STAMPS
@@ -748,16 +749,8 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   };
   // columns holding v (0 if none)
   auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
-    const uint32_t tag = fp_tag(v);
-    for (;;) {
-      if (x == kFFree) return 0ull;
-      if ((x >> 10) == tag) {
-        const ulonglong2 e = s_ent[x & 1023u];
-        if (e.x == v) return e.y;
-      }
-      h = (h + 1) & (kFSlots - 1);
-      x = s_slot[h];
-    }
+    if (x != kFFree) x = join_chain(x, h, fp_tag(v), v, 0u, s_slot, s_ent, false);
+    return x == kFFree ? 0ull : s_ent[x & 1023u].y;
   };
 
   uint32_t diag_acc = 0;  // SKS_JOIN_DIAG & 4: hits counted, not added
@@ -847,19 +840,13 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
         const uint64_t v = cur.cv[u];
         const uint32_t e = tid + kJB * u;
         uint32_t h = hs[u], x = prev[u];
-        for (;;) {
-          if (x == kFFree) {
-            made[u] = h;
-            ent[u] = e;
-            break;
-          }
-          if ((x >> 10) == tags[u] && s_ent[x & 1023u].x == v) {
-            atomicOr(&s_ent[x & 1023u].y, 1ull << cur.cid[u]);
-            ent[u] = x & 1023u;
-            break;
-          }
-          h = (h + 1) & (kFSlots - 1);
-          x = atomicCAS(&s_slot[h], kFFree, (tags[u] << 10) | e);
+        if (x != kFFree) x = join_chain(x, h, tags[u], v, (tags[u] << 10) | e, s_slot, s_ent, true);
+        if (x == kFFree) {  // created slot h naming entry e
+          made[u] = h;
+          ent[u] = e;
+        } else {  // v is present: add the column bit to its entry
+          ent[u] = x & 1023u;
+          atomicOr(&s_ent[ent[u]].y, 1ull << cur.cid[u]);
         }
       }
       __syncthreads();
@@ -873,6 +860,13 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
           const uint32_t r = cur.cid[u];
           if (hs[u] == kNoSlot || r >= r_valid) continue;
           const unsigned long long m = s_ent[ent[u]].y;
+#ifdef SKS_JOIN_CHECK  // diagnostic build: an element's entry holds its value and its column bit
+          if (s_ent[ent[u]].x != cur.cv[u] || !((m >> r) & 1ull))
+            printf("join check: tile %u,%u buckets [%u,%u) cols [%u,%u) e=%u ent=%u v=%llx entv=%llx m=%llx r=%u "
+                   "slot=%u made=%u prev=%x\n", I, J, bs, be, cs, ce, (uint32_t)(tid + kJB * u), ent[u],
+                   (unsigned long long)cur.cv[u], (unsigned long long)s_ent[ent[u]].x, m, r, hs[u], made[u],
+                   prev[u]);
+#endif
           if (SKS_JOIN_DIAG & 1) continue;
           if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
           add_hits(r, m);
@@ -1028,7 +1022,7 @@ static size_t layout_head_bytes(uint64_t len, uint64_t cells, uint64_t glen, uin
   return u32s + ((std::max<uint64_t>(total, 1) * 8 + 15) & ~(size_t)15);
 }
 
-size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total) {
+size_t join_layout_hash_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total) {
   const uint64_t n_blk = (count + kTile - 1) / kTile;
   const uint64_t cells = n_blk * (1ull << log_b), len = cells * 64;
   const uint64_t glen = n_blk * 64 * (1ull << layout_log_g(log_b));
@@ -1038,8 +1032,8 @@ size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total) {
   return layout_head_bytes(len, cells, glen, total) + scan + 16;
 }
 
-hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                             uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
+hipError_t join_layout_build_hash(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                                  uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
                              uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
                              uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
                              hipStream_t s) {
@@ -1299,7 +1293,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   // the join's per-(block, bucket, slot) counting arrays take 8 B x 64 x B per
   // block; beyond a few GB of them (very many sketches) the merge tiles are used
   const bool join_fits = total < (1ull << 32) &&
-                         join_layout_temp_bytes(n, join_log_b(max_size), total) < (8ull << 30);
+                         join_layout_hash_temp_bytes(n, join_log_b(max_size), total) < (8ull << 30);
   if (algo != kIntersectMerge && join_fits) {
     // hash-bucketed block-major copy of the column sketches (and of the row
     // range when its blocks are not aligned with the column blocks), then k_join
@@ -1311,8 +1305,10 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     uint32_t log_b = join_log_b(max_size);
     for (;;) {
       const uint32_t B = 1u << log_b;
-      const size_t tmp_c = join_layout_temp_bytes(n, log_b, total);
-      const size_t tmp_r = sep_rows ? join_layout_temp_bytes(rn, log_b, r_total) : 0;
+      static const bool hash_layout = getenv("SKS_JOIN_HASH_LAYOUT") != nullptr;
+      const size_t tmp_c = hash_layout ? join_layout_hash_temp_bytes(n, log_b, total) : join_layout_temp_bytes(n, log_b);
+      const size_t tmp_r = !sep_rows ? 0 : hash_layout ? join_layout_hash_temp_bytes(rn, log_b, r_total)
+                                                       : join_layout_temp_bytes(rn, log_b);
       size_t o = 0;
       const size_t o_cdat = o; o = align16(o + total * 8);
       const size_t o_cids = o; o = align16(o + total);
@@ -1323,6 +1319,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       const size_t o_rbof = o; o = align16(o + (sep_rows ? (size_t)n_rb * (B + 1) * 4 : 0));
       const size_t o_rbst = o; o = align16(o + (sep_rows ? (size_t)(n_rb + 1) * 8 : 0));
       const size_t o_stat = o; o = align16(o + 16);
+      const size_t o_bnd = o; o = align16(o + (size_t)(B + 1) * 8);
       const size_t o_tmp = o; o = align16(o + std::max(tmp_c, tmp_r));
       if ((e = work.reserve(o)) != hipSuccess) return e;
       char* w = static_cast<char*>(work.ptr);
@@ -1331,11 +1328,20 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       JoinLayout rl = cl;
       uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
       if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
+      // the column and row layouts share the column set's group bounds
+      uint64_t* gbounds = reinterpret_cast<uint64_t*>(w + o_bnd);
+      if (!hash_layout && (e = join_layout_bounds(data, starts, sizes, n, log_b, gbounds, s)) != hipSuccess)
+        return e;
       auto build_layout = [&](uint32_t first, uint32_t cnt, uint64_t tot, const JoinLayout& L,
                               size_t tmp_bytes) -> hipError_t {
-        return join_layout_build(data, starts, sizes, first, cnt, tot, log_b, const_cast<uint64_t*>(L.data),
-                                 const_cast<uint8_t*>(L.ids), const_cast<uint32_t*>(L.boff),
-                                 const_cast<uint64_t*>(L.bstart), stat, w + o_tmp, tmp_bytes, s);
+        if (hash_layout)
+          return join_layout_build_hash(data, starts, sizes, first, cnt, tot, log_b,
+                                        const_cast<uint64_t*>(L.data), const_cast<uint8_t*>(L.ids),
+                                        const_cast<uint32_t*>(L.boff), const_cast<uint64_t*>(L.bstart), stat,
+                                        w + o_tmp, tmp_bytes, s);
+        return join_layout_build(data, starts + first, sizes + first, cnt, log_b, gbounds, w + o_tmp,
+                                 const_cast<uint64_t*>(L.data), const_cast<uint8_t*>(L.ids),
+                                 const_cast<uint32_t*>(L.boff), const_cast<uint64_t*>(L.bstart), stat, s);
       };
       if ((e = build_layout(0, n, total, cl, tmp_c)) != hipSuccess) return e;
       if (sep_rows) {

@@ -28,6 +28,31 @@ __device__ __forceinline__ uint32_t fp_tag(uint64_t v) {  // 22 bits, never all 
   return t == 0x3FFFFFu ? 0x3FFFFEu : t;
 }
 
+// Walks a table's probe chain from the occupied slot word x at index h to the
+// first free slot or the slot naming value v's entry, and returns that word
+// (kFFree: v is absent; with insert, the walk claimed the free slot at h for
+// `word`).  Callers take the entry from the returned word.
+//
+// The loop has ONE exit, its stop test evaluated without short-circuit (the
+// entry x names is read whether or not the tag matches; for a free word that is
+// entry 1023, read and ignored).  Written with two exits (free / match) and the
+// entry index assigned at the match exit, the compiler (ROCm 7.2, gfx950)
+// merged the exits and kept the joined entry in the register of the element's
+// own entry index, updated on every tag match: an element whose chain passed a
+// slot with its tag but another value, and then claimed a free slot, came out
+// naming the other value's entry.  k_join then counted that column element
+// with a foreign mask (about one insert in 10^7; a diagonal count one short,
+// one stray +1; tools/layout_verify.py and tools/join_repeat.py found it).
+__device__ __forceinline__ uint32_t join_chain(uint32_t x, uint32_t& h, uint32_t tag, uint64_t v, uint32_t word,
+                                               uint32_t* s_slot, const ulonglong2* s_ent, bool insert) {
+  for (;;) {
+    const uint64_t ev = s_ent[x & 1023u].x;
+    if ((x == kFFree) | (((x >> 10) == tag) & (ev == v))) return x;
+    h = (h + 1) & (kFSlots - 1);
+    x = insert ? atomicCAS(&s_slot[h], kFFree, word) : s_slot[h];
+  }
+}
+
 // (I, J) of upper-triangle tile t of nb x nb blocks, row-major, I <= J
 __device__ __forceinline__ void sym_tile(uint64_t t, uint32_t nb, uint32_t& I, uint32_t& J) {
   uint32_t i = 0;

@@ -262,18 +262,17 @@ __global__ __launch_bounds__(kPB) void k_pl_place(const uint64_t* __restrict__ s
     if (e >= n) break;
     const uint64_t v = s_val[e];
     uint32_t h = dedupe_home(v) & (TS - 1);
-    for (;;) {
-      const uint32_t x = atomicCAS(&s_tab[h], kEmpty, e);
-      if (x == kEmpty) {
-        own |= 1u << u;
-        break;
-      }
-      if (s_val[x] == v) {
-        atomicOr(&s_msk[x], s_msk[e]);
-        break;
-      }
+    // (the loop carries only h and x; the outcome is taken from x after it —
+    // see k_join's lookup in intersect.hip)
+    uint32_t x = atomicCAS(&s_tab[h], kEmpty, e);
+    while (x != kEmpty && s_val[x] != v) {
       h = (h + 1) & (TS - 1);
+      x = atomicCAS(&s_tab[h], kEmpty, e);
     }
+    if (x == kEmpty)
+      own |= 1u << u;
+    else
+      atomicOr(&s_msk[x], s_msk[e]);
   }
   __syncthreads();
   // 2) postings per bucket of the group
@@ -508,16 +507,13 @@ __global__ __launch_bounds__(kJB) void k_pjoin(PJoinArgs a) {
           if (R && T) {
             const uint32_t tb = s_tb[lb];
             uint32_t p = phome(v, T);
-            for (;;) {
-              const ulonglong2 x = s_tab[tb + p];
-              if (x.y == 0) break;
-              if (x.x == v) {
-                hit = true;
-                C = x.y;
-                break;
-              }
+            ulonglong2 x = s_tab[tb + p];
+            while (x.y != 0 && x.x != v) {
               p = (p + 1 == T) ? 0 : p + 1;
+              x = s_tab[tb + p];
             }
+            hit = x.y != 0;
+            C = x.y;
           }
         }
         append(hit, R, C);

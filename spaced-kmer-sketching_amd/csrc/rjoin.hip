@@ -45,6 +45,7 @@ namespace {
 
 using jc::fp_slot;
 using jc::fp_tag;
+using jc::join_chain;
 using jc::kFFree;
 using jc::kFSlots;
 using jc::sym_tile;
@@ -57,7 +58,7 @@ constexpr int kPlanes = 32;           // bit-sliced counter planes (any int32 co
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr int kPB = 256;              // threads of the prefix kernel
 constexpr uint64_t kMaxGrid = 1ull << 22;
-static_assert(kRCap <= 1024, "entry index must fit 10 bits");
+static_assert(kRCap == 1024, "entry index: 10 bits; join_chain reads entry x & 1023 of any slot word");
 
 // pre[blk * (B + 1) + b] = sum of pos[i * (B + 1) + b] over the block's sketches
 __global__ __launch_bounds__(kPB) void k_rj_prefix(const uint32_t* __restrict__ pos, uint32_t n,
@@ -305,16 +306,8 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
     top = max(top, b);
   };
   auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
-    const uint32_t tag = fp_tag(v);
-    for (;;) {
-      if (x == kFFree) return 0ull;
-      if ((x >> 10) == tag) {
-        const ulonglong2 e = s_ent[x & 1023u];
-        if (e.x == v) return e.y;
-      }
-      h = (h + 1) & (kFSlots - 1);
-      x = s_slot[h];
-    }
+    if (x != kFFree) x = join_chain(x, h, fp_tag(v), v, 0u, s_slot, s_ent, false);
+    return x == kFFree ? 0ull : s_ent[x & 1023u].y;
   };
 
   const int rs_s = tid >> 3, rs_k = tid & 7;  // range map: sketch, lane within it
@@ -349,16 +342,10 @@ __global__ __launch_bounds__(kRB, 6) void k_rjoin(RJoinArgs a) {
   // entry now holding v.
   // resolve an insert whose first compare-swap at slot h returned x
   auto insert_chain = [&](uint64_t v, uint32_t e, uint32_t tag, uint32_t h, uint32_t x) -> uint32_t {
-    const unsigned long long bit = 1ull << rs_s;
-    for (;;) {
-      if (x == kFFree) return e;
-      if ((x >> 10) == tag && s_ent[x & 1023u].x == v) {
-        atomicOr(&s_ent[x & 1023u].y, bit);
-        return x & 1023u;
-      }
-      h = (h + 1) & (kFSlots - 1);
-      x = atomicCAS(&s_slot[h], kFFree, (tag << 10) | e);
-    }
+    if (x != kFFree) x = join_chain(x, h, tag, v, (tag << 10) | e, s_slot, s_ent, true);  // (join_common.hpp)
+    if (x == kFFree) return e;
+    atomicOr(&s_ent[x & 1023u].y, 1ull << rs_s);
+    return x & 1023u;
   };
   int buf = 0;
 

@@ -200,16 +200,29 @@ struct JoinLayout {
 uint32_t join_cap();                       // elements per join chunk (table capacity)
 uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch of max_size
 // total = elements of the `count` sketches (sizes the staging array)
-size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total);
-// Layout of sketches [first, first + count) (total elements) into out_*;
-// out_bstart gets ceil(count/64) + 1 entries (the last = element total);
-// *d_stat is raised to the largest block-bucket population (the join needs it
-// <= join_cap()).
+// Join layout (layout.hip): value groups of 64 hash buckets.  join_layout_groups:
+// G = 2^log_b / 64 (>= 1); bounds u64[G + 1].  join_layout_bounds computes the
+// group bounds of a set (quantiles averaged over up to 64 samples).
+// join_layout_build: the layout of sketches (data, starts, sizes)[0, count)
+// with the caller's bounds, or (d_bounds null) bounds computed from these
+// sketches; temp: join_layout_temp_bytes; *d_stat is raised to the largest
+// block-bucket population.  Three launches, no host synchronisation.
+uint32_t join_layout_groups(uint32_t log_b);
+hipError_t join_layout_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                              uint32_t count, uint32_t log_b, uint64_t* bounds, hipStream_t s);
+size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b);
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                             uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
+                             uint32_t count, uint32_t log_b, const uint64_t* d_bounds, void* temp,
                              uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
-                             uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
-                             hipStream_t s);
+                             uint64_t* out_bstart, uint32_t* d_stat, hipStream_t s);
+// the round-2 all-hash build (intersect.hip k_hb_*): six launches; measured
+// against join_layout_build with SKS_JOIN_HASH_LAYOUT
+size_t join_layout_hash_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total);
+hipError_t join_layout_build_hash(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
+                                  uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
+                                  uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
+                                  uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
+                                  hipStream_t s);
 // Tiles of the n x n (sym: upper-triangle range [tile_begin, tile_end), or
 // with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
 // written) or rows x n matrix; tile (I, J) reads row block r_blk0 + I of

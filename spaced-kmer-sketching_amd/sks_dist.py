@@ -349,13 +349,34 @@ def _gather_many(ts, world):
     return res
 
 
+def _broadcast(t, src, world):
+    if _solo(world):
+        return t
+    if dist.get_backend() == "nccl" or t.device.type == "cpu":
+        dist.broadcast(t, src=src)
+        return t
+    host = t.cpu()
+    dist.broadcast(host, src=src)
+    t.copy_(host)
+    return t
+
+
+def layout_groups(log_b):
+    """Value groups of a join layout with 2^log_b buckets (sks_join_layout_groups)."""
+    return 1 << (log_b - 4) if log_b > 4 else 1
+
+
 def all_vs_all_join(n_genomes, world, rank, local_max_size, local_total, log_b_for, build, count,
-                    device="cpu", out=None, dst=0):
+                    device="cpu", out=None, dst=0, bounds=None):
     """n x n int32 intersection matrix on rank `dst` (None on the others; on
     every rank when dst is None).
 
-    build(log_b, pad) -> (data u64[], ids u8[], boff u32[], bstart u64[]): the
-    join layout of this rank's block-aligned genomes (block_shard).  pad is None
+    build(log_b, pad, bounds) -> (data u64[], ids u8[], boff u32[], bstart u64[]):
+    the join layout of this rank's block-aligned genomes (block_shard), with the
+    value-group bounds `bounds` (an int64 tensor of layout_groups(log_b) + 1
+    words; None: the rank's own).  Layouts joined with each other must share
+    bounds: with a process group, rank 0 computes them (bounds(log_b) -> tensor)
+    and broadcasts them before the builds.  pad is None
     for one rank without a process group; otherwise (cap_e, bpr), and the
     buffers must have exactly cap_e data / id entries, bpr * (B + 1) bucket
     starts and bpr + 1 block starts (entries past the rank's own blocks are never
@@ -379,7 +400,12 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, local_total, log_b_f
     log_b = log_b_for(max(max_all, 1))
     local, remote = tile_plan(n_genomes, world, rank)
     T = len(local) + len(remote)
-    lay = build(log_b, None if solo else (max(1, cap_e), bpr))
+    gb = None
+    if not solo and bounds is not None:
+        gb = bounds(log_b) if rank == 0 else \
+            torch.empty(layout_groups(log_b) + 1, dtype=torch.int64, device=device)
+        gb = _broadcast(gb, 0, world)
+    lay = build(log_b, None if solo else (max(1, cap_e), bpr), gb)
     if solo:
         if out is None:
             out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
@@ -417,7 +443,7 @@ def all_vs_all_join(n_genomes, world, rank, local_max_size, local_total, log_b_f
 
 
 def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
-    """The build / count callables of all_vs_all_join for this rank's sketches
+    """The build / count / bounds callables of all_vs_all_join for this rank's sketches
     on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
     `local_sizes` its sizes (numpy).  build(log_b, pad) runs
     sks_join_layout_build into device buffers (kept in `cache` across calls of
@@ -434,8 +460,17 @@ def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
     tile_cache = cache.setdefault("_tiles", {}) if isinstance(cache, dict) else {}
     keep = {}
 
-    def build(log_b, pad=None):
+    def bounds(log_b):
+        b = torch.empty(layout_groups(log_b) + 1, dtype=torch.int64, device="cuda")
+        _ctx_waits_for_torch(ctx)
+        ctx.join_layout_bounds(data, starts, sizes, n_local, log_b, b.data_ptr())
+        _torch_waits_for_ctx(ctx)
+        keep["bounds"] = b
+        return b.to(device)
+
+    def build(log_b, pad=None, gbounds=None):
         B1 = (1 << log_b) + 1
+        gb = gbounds.to("cuda").contiguous() if gbounds is not None else None
         # padded (all_vs_all_join with a process group): the send buffers
         # themselves, cap_e elements and bpr blocks, gathered as they are
         cap_e, nb = pad if pad is not None else (max(tot, 1), max(nb_local, 1))
@@ -449,8 +484,10 @@ def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
                           torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
         out = cache[key]
         _ctx_waits_for_torch(ctx)  # the buffers' previous readers (gathers, joins)
-        ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out), stat=False)
+        ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out), stat=False,
+                              total=tot, bounds=gb.data_ptr() if gb is not None else None)
         _torch_waits_for_ctx(ctx)
+        keep["gb"] = gb
         return tuple(t.to(device) for t in out)
 
     def count(n, log_b, lay, blk0, tiles, out):
@@ -459,7 +496,7 @@ def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
         if key not in tile_cache:
             if len(tile_cache) > 8:
                 tile_cache.clear()
-            tile_cache[key] = torch.as_tensor(tiles, dtype=torch.int32).reshape(-1, 2).to("cuda").contiguous()
+            tile_cache[key] = torch.from_numpy(np.array(tiles, dtype=np.int32)).reshape(-1, 2).to("cuda").contiguous()
         tl = tile_cache[key]
         tgt = out if out.is_cuda else torch.zeros(out.shape, dtype=out.dtype, device="cuda")
         _ctx_waits_for_torch(ctx)
@@ -469,7 +506,7 @@ def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
         keep["last"] = (lay, tl)  # alive until torch's stream is past the kernel
         if tgt is not out:
             out.copy_(tgt.cpu())
-    return build, count
+    return build, count, bounds
 
 
 # ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------

@@ -61,6 +61,7 @@ EXPORTED = [
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
     "sks_sketch_set_name", "sks_sketch_set_save", "sks_sketch_set_load", "sks_sketch_set_concat",
     "sks_range_log_b", "sks_range_bounds", "sks_intersect_range", "sks_intersect_layout_tiles",
+    "sks_join_layout_bounds", "sks_join_layout_groups",
 ]
 
 _lib = None
@@ -119,8 +120,11 @@ def lib():
     L.sks_join_layout_log_b.restype = C.c_uint32
     L.sks_join_layout_capacity.argtypes = []
     L.sks_join_layout_capacity.restype = C.c_uint32
-    L.sks_join_layout_build.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp,
-                                        C.POINTER(C.c_uint32)]
+    L.sks_join_layout_build.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint64, C.c_uint32, vp, vp, vp,
+                                        vp, vp, C.POINTER(C.c_uint32)]
+    L.sks_join_layout_bounds.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp]
+    L.sks_join_layout_groups.argtypes = [C.c_uint32]
+    L.sks_join_layout_groups.restype = C.c_uint32
     L.sks_intersect_sym_layout.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint64,
                                            C.c_uint64, vp]
     L.sks_intersect_layout_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp,
@@ -213,6 +217,10 @@ def join_layout_log_b(max_sketch_size):
 
 def join_layout_capacity():
     return int(lib().sks_join_layout_capacity())
+
+
+def join_layout_groups(log_b):
+    return int(lib().sks_join_layout_groups(log_b))
 
 
 def range_log_b(max_sketch_size):
@@ -320,15 +328,25 @@ class Context:
         return int(k.value)
 
     def join_layout_build(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_data, out_ids,
-                          out_boff, out_bstart, stat=True):
+                          out_boff, out_bstart, stat=True, total=None, bounds=None):
         """sks_join_layout_build; returns the largest block-bucket population, or
-        None with stat=False (no read-back: the call does not wait for the build)."""
+        None with stat=False (no read-back).  total: the sizes' sum when known
+        (with stat=False the call then does not wait for the stream at all);
+        bounds: device pointer of the group bounds (None: the set's own)."""
         mx = C.c_uint32(0)
         check(lib().sks_join_layout_build(self.h, C.c_void_p(data_ptr), C.c_void_p(starts_ptr),
-                                          C.c_void_p(sizes_ptr), n, log_b, C.c_void_p(out_data),
-                                          C.c_void_p(out_ids), C.c_void_p(out_boff),
+                                          C.c_void_p(sizes_ptr), n,
+                                          (1 << 64) - 1 if total is None else int(total), log_b,
+                                          C.c_void_p(bounds) if bounds else None,
+                                          C.c_void_p(out_data), C.c_void_p(out_ids), C.c_void_p(out_boff),
                                           C.c_void_p(out_bstart), C.byref(mx) if stat else None))
         return mx.value if stat else None
+
+    def join_layout_bounds(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_bounds):
+        """sks_join_layout_bounds: the set's group bounds (device pointer out_bounds,
+        join_layout_groups(log_b) + 1 words)."""
+        check(lib().sks_join_layout_bounds(self.h, C.c_void_p(data_ptr), C.c_void_p(starts_ptr),
+                                           C.c_void_p(sizes_ptr), n, log_b, C.c_void_p(out_bounds)))
 
     def intersect_sym_layout(self, n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out):
         check(lib().sks_intersect_sym_layout(self.h, n, log_b, C.c_void_p(data), C.c_void_p(ids),

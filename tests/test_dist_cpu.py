@@ -284,8 +284,13 @@ def _join_worker(rank, world, port, q, dst, n_genomes):
     mine = sk[g0:g1]
     built, calls = [], []
 
-    def build(lb, pad):
+    def bounds(lb):  # rank 0's bounds are broadcast: rank-specific values show it
+        assert rank == 0
+        return torch.arange(sks_dist.layout_groups(lb) + 1, dtype=torch.int64) * 1000 + 7
+
+    def build(lb, pad, gb):
         built.append((lb, pad))
+        assert torch.equal(gb, bounds.__wrapped__(lb)), gb  # every rank got rank 0's
         d, i, b, s, _ = _np_layout(mine, lb)
         if pad is None:
             return d, i, b, s
@@ -304,9 +309,10 @@ def _join_worker(rank, world, port, q, dst, n_genomes):
     def count(n, lb, lay, blk0, tiles, out):
         calls.append((blk0, len(tiles)))
         _np_count_tiles_layout(n, lb, lay, blk0, tiles, out)
+    bounds.__wrapped__ = lambda lb: torch.arange(sks_dist.layout_groups(lb) + 1, dtype=torch.int64) * 1000 + 7
     mat = sks_dist.all_vs_all_join(
         n_genomes, world, rank, max((len(s) for s in mine), default=0), sum(len(s) for s in mine),
-        lambda m: 3, build, count, dst=dst)
+        lambda m: 3, build, count, dst=dst, bounds=bounds)
     q.put((rank, None if mat is None else mat.numpy(), built, calls))
     dist.destroy_process_group()
 

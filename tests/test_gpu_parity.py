@@ -645,6 +645,12 @@ def test_join_layout_build_and_concat(torch_cuda, ctx):
     B1 = (1 << log_b) + 1
     cap = sksffi.join_layout_capacity()
 
+    # the halves share one set of value-group bounds, as a multi-GPU run's
+    # layouts do (rank 0's, broadcast): here the last 86 sketches' own bounds
+    gb = torch.empty(sksffi.join_layout_groups(log_b) + 1, dtype=torch.int64, device="cuda:0")
+    ctx.join_layout_bounds(d.data_ptr(), st.data_ptr() + 8 * 64, sz.data_ptr() + 4 * 64, n - 64, log_b,
+                           gb.data_ptr())
+
     def build(first, count):
         tot = int(sum(len(s) for s in sk[first:first + count]))
         nb = (count + 63) // 64
@@ -653,7 +659,7 @@ def test_join_layout_build_and_concat(torch_cuda, ctx):
                torch.empty(nb * B1, dtype=torch.int32, device="cuda:0"),
                torch.empty(nb + 1, dtype=torch.int64, device="cuda:0"))
         mx = ctx.join_layout_build(d.data_ptr(), st.data_ptr() + 8 * first, sz.data_ptr() + 4 * first,
-                                   count, log_b, *(t.data_ptr() for t in out))
+                                   count, log_b, *(t.data_ptr() for t in out), bounds=gb.data_ptr())
         assert mx <= cap
         torch.cuda.synchronize()
         assert int(out[3][nb].item()) == tot
@@ -893,8 +899,11 @@ def test_join_layout_tiles_block_offset_and_packed(torch_cuda, ctx):
         nb = (cnt + 63) // 64
         lay = (torch.empty(tot, dtype=torch.int64, device="cuda"), torch.empty(tot, dtype=torch.uint8, device="cuda"),
                torch.zeros(nb * B1, dtype=torch.int32, device="cuda"), torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
-        ctx.join_layout_build(d, st + 8 * first, sz + 4 * first, cnt, log_b, *(t.data_ptr() for t in lay), stat=False)
+        ctx.join_layout_build(d, st + 8 * first, sz + 4 * first, cnt, log_b, *(t.data_ptr() for t in lay),
+                              stat=False, bounds=gb.data_ptr())
         return lay
+    gb = torch.empty(sksffi.join_layout_groups(log_b) + 1, dtype=torch.int64, device="cuda")
+    ctx.join_layout_bounds(d, st, sz, n, log_b, gb.data_ptr())  # shared by both layouts
     own = layout(64, n - 64)
     tiles = [(1, 1), (1, 3), (3, 3), (2, 3), (1, 2), (2, 2)]
     tl = torch.tensor(tiles, dtype=torch.int32, device="cuda")
@@ -912,3 +921,56 @@ def test_join_layout_tiles_block_offset_and_packed(torch_cuda, ctx):
         blk = ref[I * 64:I * 64 + 64, J * 64:J * 64 + 64]
         assert torch.equal(pk[t, :blk.shape[0], :blk.shape[1]], blk), (I, J)
         assert int(pk[t].sum()) == int(blk.sum())
+
+
+@pytest.fixture(scope="module")
+def scale_sets(torch_cuda, ctx):
+    """Config 4's shape at 100 kb genomes: 1000 bottom-10000 sketches of
+    unrelated genomes ("indep") and of 25 mutated families ("family")."""
+    torch = torch_cuda
+    n, L = 1000, 100_000
+    seg = [0]
+    for _ in range(n):
+        seg.append(seg[-1] + L + 1)
+    mask = sksffi.mask_generate(31, 21, 0)
+    sets = {}
+    for mode in ("indep", "family"):
+        buf = torch.empty(seg[-1], dtype=torch.uint8, device="cuda:0")
+        for g in range(n):
+            if mode == "indep":
+                ctx.synth_bases(buf.data_ptr() + seg[g], L, 7000 + g)
+            else:
+                ctx.synth_bases(buf.data_ptr() + seg[g], L, 100 + g % 25, 9000 + g, 0.002 + 0.0005 * (g % 9))
+        buf[torch.tensor(seg[1:], device="cuda:0") - 1] = ord("\n")
+        ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, 31, mask, sksffi.SKS_BOTTOM_S, 10000)
+        del buf
+        sets[mode] = ss
+    return n, sets
+
+
+@pytest.mark.parametrize("kernel_ctx", [sksffi.INTERSECT_JOIN, sksffi.INTERSECT_RANGE], indirect=True)
+@pytest.mark.parametrize("mode", ["indep", "family"])
+def test_join_exact_at_scale(torch_cuda, kernel_ctx, scale_sets, mode):
+    """~10^8 hash-table inserts per all-pairs call (1000 sketches of 10000):
+    three calls each equal the merge kernel cell for cell.  Round 3: a probe
+    loop compiled with its joined-entry register updated on every tag match gave
+    about one insert in 10^7 a foreign entry (a diagonal one short, one stray +1;
+    join_common.hpp join_chain) — far too rare for the small tests above."""
+    torch = torch_cuda
+    ctx = kernel_ctx
+    n, sets = scale_sets
+    d, st, sz = sets[mode].device_ptrs()
+    T = sksffi.intersect_sym_tiles(n)
+    kernel = ctx_kernel(ctx)
+    ref = torch.empty((n, n), dtype=torch.int32, device="cuda:0")
+    ctx.set_intersect_kernel(sksffi.INTERSECT_MERGE)
+    ctx.intersect_sym(d, st, sz, 1, n, 0, T, ref.data_ptr())
+    ctx.set_intersect_kernel(kernel)
+    out = torch.empty((n, n), dtype=torch.int32, device="cuda:0")
+    for _ in range(3):
+        out.fill_(-1)
+        ctx.intersect_sym(d, st, sz, 1, n, 0, T, out.data_ptr())
+        torch.cuda.synchronize()
+        bad = torch.nonzero(out != ref)
+        assert bad.shape[0] == 0, [(i, j, int(out[i, j]), int(ref[i, j])) for i, j in bad[:4].tolist()]
+    assert int(torch.diagonal(ref).min()) == 10000

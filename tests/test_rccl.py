@@ -95,10 +95,11 @@ def test_join_layout_all_vs_all_on_rccl(env, side_stream):
     assert want[0, 9] > 0 and want[40].sum() == 0
     stream = torch.cuda.Stream() if side_stream else None
     cctx = sksffi.Context(0, stream.cuda_stream) if side_stream else ctx
-    build, count = sks_dist.join_layout_fns(cctx, ss, sizes, device="cuda")
+    build, count, bounds = sks_dist.join_layout_fns(cctx, ss, sizes, device="cuda")
     out = torch.full((n, n), -5, dtype=torch.int32, device="cuda")
     mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), int(sizes.astype(np.int64).sum()),
-                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out)
+                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out,
+                                   bounds=bounds)
     torch.cuda.synchronize()
     assert np.array_equal(mat.cpu().numpy().astype(np.int64), want), side_stream
     if side_stream:

@@ -87,10 +87,11 @@ def test_config4_all_vs_all_1000x5mb(env):
         assert np.array_equal(ss.sketch(g), want), g
         assert int(ss.windows()[g]) == nw
     # the bench's pair path, world 1
-    build, count = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda")
+    build, count, bounds = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda")
     out = torch.full((n, n), -1, dtype=torch.int32, device="cuda")
     mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), int(sizes.astype(np.int64).sum()),
-                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out)
+                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out,
+                                   bounds=bounds)
     torch.cuda.synchronize()
     got = mat.cpu().numpy().astype(np.int64)
     want = _host_counts(_exported(ss, n))
