@@ -20,12 +20,13 @@
 // Counts are exact for any non-decreasing bounds; all layouts whose blocks are
 // joined with each other (a multi-GPU gather) must share one bounds array.
 //
-// Build (join_layout_build): k_gl_prep (the group bounds when the caller gives
-// none, and the block starts), then k_gl_place, one workgroup per (block,
-// group): the 64 sketches' group ranges, a (bucket x slot) histogram in LDS, its
-// scans (the block's bucket starts and each (bucket, slot) cursor), and the
-// scatter of the group's elements into LDS, copied out to its own contiguous
-// part of the layout with contiguous stores.
+// Build (join_layout_build), three launches: k_gl_prep (the group bounds when
+// the caller gives none, and the block starts), k_gl_pos (every sketch's group
+// starts: a thread per binary search), then k_gl_place, one workgroup per
+// (block, group): the group's elements read once into registers, a (bucket x
+// slot) histogram in LDS, its scans (the block's bucket starts and each
+// (bucket, slot) cursor), and the scatter into LDS, copied out to the group's
+// own contiguous part of the layout with contiguous stores.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -153,7 +154,17 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
   pos[idx] = g == 0 ? 0 : g == G ? sz : lower_bound(data + starts[i], sz, bounds[g]);
 }
 
-// One workgroup per (block, value group).
+// One workgroup per (block, value group).  A group of at most kGCap elements
+// (the normal case) is read ONCE: its elements are spread over all 256 threads
+// (element i of the group -> its sketch through an owner map in LDS) and held in
+// registers through the histogram, the scans and the scatter into LDS, then
+// copied out with contiguous stores.  A larger group (skewed values) takes a
+// wave per sketch, reads it twice and scatters straight to global memory.
+// (Round 3's first version took the wave-per-sketch loops for every group:
+// ~39 elements per sketch and group left a third of the lanes idle behind
+// serial load -> atomic chains; config 4: 127 us, now 66 us.  Scattering
+// straight to global memory instead of assembling in LDS — 10 instead of 47 KB
+// of LDS, twice the workgroups per CU — measured the same, 68 us.)
 __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ data,
                                                   const uint64_t* __restrict__ starts,
                                                   const uint32_t* __restrict__ sizes, uint32_t count,
@@ -163,15 +174,16 @@ __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ d
                                                   uint8_t* __restrict__ out_ids,
                                                   uint32_t* __restrict__ out_boff,
                                                   uint32_t* __restrict__ stat) {
-  // counts, then cursors, [slot][bucket]; the row pad puts the lanes of a wave
-  // (one slot, random buckets) and of the scans (one bucket, all slots) on
-  // distinct banks
+  // counts, then cursors, [slot][bucket]; the row pad puts the lanes of the
+  // scans (one bucket, all slots) on distinct banks
   __shared__ uint32_t s_cnt[kTile][kGB + 1];
   __shared__ uint64_t s_out[kGCap];
   __shared__ uint8_t s_oid[kGCap];
-  __shared__ uint32_t s_lo[kTile], s_hi[kTile];
+  __shared__ uint8_t s_own[kGCap];  // group element i -> its sketch's slot
+  __shared__ uint64_t s_src[kTile];  // data index of slot s's group element i: s_src[s] + i
+  __shared__ uint32_t s_lo[kTile], s_hi[kTile], s_pre[kTile];
   __shared__ uint32_t s_btot[kGB];
-  __shared__ uint32_t s_gstart, s_gend;
+  __shared__ uint32_t s_gstart, s_gn;
   const uint32_t B = 1u << log_b;
   const uint32_t gb_log = log_b < kGLog ? log_b : kGLog, GB = 1u << gb_log;
   const uint32_t G = B >> gb_log;
@@ -179,32 +191,55 @@ __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ d
   const uint32_t s_end = min((uint32_t)kTile, count - kTile * blk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (uint32_t i = tid; i < kTile * (kGB + 1); i += kPT) (&s_cnt[0][0])[i] = 0;
-  // the group's range of each sketch (k_gl_pos)
-  if (wave < 2) {
-    uint32_t p = 0;
-    if ((uint32_t)lane < s_end) p = pos[(uint64_t)(kTile * blk + lane) * (G + 1) + g + wave];
-    if (wave == 0) {
-      s_lo[lane] = p;
-      // elements of the block below the group = sum of the sketches' lo
-      const uint32_t below = wave_scan(p);
-      if (lane == 63) s_gstart = below;
-    } else {
-      s_hi[lane] = p;
+  // each sketch's range in the group (k_gl_pos), the group's start in the
+  // block (the sum of the ranges' starts) and the element prefix over sketches
+  if (wave == 0) {
+    uint32_t lo = 0, hi = 0;
+    uint64_t st = 0;
+    if ((uint32_t)lane < s_end) {
+      const uint32_t* p = pos + (uint64_t)(kTile * blk + lane) * (G + 1) + g;
+      lo = p[0];
+      hi = max(p[1], lo);  // (non-decreasing bounds: only a guard)
+      st = starts[kTile * blk + lane];
+    }
+    const uint32_t c = hi - lo;
+    const uint32_t below = wave_scan(lo);
+    const uint32_t incl = wave_scan(c);
+    s_lo[lane] = lo;
+    s_hi[lane] = hi;
+    s_pre[lane] = incl - c;
+    s_src[lane] = st + lo - (incl - c);
+    if (lane == 63) {
+      s_gstart = below;
+      s_gn = incl;
     }
   }
   __syncthreads();
-  // 1) (slot, bucket) histogram: a wave per sketch, lanes over its range, two
-  //    loads in flight
-  for (uint32_t s = wave; s < s_end; s += kPT / 64) {
-    const uint64_t* S = data + starts[kTile * blk + s];
-    const uint32_t hi = max(s_hi[s], s_lo[s]);  // (non-decreasing bounds: only a guard)
-    uint32_t e = s_lo[s] + lane;
-    for (; e + 64 < hi; e += 128) {
-      const uint64_t v0 = S[e], v1 = S[e + 64];
-      atomicAdd(&s_cnt[s][group_bucket(v0, gb_log)], 1u);
-      atomicAdd(&s_cnt[s][group_bucket(v1, gb_log)], 1u);
+  const uint32_t g_lo = s_gstart;  // the group's first element (block-relative)
+  const uint32_t g_n = s_gn;
+  const bool in_lds = g_n <= kGCap;
+  constexpr int kPer = kGCap / kPT;
+  uint64_t v[kPer];
+  // 1) (slot, bucket) histogram
+  if (in_lds) {
+    for (uint32_t s = wave; s < s_end; s += kPT / 64)
+      for (uint32_t j = s_pre[s] + lane; j < s_pre[s] + (s_hi[s] - s_lo[s]); j += 64) s_own[j] = (uint8_t)s;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * kPT;
+      if (i < g_n) v[k] = data[s_src[s_own[i]] + i];
     }
-    if (e < hi) atomicAdd(&s_cnt[s][group_bucket(S[e], gb_log)], 1u);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t i = tid + k * kPT;
+      if (i < g_n) atomicAdd(&s_cnt[s_own[i]][group_bucket(v[k], gb_log)], 1u);
+    }
+  } else {
+    for (uint32_t s = wave; s < s_end; s += kPT / 64) {
+      const uint64_t* S = data + starts[kTile * blk + s];
+      for (uint32_t e = s_lo[s] + lane; e < s_hi[s]; e += 64) atomicAdd(&s_cnt[s][group_bucket(S[e], gb_log)], 1u);
+    }
   }
   __syncthreads();
   // 2) per bucket: slot prefix (a wave scan) and total; lane s of wave w holds
@@ -220,15 +255,12 @@ __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ d
   if (wave == 0) {
     const uint32_t t = (uint32_t)lane < GB ? s_btot[lane] : 0;
     const uint32_t incl = wave_scan(t);
-    const uint32_t start = s_gstart + incl - t;
+    const uint32_t start = g_lo + incl - t;
     if ((uint32_t)lane < GB) {
       out_boff[(uint64_t)blk * (B + 1) + g * GB + lane] = start;
       s_btot[lane] = start;
     }
-    if (lane == 63) {
-      s_gend = s_gstart + incl;
-      if (g + 1 == G) out_boff[(uint64_t)blk * (B + 1) + B] = s_gstart + incl;
-    }
+    if (lane == 63 && g + 1 == G) out_boff[(uint64_t)blk * (B + 1) + B] = g_lo + incl;
     uint32_t mx = t;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
@@ -238,28 +270,30 @@ __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ d
   for (uint32_t i = tid; i < kTile * GB; i += kPT) s_cnt[i / GB][i % GB] += s_btot[i % GB];
   __syncthreads();
   // 4) scatter: every element to its (bucket, slot) cell of the group's own
-  //    contiguous part of the block — assembled in LDS, then copied out with
-  //    contiguous stores; a group above kGCap scatters to global memory
+  //    contiguous part of the block
   const uint64_t base = bstart[blk];
-  const uint32_t g_lo = s_gstart;  // the group's first element (block-relative)
-  const uint32_t g_n = s_gend - g_lo;
-  const bool in_lds = g_n <= kGCap;
-  for (uint32_t s = wave; s < s_end; s += kPT / 64) {
-    const uint64_t* S = data + starts[kTile * blk + s];
-    const uint32_t hi = max(s_hi[s], s_lo[s]);
-    for (uint32_t e = s_lo[s] + lane; e < hi; e += 64) {
-      const uint64_t v = S[e];
-      const uint32_t d = atomicAdd(&s_cnt[s][group_bucket(v, gb_log)], 1u);
-      if (in_lds) {
-        s_out[d - g_lo] = v;
-        s_oid[d - g_lo] = (uint8_t)s;
-      } else {
-        out_data[base + d] = v;
+  if (!in_lds) {
+    for (uint32_t s = wave; s < s_end; s += kPT / 64) {
+      const uint64_t* S = data + starts[kTile * blk + s];
+      for (uint32_t e = s_lo[s] + lane; e < s_hi[s]; e += 64) {
+        const uint64_t x = S[e];
+        const uint32_t d = atomicAdd(&s_cnt[s][group_bucket(x, gb_log)], 1u);
+        out_data[base + d] = x;
         out_ids[base + d] = (uint8_t)s;
       }
     }
+    return;
   }
-  if (!in_lds) return;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const uint32_t i = tid + k * kPT;
+    if (i < g_n) {
+      const uint32_t s = s_own[i];
+      const uint32_t d = atomicAdd(&s_cnt[s][group_bucket(v[k], gb_log)], 1u) - g_lo;
+      s_out[d] = v[k];
+      s_oid[d] = (uint8_t)s;
+    }
+  }
   __syncthreads();
   uint64_t* od = out_data + base + g_lo;
   uint8_t* oi = out_ids + base + g_lo;
