@@ -1328,9 +1328,10 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       JoinLayout rl = cl;
       uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
       if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
-      // the column and row layouts share the column set's group bounds
-      uint64_t* gbounds = reinterpret_cast<uint64_t*>(w + o_bnd);
-      if (!hash_layout && (e = join_layout_bounds(data, starts, sizes, n, log_b, gbounds, s)) != hipSuccess)
+      // a separate row layout shares the column set's group bounds; a single
+      // layout computes its own in the build's first launch (three in all)
+      uint64_t* gbounds = sep_rows ? reinterpret_cast<uint64_t*>(w + o_bnd) : nullptr;
+      if (!hash_layout && sep_rows && (e = join_layout_bounds(data, starts, sizes, n, log_b, gbounds, s)) != hipSuccess)
         return e;
       auto build_layout = [&](uint32_t first, uint32_t cnt, uint64_t tot, const JoinLayout& L,
                               size_t tmp_bytes) -> hipError_t {

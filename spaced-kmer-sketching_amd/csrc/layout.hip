@@ -141,7 +141,10 @@ __global__ __launch_bounds__(kPT) void k_gl_prep(const uint64_t* __restrict__ da
 
 // pos[i][g] = first element of sketch i in value group g (lower bound of
 // bounds[g]; pos[i][0] = 0, pos[i][G] = size): a thread per (sketch, bound), so
-// every binary search of the build runs in one wave of the whole GPU.
+// every binary search of the build runs in one wave of the whole GPU.  (A
+// workgroup per sketch searching an LDS sample of every 64th element first —
+// 7 instead of 14 dependent global loads — measured the same, 20.7 vs 21.4 us
+// for config 4: the searches are not what this launch waits on.)
 __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ data,
                                                 const uint64_t* __restrict__ starts,
                                                 const uint32_t* __restrict__ sizes, uint32_t count,
