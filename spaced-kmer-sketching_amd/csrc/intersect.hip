@@ -1109,19 +1109,22 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.out = out;
   ja.ld = n;
   ja.cap = join_cap();
-  // bucket groups per tile: ~64 buckets per workgroup (a workgroup's start-up —
-  // clearing its table and count matrix — and its count flush are then small
-  // beside its chunks), at least ~1024 workgroups in all, at least 16 buckets
-  // each. Config 4 (136 tiles, B = 4096): 8704 workgroups, 1.17 ms; config 5
-  // (10 tiles): 1030, 0.31 ms — against 1.32 / 0.36 ms with 2048 in all.
+  // bucket groups per tile: ~128 buckets per workgroup (a workgroup's start-up —
+  // clearing its table and count planes — and its count flush, up to 4096 global
+  // atomics on a tile of related genomes, are then small beside its chunks), at
+  // least ~1024 workgroups in all, at least 16 buckets each.  Config 4 (136
+  // tiles, B = 4096), round 3 sweep of SKS_JOIN_WGS, whole call family /
+  // unrelated genomes: 1088 workgroups 0.870 / 0.792 ms, 2176 0.705 / 0.691,
+  // 4352 (this rule) 0.681 / 0.674, 8704 (round 2's ~64 buckets) 0.742 / 0.681,
+  // 17408 0.900 / 0.734.  Config 5 (10 tiles): the 1024 floor, 1030.
   // SKS_JOIN_WGS (diagnostics) sets the total instead.
-  // The ~64-buckets floor only applies while the grid is small (<= 64K
+  // The ~128-buckets floor only applies while the grid is small (<= 64K
   // workgroups); with very many tiles a tile gets fewer, larger groups (down to
   // one), and the launch is cut into tile slices of at most kMaxGrid workgroups
   // (HIP caps a grid at 2^32 - 1 work-items).
   static const uint64_t wgs_env = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 0;
   uint64_t want = wgs_env ? (wgs_env + tiles - 1) / tiles
-                          : std::max<uint64_t>(std::min<uint64_t>((B + 63) / 64, (65536 + tiles - 1) / tiles),
+                          : std::max<uint64_t>(std::min<uint64_t>((B + 127) / 128, (65536 + tiles - 1) / tiles),
                                                (1024 + tiles - 1) / tiles);
   if (!wgs_env) want = std::min<uint64_t>(want, std::max<uint32_t>(1, B / 16));
   const uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, want));
