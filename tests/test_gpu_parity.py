@@ -974,3 +974,41 @@ def test_join_exact_at_scale(torch_cuda, kernel_ctx, scale_sets, mode):
         bad = torch.nonzero(out != ref)
         assert bad.shape[0] == 0, [(i, j, int(out[i, j]), int(ref[i, j])) for i, j in bad[:4].tolist()]
     assert int(torch.diagonal(ref).min()) == 10000
+
+
+def test_config3_contig_against_oracle(torch_cuda, ctx):
+    """One real config-3 contig: contig 0 of bench.py's
+    genome — 125 Mb from sks_synth_bases(seed 3) with four 10 kb N-runs at
+    L*(j+1)/5 — sketched with w=31/k=21 (mask seed 0), FracMinHash 1/1000, equals
+    the oracle's set (8 chunks with (w-1)-base halos, unioned) and window count."""
+    from concurrent.futures import ThreadPoolExecutor
+    torch = torch_cuda
+    L, w, frac, nrun, nrun_len = 125_000_000, 31, 1000, 4, 10_000
+    mask = sksffi.mask_generate(w, 21, 0)
+    dev = torch.empty(L + 1, dtype=torch.uint8, device="cuda:0")
+    ctx.synth_bases(dev.data_ptr(), L, 3)
+    edges = [0]
+    for j in range(nrun):
+        o = int(L * (j + 1) / (nrun + 1))
+        dev[o:o + nrun_len] = ord("N")
+        edges += [o, o + nrun_len]
+    edges.append(L)
+    dev[L] = ord("\n")
+    torch.cuda.synchronize()
+    gpu = ctx.sketch_build(dev.data_ptr(), L + 1, [0, L + 1], w, mask, sksffi.SKS_FRAC_MOD, frac)
+    host = dev[:L].cpu().numpy().tobytes()
+    T = 8
+    cuts = [L * i // T for i in range(T + 1)]
+
+    def one(i):
+        a, b = cuts[i], min(L, cuts[i + 1] + w - 1)
+        sk, nw = O.sketch(O.cut_runs(host[a:b]), w, mask, "frac", frac)
+        return sk[:, 0], nw
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(one, range(T)))
+    want = np.unique(np.concatenate([r[0] for r in res]))
+    windows = sum(max(0, edges[i + 1] - edges[i] - w + 1) for i in range(0, len(edges), 2))
+    assert sum(r[1] for r in res) == windows
+    assert int(gpu.windows()[0]) == windows
+    got = gpu.sketch(0)[:, 0]
+    assert got.size == want.size and np.array_equal(got, want)

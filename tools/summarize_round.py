@@ -89,7 +89,7 @@ def main(src, dst, warmup, steps):
     with open(os.path.join(dst, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     for sub, name, kernels in (("sq", "scan_counters.txt", ["scan_kernel"]),
-                               ("pairs", "pair_counters.txt", ["k_join", "k_bottom_fused", "k_hb_"])):
+                               ("pairs", "pair_counters.txt", ["k_join", "k_bottom_fused", "k_gl_"])):
         if os.path.isdir(os.path.join(src, sub)):
             buf = io.StringIO()
             with redirect_stdout(buf):
