@@ -22,7 +22,7 @@
 //
 // Build (join_layout_build), three launches: k_gl_prep (the group bounds when
 // the caller gives none, and the block starts), k_gl_pos (every sketch's group
-// starts: a thread per binary search), then k_gl_place, one workgroup per
+// starts: a workgroup per sketch), then k_gl_place, one workgroup per
 // (block, group): the group's elements read once into registers, a (bucket x
 // slot) histogram in LDS, its scans (the block's bucket starts and each
 // (bucket, slot) cursor), and the scatter into LDS, copied out to the group's
@@ -61,15 +61,6 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
   return v;
-}
-
-__device__ __forceinline__ uint32_t lower_bound(const uint64_t* __restrict__ S, uint32_t n, uint64_t x) {
-  uint32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (S[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
 }
 
 // Workgroups [0, nb_bounds): the group bounds, a wave per bound (bounds[g] =
@@ -140,21 +131,51 @@ __global__ __launch_bounds__(kPT) void k_gl_prep(const uint64_t* __restrict__ da
 }
 
 // pos[i][g] = first element of sketch i in value group g (lower bound of
-// bounds[g]; pos[i][0] = 0, pos[i][G] = size): a thread per (sketch, bound), so
-// every binary search of the build runs in one wave of the whole GPU.  (A
-// workgroup per sketch searching an LDS sample of every 64th element first —
-// 7 instead of 14 dependent global loads — measured the same, 20.7 vs 21.4 us
-// for config 4: the searches are not what this launch waits on.)
+// bounds[g]; pos[i][0] = 0, pos[i][G] = size).  A workgroup per sketch stages
+// every kPosStride-th element in LDS with one coalesced pass, and a thread per
+// bound searches that sample and then the one cache line it points at.  (A
+// thread per (sketch, bound) binary-searching the sketch took 21 us for config
+// 4: the threads of a sketch share the top of the search tree, so its last ~6
+// levels are the dependent misses — which is also why a 64-element sample,
+// leaving 6 levels to search in global memory, measured the same.)  This
+// version: 19.8 us — a stride-8 sample touches every 64-B line of the sketch,
+// so the launch is bound by reading the sketches once (80 MB).  A sketch
+// above kPosSamples * kPosStride elements samples with a larger stride.
+constexpr uint32_t kPosStride = 8, kPosSamples = 2048;
 __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ data,
                                                 const uint64_t* __restrict__ starts,
                                                 const uint32_t* __restrict__ sizes, uint32_t count,
                                                 uint32_t G, const uint64_t* __restrict__ bounds,
                                                 uint32_t* __restrict__ pos) {
-  const uint64_t idx = (uint64_t)blockIdx.x * kPT + threadIdx.x;
-  if (idx >= (uint64_t)count * (G + 1)) return;
-  const uint32_t i = (uint32_t)(idx / (G + 1)), g = (uint32_t)(idx % (G + 1));
+  __shared__ uint64_t s_smp[kPosSamples];
+  const uint32_t i = blockIdx.x;
   const uint32_t sz = sizes[i];
-  pos[idx] = g == 0 ? 0 : g == G ? sz : lower_bound(data + starts[i], sz, bounds[g]);
+  const uint64_t* S = data + starts[i];
+  uint32_t stride = kPosStride;
+  while ((uint64_t)stride * kPosSamples < sz) stride <<= 1;
+  const uint32_t ns = (sz + stride - 1) / stride;  // sample k = S[k * stride]
+  for (uint32_t k = threadIdx.x; k < ns; k += kPT) s_smp[k] = S[(uint64_t)k * stride];
+  __syncthreads();
+  uint32_t* out = pos + (uint64_t)i * (G + 1);
+  for (uint32_t g = threadIdx.x; g <= G; g += kPT) {
+    if (g == 0 || g == G) {
+      out[g] = g == 0 ? 0 : sz;
+      continue;
+    }
+    const uint64_t x = bounds[g];
+    // lo = samples below x: the lower bound lies in ((lo - 1) * stride, lo * stride]
+    uint32_t lo = 0, hi = ns;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_smp[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    uint32_t a = lo ? (lo - 1) * stride + 1 : 0, e = min(sz, lo * stride);
+    while (a < e) {
+      const uint32_t mid = (a + e) >> 1;
+      if (S[mid] < x) a = mid + 1; else e = mid;
+    }
+    out[g] = a;
+  }
 }
 
 // One workgroup per (block, value group).  A group of at most kGCap elements
@@ -267,7 +288,13 @@ __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ d
     uint32_t mx = t;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
-    if (lane == 0 && mx) atomicMax(stat, mx);
+    // one word for all 4096 workgroups: a device-scope atomic per workgroup
+    // would serialise (one word takes ~88 atomics per microsecond,
+    // MI355X_MICROARCH.md "dequeue"); the stat only grows, so a workgroup whose
+    // maximum is not above the value it reads skips the atomic (a stale read
+    // only costs an atomic)
+    if (lane == 0 && mx && mx > __hip_atomic_load(stat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(stat, mx);
   }
   __syncthreads();
   for (uint32_t i = tid; i < kTile * GB; i += kPT) s_cnt[i / GB][i % GB] += s_btot[i % GB];
@@ -340,9 +367,7 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   hipLaunchKernelGGL(k_gl_prep, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
                      bounds_tmp, nb_bounds, out_bstart);
   const uint64_t* bounds = d_bounds ? d_bounds : bounds_tmp;
-  const uint64_t items = (uint64_t)count * (G + 1);
-  hipLaunchKernelGGL(k_gl_pos, dim3((unsigned)((items + kPT - 1) / kPT)), dim3(kPT), 0, s, data, starts, sizes,
-                     count, G, bounds, pos);
+  hipLaunchKernelGGL(k_gl_pos, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
   hipLaunchKernelGGL(k_gl_place, dim3(n_blk * G), dim3(kPT), 0, s, data, starts, sizes, count, log_b, pos,
                      out_bstart, out_data, out_ids, out_boff, d_stat);
   return hipGetLastError();
