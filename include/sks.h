@@ -305,34 +305,6 @@ int sks_intersect_layout_tiles(sks_ctx* ctx, uint32_t n, uint32_t log_b, const u
                                uint32_t blk0, const uint32_t* d_tiles, uint64_t tile_begin,
                                uint64_t tile_end, int packed, int32_t* d_out);
 
-/* ---- range join: all-pairs straight from the sorted sketches, across GPUs -----------------
- * Replaces the pair loop of compute_pairwise_kmer_set_intersections
- * (kmer_set.cpp:143-184) over u64 sketches, each count equal to
- * kmer_set_intersection (kmer_set.cpp:23-41).  The kernel of SKS_INTERSECT_RANGE
- * reads sketches (d_data, d_starts, d_sizes: sorted unique u64 values, as an
- * sks_sketch_set holds them) through value-range buckets: bounds u64[2^log_b + 1],
- * non-decreasing, bounds[0] = 0 and bounds[2^log_b] = 2^64 - 1.  Any such bounds
- * give exact counts; sks_range_bounds picks balanced ones (quantiles averaged
- * over up to 64 sample sketches).  A multi-GPU caller can count the tiles of its
- * own sketches while the others' are still being gathered, as long as it uses
- * one bounds array for all of its calls. */
-uint32_t sks_range_log_b(uint32_t max_sketch_size);
-int sks_range_bounds(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
-                     const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_bounds);
-/* Counts of 64x64 tiles of the n x n matrix of the n sketches.  Tiles:
- * d_tiles == NULL -> upper-triangle tiles [tile_begin, tile_end) in row-major
- * order (sks_intersect_sym_tiles); else the list d_tiles[2t] = I,
- * d_tiles[2t + 1] = J (block indices, I <= J < ceil(n / 64)) for t in
- * [tile_begin, tile_end).  packed == 0: counts are ADDED to the n x n int32
- * matrix d_out at (i, j) and (j, i); packed != 0: to
- * d_out[(t - tile_begin) * 4096 + r * 64 + c] for row I*64 + r, column J*64 + c
- * (a diagonal tile holds both triangles).  The caller zeroes d_out.  The
- * element offsets d_starts[i] + d_sizes[i] must stay below 2^32. */
-int sks_intersect_range(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
-                        const uint32_t* d_sizes, uint32_t n, uint32_t log_b, const uint64_t* d_bounds,
-                        const uint32_t* d_tiles, uint64_t tile_begin, uint64_t tile_end, int packed,
-                        int32_t* d_out);
-
 /* ---- FASTA ingress (device) — fasta_processing.cpp:79-133 on the GPU ------------------
  * d_raw: the n_raw bytes of one FASTA file in device memory (the host only reads
  * the file).  Writes to d_stream exactly the bytes sks_fasta_stream() holds for
@@ -357,16 +329,13 @@ int sks_ctx_set_scan_grid(sks_ctx* ctx, int grid);
 /* Kernel used by sks_intersect_all / sks_intersect_sym for u64 sketches.  All
  * give identical counts; AUTO (default) = the LDS hash join when the bucket
  * sizes allow it, else the LDS merge tiles, else one wavefront per pair.
- * POSTINGS is selected explicitly only (config 4: 1.9 ms against 0.81 ms for
- * the hash join). */
+ * (Round 3's block-postings and range-join kernels were measured slower than
+ * the hash join on every workload and removed) */
 enum {
   SKS_INTERSECT_AUTO = 0,
   SKS_INTERSECT_MERGE = 1,    /* 64x64 tiles of pairwise LDS merges */
   SKS_INTERSECT_JOIN = 2,     /* 64x64 tiles, LDS hash join of the two blocks */
-  SKS_INTERSECT_GLOBAL = 3,   /* one wavefront per pair, straight from HBM */
-  SKS_INTERSECT_POSTINGS = 4, /* 64x64 tiles, join of the blocks' postings, counts on MFMA */
-  SKS_INTERSECT_RANGE = 5     /* 64x64 tiles, LDS hash join read straight from the sorted
-                                 sketches through value-range bucket positions */
+  SKS_INTERSECT_GLOBAL = 3    /* one wavefront per pair, straight from HBM */
 };
 int sks_ctx_set_intersect_kernel(sks_ctx* ctx, int kind);
 

@@ -630,7 +630,7 @@ int sks_ctx_set_scan_grid(sks_ctx* c, int grid) {
 
 int sks_ctx_set_intersect_kernel(sks_ctx* c, int kind) {
   if (!c) return sks::fail(SKS_E_ARG, "null ctx");
-  if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_RANGE)
+  if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_GLOBAL)
     return sks::fail(SKS_E_ARG, "sks_ctx_set_intersect_kernel: unknown kernel");
   c->intersect_algo = kind;
   return SKS_OK;
@@ -1547,46 +1547,6 @@ int sks_intersect_sym_layout(sks_ctx* c, uint32_t n, uint32_t log_b, const uint6
     const sks::JoinLayout L{d_data, d_ids, d_boff, d_bstart};
     SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, true, 0, n, tile_begin, tile_end, nullptr, false, d_out,
                              c->stream));
-  }
-  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
-  return SKS_OK;
-}
-
-uint32_t sks_range_log_b(uint32_t max_sketch_size) { return sks::join_log_b(max_sketch_size); }
-
-int sks_range_bounds(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
-                     const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_bounds) {
-  if (!c) return sks::fail(SKS_E_ARG, "sks_range_bounds: null ctx");
-  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_range_bounds: log_b > 14");
-  if (!d_bounds || (n && (!d_starts || !d_sizes))) return sks::fail(SKS_E_ARG, "sks_range_bounds: null argument");
-  DeviceGuard g(c->device);
-  SKS_HIP(sks::rjoin_bounds(d_data, d_starts, d_sizes, n, 1u << log_b, d_bounds, c->stream));
-  return SKS_OK;
-}
-
-int sks_intersect_range(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
-                        const uint32_t* d_sizes, uint32_t n, uint32_t log_b, const uint64_t* d_bounds,
-                        const uint32_t* d_tiles, uint64_t tile_begin, uint64_t tile_end, int packed,
-                        int32_t* d_out) {
-  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_range: null ctx");
-  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_range: log_b > 14");
-  if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_range: bad tile range");
-  if (!d_tiles && tile_end > sks::intersect_sym_tiles(n))
-    return sks::fail(SKS_E_ARG, "sks_intersect_range: tile range beyond the upper triangle");
-  if (tile_end > tile_begin && (!d_starts || !d_sizes || !d_bounds || !d_out))
-    return sks::fail(SKS_E_ARG, "sks_intersect_range: null argument");
-  DeviceGuard g(c->device);
-  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
-  if (tile_end > tile_begin && n) {
-    const uint32_t B = 1u << log_b, n_cb = (n + 63) / 64;
-    const size_t o_pre = ((size_t)n * (B + 1) * 4 + 255) & ~(size_t)255;
-    SKS_HIP(c->iwork.reserve(o_pre + (size_t)n_cb * (B + 1) * 4));
-    uint32_t* pos = static_cast<uint32_t*>(c->iwork.ptr);
-    uint32_t* pre = reinterpret_cast<uint32_t*>(static_cast<char*>(c->iwork.ptr) + o_pre);
-    SKS_HIP(sks::rjoin_pos(d_data, d_starts, d_sizes, n, B, d_bounds, pos, c->stream));
-    SKS_HIP(sks::rjoin_block_prefix(pos, n, B, pre, c->stream));
-    SKS_HIP(sks::rjoin_launch(d_data, d_starts, pos, pre, n, B, true, 0, n, tile_begin, tile_end, d_tiles,
-                              packed != 0, d_out, c->stream));
   }
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;

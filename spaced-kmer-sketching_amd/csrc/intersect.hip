@@ -401,218 +401,6 @@ constexpr uint32_t kJMaxLogB = 14;          // B <= 16384 (LDS histogram of k_hb
 constexpr int kPlanes = 32;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t bucket_hash(uint64_t v, uint32_t log_b) {
-  return log_b ? (uint32_t)((v * 0x9E3779B97F4A7C15ull) >> (64 - log_b)) : 0u;
-}
-
-// One workgroup per sketch i in [first, first + count): per-bucket element
-// counts into counts[(blk * 64 + slot) * B + b] (one contiguous row per
-// sketch, so the writes coalesce), blk/slot of i - base.
-__global__ __launch_bounds__(kB) void k_hb_count(const uint64_t* __restrict__ data,
-                                                 const uint64_t* __restrict__ starts,
-                                                 const uint32_t* __restrict__ sizes,
-                                                 uint32_t first, uint32_t base, uint32_t B,
-                                                 uint32_t log_b, uint32_t* __restrict__ counts,
-                                                 uint32_t G, uint32_t* __restrict__ gcounts) {
-  extern __shared__ uint32_t h[];
-  const uint32_t i = first + blockIdx.x;
-  const uint32_t sz = sizes[i];
-  const uint64_t* src = data + starts[i];
-  for (uint32_t b = threadIdx.x; b < B; b += kB) h[b] = 0;
-  __syncthreads();
-  // four loads in flight per thread before their histogram atomics
-  uint32_t e = threadIdx.x;
-  for (; e + 3 * kB < sz; e += 4 * kB) {
-    uint64_t v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src[e + u * kB];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) atomicAdd(&h[bucket_hash(v[u], log_b)], 1u);
-  }
-  for (; e < sz; e += kB) atomicAdd(&h[bucket_hash(src[e], log_b)], 1u);
-  __syncthreads();
-  uint32_t* dst = counts + (uint64_t)(i - base) * B;  // (blk * 64 + slot) * B
-  for (uint32_t b = threadIdx.x; b < B; b += kB) dst[b] = h[b];
-  // elements per coarse group of B / G consecutive buckets (two-phase scatter)
-  const uint32_t bpg = B / G;
-  for (uint32_t g = threadIdx.x; g < G; g += kB) {
-    uint32_t t = 0;
-    for (uint32_t b = g * bpg; b < (g + 1) * bpg; ++b) t += h[b];
-    gcounts[(uint64_t)(i - base) * G + g] = t;
-  }
-}
-
-// colsum[blk * B + b] = elements of bucket b in block blk (all 64 slots);
-// colsum[n_blk * B] = 0 so that its exclusive scan ends with the total.
-__global__ void k_hb_colsum(const uint32_t* __restrict__ counts, uint32_t n_blk, uint32_t B,
-                            uint32_t* __restrict__ colsum) {
-  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  const uint64_t cells = (uint64_t)n_blk * B;
-  if (idx > cells) return;
-  if (idx == cells) {
-    colsum[idx] = 0;
-    return;
-  }
-  const uint64_t blk = idx / B, b = idx % B;
-  const uint32_t* c = counts + blk * 64 * B + b;
-  uint32_t t = 0;
-#pragma unroll 8
-  for (int slot = 0; slot < 64; ++slot) t += c[(uint64_t)slot * B];
-  colsum[idx] = t;
-}
-
-// From bbase = exclusive scan of colsum: each sketch's cursor for each bucket,
-// off[(blk * 64 + slot) * B + b] = bbase[blk * B + b] + counts of the slots
-// before it; the per-block bucket starts boff[blk][b] (b = 0..B), bstart and
-// the largest block-bucket population (*stat) of the JoinLayout.
-__global__ void k_hb_offsets(const uint32_t* __restrict__ counts, const uint32_t* __restrict__ bbase,
-                             uint32_t n_blk, uint32_t B, uint32_t* __restrict__ off,
-                             uint32_t* __restrict__ boff, uint64_t* __restrict__ bstart,
-                             uint32_t* __restrict__ stat, uint32_t G,
-                             const uint32_t* __restrict__ gcounts, uint32_t* __restrict__ goff) {
-  __shared__ uint32_t s_max[kB / 64];
-  const uint64_t idx = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  const bool in = idx < (uint64_t)n_blk * (B + 1);
-  const uint32_t blk = in ? (uint32_t)(idx / (B + 1)) : 0, b = in ? (uint32_t)(idx % (B + 1)) : B;
-  const uint32_t base = in ? bbase[(uint64_t)blk * B] : 0;
-  const uint32_t v = in ? bbase[(uint64_t)blk * B + b] : 0;  // b == B: the next block's start
-  // the largest block-bucket: one atomic per workgroup (one per wave cost
-  // ~12 us of this kernel's 27 on one contended word, config 4)
-  uint32_t pop = in && b < B ? bbase[(uint64_t)blk * B + b + 1] - v : 0;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) pop = max(pop, (uint32_t)__shfl_xor(pop, o, 64));
-  if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = pop;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t m = 0;
-    for (int w = 0; w < kB / 64; ++w) m = max(m, s_max[w]);
-    if (m) atomicMax(stat, m);
-  }
-  if (!in) return;
-  boff[idx] = v - base;
-  if (b == 0) bstart[blk] = base;
-  if (blk == n_blk - 1 && b == B) bstart[n_blk] = v;
-  if (b == B) return;
-  const uint64_t row0 = (uint64_t)blk * 64 * B + b;
-  uint32_t run = v;
-#pragma unroll 8
-  for (int slot = 0; slot < 64; ++slot) {
-    off[row0 + (uint64_t)slot * B] = run;
-    run += counts[row0 + (uint64_t)slot * B];
-  }
-  // the first bucket of each coarse group: where each slot's elements of the
-  // group start in the staging array (group-major, then slot)
-  const uint32_t bpg = B / G;
-  if (b % bpg == 0) {
-    const uint64_t grow0 = (uint64_t)blk * 64 * G + b / bpg;
-    uint32_t grun = v;
-    for (int slot = 0; slot < 64; ++slot) {
-      goff[grow0 + (uint64_t)slot * G] = grun;
-      grun += gcounts[grow0 + (uint64_t)slot * G];
-    }
-  }
-}
-
-// Phase 1 of the scatter: one workgroup per sketch appends its elements to
-// their coarse group's run for this slot in `stage` (runs of ~|S| / G
-// elements, so the writes are long contiguous runs).
-__global__ __launch_bounds__(kB) void k_hb_stage(const uint64_t* __restrict__ data,
-                                                 const uint64_t* __restrict__ starts,
-                                                 const uint32_t* __restrict__ sizes,
-                                                 uint32_t first, uint32_t base, uint32_t log_b,
-                                                 uint32_t log_g, const uint32_t* __restrict__ goff,
-                                                 uint64_t* __restrict__ stage) {
-  __shared__ uint32_t cur[1u << (kJMaxLogB - 6)];
-  const uint32_t G = 1u << log_g;
-  const uint32_t i = first + blockIdx.x;
-  const uint32_t sz = sizes[i];
-  const uint64_t* src = data + starts[i];
-  const uint32_t* o = goff + (uint64_t)(i - base) * G;
-  for (uint32_t g = threadIdx.x; g < G; g += kB) cur[g] = o[g];
-  __syncthreads();
-  auto put = [&](uint64_t v) {
-    stage[atomicAdd(&cur[bucket_hash(v, log_b) >> (log_b - log_g)], 1u)] = v;
-  };
-  // four loads in flight per thread before their cursor atomics
-  uint32_t e = threadIdx.x;
-  for (; e + 3 * kB < sz; e += 4 * kB) {
-    uint64_t v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src[e + u * kB];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) put(v[u]);
-  }
-  for (; e < sz; e += kB) put(src[e]);
-}
-
-// Phase 2: one workgroup per (block, coarse group) places the group's
-// elements (64 slot runs in `stage`) at their (bucket, slot) cells. All its
-// writes fall in the group's own contiguous range of the layout (~|S| * 64 / G
-// elements), which L2 assembles into whole lines.  The u8 slot ids of a group
-// of <= kPlaceIds elements are assembled in LDS and written out in order
-// afterwards: one scattered byte store per element cost about as much as the
-// 8-byte value stores (config 4: k_hb_place 110 -> 72 us).  Assembling the
-// values too needs smaller groups (LDS), and the staging pass then writes
-// shorter runs: 16 or 32 buckets per group measured 214-226 us for the whole
-// layout build against 186.
-constexpr uint32_t kPlaceIds = 16384;
-__global__ __launch_bounds__(kB) void k_hb_place(const uint64_t* __restrict__ stage,
-                                                 const uint32_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ goff,
-                                                 const uint32_t* __restrict__ gcounts, uint32_t B,
-                                                 uint32_t log_b, uint32_t log_g,
-                                                 uint64_t* __restrict__ out,
-                                                 uint8_t* __restrict__ ids) {
-  __shared__ uint32_t cur[64 * 64];  // [slot][bucket in group], B / G <= 64
-  __shared__ uint8_t s_ids[kPlaceIds];
-  __shared__ uint32_t s_total;
-  const uint32_t G = 1u << log_g, bpg = B >> log_g;
-  const uint32_t blk = blockIdx.x >> log_g, g = blockIdx.x & (G - 1);
-  const uint64_t rowb = (uint64_t)blk * 64 * B + (uint64_t)g * bpg;
-  for (uint32_t t = threadIdx.x; t < 64 * bpg; t += kB) {
-    const uint32_t slot = t / bpg, bl = t % bpg;
-    cur[slot * bpg + bl] = off[rowb + (uint64_t)slot * B + bl];
-  }
-  if (threadIdx.x < 64) {  // wave 0: the group's element count
-    uint32_t c = gcounts[((uint64_t)blk * 64 + threadIdx.x) * G + g];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if (threadIdx.x == 0) s_total = c;
-  }
-  __syncthreads();
-  const uint32_t base = cur[0];  // slot 0, first bucket: the group's first cell
-  const uint32_t total = s_total;
-  const bool local_ids = total <= kPlaceIds;
-  // a wave per slot run; each lane loads its (up to) four elements of the run
-  // before placing any, so a run of <= 256 elements is one round of loads (one
-  // dependent load per lane and iteration before: 119 us for config 4)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint32_t slot = wave; slot < 64; slot += kB / 64) {
-    const uint64_t gi = ((uint64_t)blk * 64 + slot) * G + g;
-    const uint32_t s0 = goff[gi], n = gcounts[gi];
-    for (uint32_t e0 = 0; e0 < n; e0 += 256) {
-      uint64_t v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t e = e0 + lane + 64 * u;
-        v[u] = e < n ? stage[s0 + e] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (e0 + lane + 64 * u >= n) continue;
-        const uint32_t bl = bucket_hash(v[u], log_b) - g * bpg;
-        const uint32_t d = atomicAdd(&cur[slot * bpg + bl], 1u);
-        out[d] = v[u];
-        if (local_ids) s_ids[d - base] = (uint8_t)slot;
-        else ids[d] = (uint8_t)slot;
-      }
-    }
-  }
-  if (!local_ids) return;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < total; i += kB) ids[base + i] = s_ids[i];
-}
-
 struct JoinArgs {
   JoinLayout r, c;  // row blocks (tile row I = block r_blk0 + I) and column blocks
   uint32_t r_blk0, c_blk0;  // (tile column J = block c_blk0 + J; uint32 arithmetic, -blk0 works)
@@ -1023,75 +811,6 @@ uint32_t join_log_b(uint32_t max_size) {
   return log_b;
 }
 
-// temp = counts[len] | off[len] | colsum[cells + 1] | bbase[cells + 1] | scan
-// temporaries, len = n_blk * 64 * B, cells = n_blk * B.
-// Coarse groups of the two-phase scatter: B / G <= 64 buckets each.
-static uint32_t layout_log_g(uint32_t log_b) { return log_b > 6 ? log_b - 6 : 0; }
-
-// temp = counts[len] | off[len] | colsum[cells + 1] | bbase[cells + 1] |
-// gcounts[glen] | goff[glen] | stage[total] (u64) | scan temporaries, with
-// len = n_blk * 64 * B, cells = n_blk * B, glen = n_blk * 64 * G.
-static size_t layout_head_bytes(uint64_t len, uint64_t cells, uint64_t glen, uint64_t total) {
-  const size_t u32s = ((2 * len + 2 * (cells + 1) + 2 * glen) * 4 + 15) & ~(size_t)15;
-  return u32s + ((std::max<uint64_t>(total, 1) * 8 + 15) & ~(size_t)15);
-}
-
-size_t join_layout_hash_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total) {
-  const uint64_t n_blk = (count + kTile - 1) / kTile;
-  const uint64_t cells = n_blk * (1ull << log_b), len = cells * 64;
-  const uint64_t glen = n_blk * 64 * (1ull << layout_log_g(log_b));
-  size_t scan = 0;
-  (void)rocprim::exclusive_scan(nullptr, scan, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                (size_t)(cells + 1), rocprim::plus<uint32_t>(), (hipStream_t)0);
-  return layout_head_bytes(len, cells, glen, total) + scan + 16;
-}
-
-hipError_t join_layout_build_hash(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                                  uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
-                             uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
-                             uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
-                             hipStream_t s) {
-  static const hipError_t attr_c = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(k_hb_count), hipFuncAttributeMaxDynamicSharedMemorySize,
-      (int)((1u << kJMaxLogB) * sizeof(uint32_t)));
-  if (attr_c != hipSuccess) return attr_c;
-  if (count == 0) return hipSuccess;
-  const uint32_t B = 1u << log_b, log_g = layout_log_g(log_b), G = 1u << log_g;
-  const uint32_t n_blk = (count + kTile - 1) / kTile;
-  const uint64_t cells = (uint64_t)n_blk * B, len = cells * 64, glen = (uint64_t)n_blk * 64 * G;
-  uint32_t* cnt = static_cast<uint32_t*>(temp);
-  uint32_t* off = cnt + len;
-  uint32_t* colsum = off + len;
-  uint32_t* bbase = colsum + (cells + 1);
-  uint32_t* gcnt = bbase + (cells + 1);
-  uint32_t* goff = gcnt + glen;
-  uint64_t* stage = reinterpret_cast<uint64_t*>(
-      static_cast<char*>(temp) + (((2 * len + 2 * (cells + 1) + 2 * glen) * 4 + 15) & ~(size_t)15));
-  const size_t head = layout_head_bytes(len, cells, glen, total);
-  if (temp_bytes < head) return hipErrorInvalidValue;
-  void* scan_tmp = static_cast<char*>(temp) + head;
-  size_t scan_bytes = temp_bytes - head;
-  hipError_t e;
-  // slots past `count` in the last block have no workgroup: zero counts
-  if ((e = hipMemsetAsync(cnt, 0, len * 4, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(gcnt, 0, glen * 4, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_hb_count, dim3(count), dim3(kB), B * 4, s, data, starts, sizes, first, first,
-                     B, log_b, cnt, G, gcnt);
-  hipLaunchKernelGGL(k_hb_colsum, dim3((unsigned)((cells + 1 + kB - 1) / kB)), dim3(kB), 0, s, cnt,
-                     n_blk, B, colsum);
-  if ((e = rocprim::exclusive_scan(scan_tmp, scan_bytes, colsum, bbase, 0u, (size_t)(cells + 1),
-                                   rocprim::plus<uint32_t>(), s)) != hipSuccess)
-    return e;
-  const uint64_t bcells = (uint64_t)n_blk * (B + 1);
-  hipLaunchKernelGGL(k_hb_offsets, dim3((unsigned)((bcells + kB - 1) / kB)), dim3(kB), 0, s, cnt,
-                     bbase, n_blk, B, off, out_boff, out_bstart, d_stat, G, gcnt, goff);
-  hipLaunchKernelGGL(k_hb_stage, dim3(count), dim3(kB), 0, s, data, starts, sizes, first, first,
-                     log_b, log_g, goff, stage);
-  hipLaunchKernelGGL(k_hb_place, dim3(n_blk * G), dim3(kB), 0, s, stage, off, goff, gcnt, B, log_b,
-                     log_g, out_data, out_ids);
-  return hipGetLastError();
-}
-
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
                        uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
@@ -1240,77 +959,8 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
 
   uint64_t total = 0;
   for (uint32_t i = 0; i < n; ++i) total += h_sizes[i];
-  const bool sep_rows_any = !sym && (row_begin % kTile) != 0;
-  if (algo == kIntersectPostings && total < (1ull << 32)) {
-    // block postings + MFMA counts (postings.hip).  The layout is checked after
-    // the join (its stat is read back with the counts); a build whose group
-    // outgrew the place kernel or whose bucket outgrew the join table is
-    // redone with twice the buckets, and past 2^14 the older kernels take over
-    const uint32_t rn = row_end - row_begin;
-    uint64_t r_total = 0;
-    if (sep_rows_any)
-      for (uint32_t i = row_begin; i < row_end; ++i) r_total += h_sizes[i];
-    for (uint32_t log_b = postings_log_b(max_size); log_b <= kJMaxLogB; ++log_b) {
-      const size_t oc = postings_bytes(n, log_b, total);
-      const size_t orr = sep_rows_any ? postings_bytes(rn, log_b, r_total) : 0;
-      const size_t tmp = std::max(postings_temp_bytes(n, log_b, total),
-                                  sep_rows_any ? postings_temp_bytes(rn, log_b, r_total) : 0);
-      const size_t o_r = align16(oc), o_st = o_r + align16(orr), o_tmp = o_st + 256;
-      if ((e = work.reserve(o_tmp + tmp)) != hipSuccess) return e;
-      char* w = static_cast<char*>(work.ptr);
-      uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_st);
-      if ((e = hipMemsetAsync(stat, 0, 8, s)) != hipSuccess) return e;
-      PostingsLayout cl{}, rl{};
-      if ((e = postings_build(data, starts, sizes, h_sizes.data(), 0, n, log_b, w, w + o_tmp, stat, &cl,
-                              s)) != hipSuccess)
-        return e;
-      rl = cl;
-      if (sep_rows_any &&
-          (e = postings_build(data, starts, sizes, h_sizes.data(), row_begin, rn, log_b, w + o_r,
-                              w + o_tmp, stat, &rl, s)) != hipSuccess)
-        return e;
-      const uint32_t r_blk0 = sep_rows_any ? 0 : (sym ? 0 : row_begin / kTile);
-      if ((e = postings_join(rl, r_blk0, cl, n, log_b, sym, row_begin, row_end, tile_begin, tile_end,
-                             nullptr, false, out, s)) != hipSuccess)
-        return e;
-      uint32_t h_stat[2] = {0, 0};
-      if ((e = pinned_d2h(h_stat, stat, 8, s)) != hipSuccess) return e;
-      if (dbg)
-        fprintf(stderr, "[sks intersect] postings n=%u log_b=%u max bucket %u group overflow %u\n", n,
-                log_b, h_stat[0], h_stat[1]);
-      if (h_stat[1] == 0 && h_stat[0] <= postings_max_distinct()) {
-        *used_tiles = true;
-        return hipSuccess;
-      }
-      if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
-    }
-  }
-  if (algo == kIntersectRange && total < (1ull << 32)) {
-    // range join (rjoin.hip): bounds, positions and column-block bucket starts
-    // only; the join reads the sketches where they lie
-    const uint32_t log_b = join_log_b(max_size), B = 1u << log_b;
-    const size_t o_bnd = 0, o_pos = align16((size_t)(B + 1) * 8);
-    const size_t o_pre = align16(o_pos + (size_t)n * (B + 1) * 4);
-    const size_t o_end = align16(o_pre + (size_t)n_cb * (B + 1) * 4);
-    if ((e = work.reserve(o_end)) != hipSuccess) return e;
-    char* w = static_cast<char*>(work.ptr);
-    uint64_t* bounds = reinterpret_cast<uint64_t*>(w + o_bnd);
-    uint32_t* pos = reinterpret_cast<uint32_t*>(w + o_pos);
-    uint32_t* pre = reinterpret_cast<uint32_t*>(w + o_pre);
-    if (dbg) fprintf(stderr, "[sks intersect] range join n=%u B=%u tiles=%llu\n", n, B, (unsigned long long)tiles);
-    if ((e = rjoin_bounds(data, starts, sizes, n, B, bounds, s)) != hipSuccess) return e;
-    if ((e = rjoin_pos(data, starts, sizes, n, B, bounds, pos, s)) != hipSuccess) return e;
-    if ((e = rjoin_block_prefix(pos, n, B, pre, s)) != hipSuccess) return e;
-    if ((e = rjoin_launch(data, starts, pos, pre, n, B, sym, row_begin, row_end, tile_begin, tile_end,
-                          nullptr, false, out, s)) != hipSuccess)
-      return e;
-    *used_tiles = true;
-    return hipSuccess;
-  }
-  // the join's per-(block, bucket, slot) counting arrays take 8 B x 64 x B per
-  // block; beyond a few GB of them (very many sketches) the merge tiles are used
-  const bool join_fits = total < (1ull << 32) &&
-                         join_layout_hash_temp_bytes(n, join_log_b(max_size), total) < (8ull << 30);
+  // the layout's bucket starts are u32 (< 2^32 elements per layout)
+  const bool join_fits = total < (1ull << 32);
   if (algo != kIntersectMerge && join_fits) {
     // hash-bucketed block-major copy of the column sketches (and of the row
     // range when its blocks are not aligned with the column blocks), then k_join
@@ -1322,10 +972,8 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     uint32_t log_b = join_log_b(max_size);
     for (;;) {
       const uint32_t B = 1u << log_b;
-      static const bool hash_layout = getenv("SKS_JOIN_HASH_LAYOUT") != nullptr;
-      const size_t tmp_c = hash_layout ? join_layout_hash_temp_bytes(n, log_b, total) : join_layout_temp_bytes(n, log_b);
-      const size_t tmp_r = !sep_rows ? 0 : hash_layout ? join_layout_hash_temp_bytes(rn, log_b, r_total)
-                                                       : join_layout_temp_bytes(rn, log_b);
+      const size_t tmp_c = join_layout_temp_bytes(n, log_b);
+      const size_t tmp_r = !sep_rows ? 0 : join_layout_temp_bytes(rn, log_b);
       size_t o = 0;
       const size_t o_cdat = o; o = align16(o + total * 8);
       const size_t o_cids = o; o = align16(o + total);
@@ -1348,15 +996,10 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       // a separate row layout shares the column set's group bounds; a single
       // layout computes its own in the build's first launch (three in all)
       uint64_t* gbounds = sep_rows ? reinterpret_cast<uint64_t*>(w + o_bnd) : nullptr;
-      if (!hash_layout && sep_rows && (e = join_layout_bounds(data, starts, sizes, n, log_b, gbounds, s)) != hipSuccess)
+      if (sep_rows && (e = join_layout_bounds(data, starts, sizes, n, log_b, gbounds, s)) != hipSuccess)
         return e;
       auto build_layout = [&](uint32_t first, uint32_t cnt, uint64_t tot, const JoinLayout& L,
                               size_t tmp_bytes) -> hipError_t {
-        if (hash_layout)
-          return join_layout_build_hash(data, starts, sizes, first, cnt, tot, log_b,
-                                        const_cast<uint64_t*>(L.data), const_cast<uint8_t*>(L.ids),
-                                        const_cast<uint32_t*>(L.boff), const_cast<uint64_t*>(L.bstart), stat,
-                                        w + o_tmp, tmp_bytes, s);
         return join_layout_build(data, starts + first, sizes + first, cnt, log_b, gbounds, w + o_tmp,
                                  const_cast<uint64_t*>(L.data), const_cast<uint8_t*>(L.ids),
                                  const_cast<uint32_t*>(L.boff), const_cast<uint64_t*>(L.bstart), stat, s);

@@ -155,9 +155,7 @@ constexpr int kIntersectAuto = 0;    // join when the bucket sizes allow, else m
 constexpr int kIntersectMerge = 1;   // k_tiles (pairwise LDS merges)
 constexpr int kIntersectJoin = 2;    // k_join (LDS hash join), merge tiles if infeasible
 constexpr int kIntersectGlobal = 3;  // one wavefront per pair from global memory
-constexpr int kIntersectPostings = 4;  // block postings join + MFMA counts (postings.hip)
 uint64_t intersect_sym_tiles(uint32_t n);
-constexpr int kIntersectRange = 5;     // k_rjoin: LDS hash join straight from the sorted sketches
 // Common value-range bucket bounds[0..B] (quantiles averaged over up to 64
 // sample sketches; any non-decreasing bounds give exact counts) and
 // pos[i][b] = first element of sketch i that is >= bounds[b] (pos[i][B] = size).
@@ -166,26 +164,6 @@ hipError_t launch_value_bounds(const uint64_t* data, const uint64_t* starts, con
 hipError_t launch_bucket_pos(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                              uint32_t n, uint32_t B, const uint64_t* bounds, uint32_t* pos,
                              hipStream_t s);
-
-// ---- range join (rjoin.hip) ---------------------------------------------------------------
-// Its "layout" is only the bucket positions of the sorted sketches: pos (above)
-// and, per 64-sketch column block, pre[blk][b] = sum of pos[i][b] over the
-// block's sketches (where bucket b starts in the block's concatenated order).
-// Rows are read through pos alone, so a row range need not be block-aligned.
-hipError_t rjoin_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes, uint32_t n,
-                        uint32_t B, uint64_t* bounds, hipStream_t s);
-hipError_t rjoin_pos(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes, uint32_t n,
-                     uint32_t B, const uint64_t* bounds, uint32_t* pos, hipStream_t s);
-hipError_t rjoin_block_prefix(const uint32_t* pos, uint32_t n, uint32_t B, uint32_t* pre, hipStream_t s);
-// Tiles of the n x n matrix (sym: upper-triangle tiles [tile_begin, tile_end),
-// or with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
-// written) or rows [row_begin, row_end) x n (sym false, d_tiles null).
-// packed: out = [tile - tile_begin][64][64] instead of the matrix.  Counts are
-// added: `out` must be zeroed.  All element offsets (starts + pos) < 2^32.
-hipError_t rjoin_launch(const uint64_t* data, const uint64_t* starts, const uint32_t* pos,
-                        const uint32_t* pre, uint32_t n, uint32_t B, bool sym, uint32_t row_begin,
-                        uint32_t row_end, uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles,
-                        bool packed, int32_t* out, hipStream_t s);
 
 // Join layout (input of k_join, intersect.hip): blocks of 64 consecutive
 // sketches, elements hash-bucketed into B = 2^log_b buckets and stored block-major.
@@ -215,14 +193,6 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
                              uint32_t count, uint32_t log_b, const uint64_t* d_bounds, void* temp,
                              uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
                              uint64_t* out_bstart, uint32_t* d_stat, hipStream_t s);
-// the round-2 all-hash build (intersect.hip k_hb_*): six launches; measured
-// against join_layout_build with SKS_JOIN_HASH_LAYOUT
-size_t join_layout_hash_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total);
-hipError_t join_layout_build_hash(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                                  uint32_t first, uint32_t count, uint64_t total, uint32_t log_b,
-                                  uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
-                                  uint64_t* out_bstart, uint32_t* d_stat, void* temp, size_t temp_bytes,
-                                  hipStream_t s);
 // Tiles of the n x n (sym: upper-triangle range [tile_begin, tile_end), or
 // with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
 // written) or rows x n matrix; tile (I, J) reads row block r_blk0 + I of
@@ -233,35 +203,6 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
                        uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
                        int32_t* out, hipStream_t s);
-
-// Block postings (postings.hip): per 64-sketch block and hash bucket, the
-// distinct values with a 64-bit mask of the block's sketches holding each,
-// every bucket with a precomputed linear-probing table position per posting.
-struct PostingsLayout {
-  const uint64_t* ent;     // {value, mask} pairs
-  const uint16_t* pos;     // slot of each posting in its bucket's table (2 slots per posting)
-  const uint32_t* bkt;     // [blk][B][2] = {first posting relative to bstart[blk], count}
-  const uint64_t* bstart;  // [n_blk + 1] first posting slot of each block
-};
-uint32_t postings_log_b(uint32_t max_size);
-uint32_t postings_max_distinct();  // largest bucket (postings) the join takes
-size_t postings_bytes(uint32_t count, uint32_t log_b, uint64_t total);       // the layout
-size_t postings_temp_bytes(uint32_t count, uint32_t log_b, uint64_t total);  // build scratch
-// Layout of sketches [first, first + count) (h_sizes: host copy of all sizes)
-// into `out` (postings_bytes); d_stat[0] is raised to the largest bucket,
-// d_stat[1] to the largest (block, group) element count when one exceeded the
-// build's capacity (then the layout is invalid: raise log_b).
-hipError_t postings_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                          const uint32_t* h_sizes, uint32_t first, uint32_t count, uint32_t log_b,
-                          void* out, void* temp, uint32_t* d_stat, PostingsLayout* L, hipStream_t s);
-// Tiles of the n x n (sym) or rows x n matrix, or the explicit (I, J) list
-// d_tiles[2t], d_tiles[2t + 1] for t in [tile_begin, tile_end) (written to
-// both halves, like sym); packed: out = [tile - tile_begin][64][64] partial
-// counts instead of the matrix.  `out` must be zeroed.
-hipError_t postings_join(const PostingsLayout& rows, uint32_t r_blk0, const PostingsLayout& cols,
-                         uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
-                         uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles,
-                         bool packed, int32_t* out, hipStream_t s);
 
 // ---- device FASTA ingress (ingress.hip) -------------------------------------------------
 // strings_from_fasta on the device: writes the host parser's record stream

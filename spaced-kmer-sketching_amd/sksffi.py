@@ -15,8 +15,7 @@ LIB_PATH = os.environ.get("SKS_LIB") or os.path.join(PKG_DIR, "lib", "libsks.so"
 
 SKS_FRAC_MOD = 0
 SKS_BOTTOM_S = 1
-INTERSECT_AUTO, INTERSECT_MERGE, INTERSECT_JOIN, INTERSECT_GLOBAL, INTERSECT_POSTINGS = 0, 1, 2, 3, 4
-INTERSECT_RANGE = 5
+INTERSECT_AUTO, INTERSECT_MERGE, INTERSECT_JOIN, INTERSECT_GLOBAL = 0, 1, 2, 3
 FLAVOUR_BOOST_MIX = 0
 FLAVOUR_BOOST_LEGACY = 1
 
@@ -60,7 +59,7 @@ EXPORTED = [
     "sks_kmer_list_counts", "sks_kmer_list_device_positions", "sks_kmer_list_device_bits",
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
     "sks_sketch_set_name", "sks_sketch_set_save", "sks_sketch_set_load", "sks_sketch_set_concat",
-    "sks_range_log_b", "sks_range_bounds", "sks_intersect_range", "sks_intersect_layout_tiles",
+    "sks_intersect_layout_tiles",
     "sks_join_layout_bounds", "sks_join_layout_groups",
 ]
 
@@ -129,11 +128,6 @@ def lib():
                                            C.c_uint64, vp]
     L.sks_intersect_layout_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp,
                                              C.c_uint64, C.c_uint64, C.c_int, vp]
-    L.sks_range_log_b.argtypes = [C.c_uint32]
-    L.sks_range_log_b.restype = C.c_uint32
-    L.sks_range_bounds.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp]
-    L.sks_intersect_range.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, C.c_uint64,
-                                      C.c_uint64, C.c_int, vp]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_device.argtypes = [vp]
@@ -221,10 +215,6 @@ def join_layout_capacity():
 
 def join_layout_groups(log_b):
     return int(lib().sks_join_layout_groups(log_b))
-
-
-def range_log_b(max_sketch_size):
-    return int(lib().sks_range_log_b(max_sketch_size))
 
 
 def intersect_sym_tiles(n):
@@ -353,20 +343,6 @@ class Context:
                                              C.c_void_p(boff), C.c_void_p(bstart), tile_begin,
                                              tile_end, C.c_void_p(out)))
 
-    def range_bounds(self, data, starts, sizes, n, log_b, bounds):
-        """sks_range_bounds (device pointers): value-range bucket bounds of the set."""
-        check(lib().sks_range_bounds(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes), n,
-                                     log_b, C.c_void_p(bounds)))
-
-    def intersect_range(self, data, starts, sizes, n, log_b, bounds, tiles, tile_begin, tile_end,
-                        packed, out):
-        """sks_intersect_range: tile counts ADDED to `out` (n x n both halves, or packed
-        [tile][64][64]); tiles: device pointer of (I, J) u32 pairs, or 0 for the
-        upper-triangle range."""
-        check(lib().sks_intersect_range(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes),
-                                        n, log_b, C.c_void_p(bounds), C.c_void_p(tiles) if tiles else None,
-                                        tile_begin, tile_end, 1 if packed else 0, C.c_void_p(out)))
-
     def intersect_layout_tiles(self, n, log_b, data, ids, boff, bstart, blk0, tiles, tile_begin, tile_end,
                                packed, out):
         """sks_intersect_layout_tiles: join tiles over a layout whose block 0 is
@@ -378,7 +354,7 @@ class Context:
                                                1 if packed else 0, C.c_void_p(out)))
 
     def set_intersect_kernel(self, kind):
-        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL / _POSTINGS / _RANGE (sks.h); all give identical counts."""
+        """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL (sks.h); all give identical counts."""
         check(lib().sks_ctx_set_intersect_kernel(self.h, kind))
         self._intersect_kernel = kind
 

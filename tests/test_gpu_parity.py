@@ -496,7 +496,7 @@ def test_argument_errors(torch_cuda, ctx):
 
 
 KERNELS = [sksffi.INTERSECT_AUTO, sksffi.INTERSECT_MERGE, sksffi.INTERSECT_JOIN,
-           sksffi.INTERSECT_GLOBAL, sksffi.INTERSECT_POSTINGS, sksffi.INTERSECT_RANGE]
+           sksffi.INTERSECT_GLOBAL]
 
 
 @pytest.fixture
@@ -822,56 +822,6 @@ def test_wide_all_vs_all_rows_path(torch_cuda, ctx):
     assert np.array_equal(got, want)
 
 
-def test_range_join_tile_lists_and_packed(torch_cuda, ctx):
-    """sks_intersect_range with explicit (I, J) tile lists and packed output:
-    every tile equals the corresponding 64 x 64 block of sks_intersect_sym's
-    matrix (merge tiles); the dense form adds both halves; a tile list in two
-    calls (as a rank's local and remote tiles) adds up to the same; bounds from
-    a different subset of sketches (any non-decreasing bounds are exact)."""
-    torch = torch_cuda
-    n = 200
-    genomes = [synth.bases(15000, seed=60 + i % 6, mut_seed=700 + i, mut_rate=0.004 * (i % 9)).tobytes()
-               for i in range(n)]
-    m = O.mask(31, 21, 4)
-    ss, _dev = build(torch, ctx, genomes, 31, m, "bottom", 700)
-    d, st, sz = ss.device_ptrs()
-    ref = torch.zeros((n, n), dtype=torch.int32, device="cuda")
-    ctx.set_intersect_kernel(sksffi.INTERSECT_MERGE)
-    ctx.intersect_sym(d, st, sz, 1, n, 0, sksffi.intersect_sym_tiles(n), ref.data_ptr())
-    ctx.set_intersect_kernel(sksffi.INTERSECT_AUTO)
-    torch.cuda.synchronize()
-    ref = ref.cpu()
-    log_b = sksffi.range_log_b(int(ss.sizes().max()))
-    bounds = torch.empty((1 << log_b) + 1, dtype=torch.int64, device="cuda")
-    ctx.range_bounds(d, st, sz, n, log_b, bounds.data_ptr())
-    nb = (n + 63) // 64
-    tiles = [(I, J) for I in range(nb) for J in range(I, nb)][::-1]
-    tl = torch.tensor(tiles, dtype=torch.int32, device="cuda")
-    packed = torch.zeros((len(tiles), 64, 64), dtype=torch.int32, device="cuda")
-    ctx.intersect_range(d, st, sz, n, log_b, bounds.data_ptr(), tl.data_ptr(), 0, 3, True, packed.data_ptr())
-    ctx.intersect_range(d, st, sz, n, log_b, bounds.data_ptr(), tl.data_ptr(), 3, len(tiles), True,
-                        packed[3:].data_ptr())
-    dense = torch.zeros((n, n), dtype=torch.int32, device="cuda")
-    ctx.intersect_range(d, st, sz, n, log_b, bounds.data_ptr(), 0, 0, sksffi.intersect_sym_tiles(n), False,
-                        dense.data_ptr())
-    torch.cuda.synchronize()
-    assert torch.equal(dense.cpu(), ref)
-    pk = packed.cpu()
-    for t, (I, J) in enumerate(tiles):
-        blk = ref[I * 64:I * 64 + 64, J * 64:J * 64 + 64]
-        assert torch.equal(pk[t, :blk.shape[0], :blk.shape[1]], blk), (I, J)
-        assert int(pk[t].sum()) == int(blk.sum())
-    # bounds from the last 20 sketches only
-    st_t = torch.as_tensor(ss.starts().astype(np.int64), device="cuda")
-    sz_t = torch.as_tensor(ss.sizes().astype(np.int32), device="cuda")
-    ctx.range_bounds(d, st_t[180:].data_ptr(), sz_t[180:].data_ptr(), 20, log_b, bounds.data_ptr())
-    dense.zero_()
-    ctx.intersect_range(d, st, sz, n, log_b, bounds.data_ptr(), 0, 0, sksffi.intersect_sym_tiles(n), False,
-                        dense.data_ptr())
-    torch.cuda.synchronize()
-    assert torch.equal(dense.cpu(), ref)
-
-
 def test_join_layout_tiles_block_offset_and_packed(torch_cuda, ctx):
     """sks_intersect_layout_tiles on the layout of a rank's own blocks (global
     blocks 1-3 of 200 sketches, built from the sketch range 64..199, blk0 = 1)
@@ -948,7 +898,7 @@ def scale_sets(torch_cuda, ctx):
     return n, sets
 
 
-@pytest.mark.parametrize("kernel_ctx", [sksffi.INTERSECT_JOIN, sksffi.INTERSECT_RANGE], indirect=True)
+@pytest.mark.parametrize("kernel_ctx", [sksffi.INTERSECT_JOIN], indirect=True)
 @pytest.mark.parametrize("mode", ["indep", "family"])
 def test_join_exact_at_scale(torch_cuda, kernel_ctx, scale_sets, mode):
     """~10^8 hash-table inserts per all-pairs call (1000 sketches of 10000):

@@ -38,8 +38,7 @@ def main():
     data, starts, sizes = ss.device_ptrs()
     T = sksffi.intersect_sym_tiles(n)
     ref = None
-    kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN),
-               ("postings", sksffi.INTERSECT_POSTINGS), ("range", sksffi.INTERSECT_RANGE))
+    kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN))
     only = os.environ.get("SKS_BENCH_KERNELS")
     if only:
         kernels = tuple(x for x in kernels if x[0] in only.split(","))
