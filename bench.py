@@ -17,12 +17,15 @@ Genomes are independent, so ranks shard them with no collective: weak scaling.
 
 Secondary (`pairs`): genome-pairs ANI/s on config 4 (1000 x 5 Mb genomes =
 10 ancestors x 100 mutated descendants, w=31/k=21, bottom-s s=10000), strong
-scaling: rank r sketches its share of genomes, the padded sketches are
-all-gathered over RCCL (torch.distributed "nccl"), rank r counts the
-intersections of its share of the upper-triangle 64x64 tiles of the N x N
-matrix (each count written to both halves), and the partial matrices are
-summed with an RCCL all-reduce; containment and ANI for every ordered pair
-are computed on the host from the exact counts.
+scaling.  A pair step is what the reference's "Time taken for comparison"
+covers (kmer-sketching.cpp:185-203): every ordered pair's intersection count,
+containment and ANI, with the ANI delivered to host memory.  Rank r owns whole
+64-genome blocks, sketches them and builds their join layout; every rank's
+sketches are broadcast by their owner over RCCL (torch.distributed "nccl") and
+each rank joins its blocks with a source's as they land (a fixed plan splits
+the upper-triangle 64x64 tiles); containment and ANI are computed on the
+device per tile and copied to the rank's host memory.  At N = 1 the counts go
+straight into the n x n matrix and the ANI matrix (8 MB) is read back.
 
 `cpu_baseline`: the reference-faithful CPU port (oracle/ref_port.cpp, see
 BASELINE.md) timed on this box's host cores on a bounded sample of the same
@@ -654,20 +657,28 @@ def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100):
     kmer_sets, probe-the-larger intersection, threads over pairs like the
     reference's cilk_for, kmer_set.cpp:23-41,167-184) over all ordered pairs of
     the first `n_sets` config-4 genomes' sketches (same family: sharing is high).
-    Counts are checked against the GPU matrix."""
+    Then containment + ANI per ordered pair, serially like the reference's
+    loop (kmer-sketching.cpp:195-200, ani_estimation.cpp:24-42), inside the
+    clock.  Counts are checked against the GPU matrix."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     T = cpu_threads()
     ss = ctx.sketch_build(buf.data_ptr(), seg[n_sets], seg[:n_sets + 1], W, mask,
                           sksffi.SKS_BOTTOM_S, C4_S)
     sets = [pyoracle.refport_set_from_elems(ss.sketch(i), W, mask) for i in range(n_sets)]
+    ones = bin(mask).count("1") // 2
     t0 = time.perf_counter()
     got = pyoracle.refport_all_pairs(sets, threads=T)
+    sz = np.diag(got)
+    ani = [pyoracle.binomial_estimator(pyoracle.containment(int(got[i, j]), int(sz[i])), ones)
+           for i in range(n_sets) for j in range(n_sets)]
     dt = time.perf_counter() - t0
     assert np.array_equal(got, counts[:n_sets, :n_sets])
-    return {"value": n_sets * n_sets / dt, "unit": "ordered pairs/s", "cores": T, "kind": "port",
+    del ani
+    return {"value": n_sets * n_sets / dt, "unit": "ordered pairs/s (count + containment + ANI)", "cores": T,
+            "kind": "port",
             "sample": f"all {n_sets}x{n_sets} ordered pairs of the first {n_sets} genomes "
-                      f"(s={C4_S}), oracle/ref_port.cpp, {T} threads over pairs, {dt:.2f} s; "
+                      f"(s={C4_S}), oracle/ref_port.cpp, {T} threads over pairs + serial ANI, {dt:.2f} s; "
                       f"counts equal the GPU's",
             "host": host_info(T)}
 
@@ -692,6 +703,11 @@ def cpu_baseline_c4_sketch(ctx, buf, seg, mask):
 
 
 def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
+    """Config 4 all-vs-all.  Timed per step: the sketch phase (every rank's
+    genomes), then the pair phase = counts for every ordered pair + containment
+    and ANI on the device + the ANI copied into pinned host memory (the whole
+    "comparison" of kmer-sketching.cpp:185-203).  A second pass times the counts
+    alone (layout + join, no ANI) for the fixed-cost figure."""
     import sks_dist
     _, g0, g1 = sks_dist.block_shard(C4_GENOMES, world, rank)
     n_local = g1 - g0
@@ -704,34 +720,36 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         ctx.synth_bases(buf.data_ptr() + seg[i], C4_LEN, anc_seed, mut_seed, rate)
         buf[seg[i] + C4_LEN] = ord("\n")
     torch.cuda.synchronize()
-    mat = torch.empty((C4_GENOMES, C4_GENOMES), dtype=torch.int32, device="cuda")
-    dev = "cuda" if os.environ.get("SKS_BENCH_DEVICE") is None else "cpu"
+    ones = bin(mask).count("1") // 2
+    ops = sks_dist.GpuJoinOps(ctx)
+    host_ani = None  # pinned, sized on the first step
 
-    lay_bufs = {}  # join layout buffers, reused across steps
+    def pair_step(ss, with_ani=True):
+        nonlocal host_ani
+        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss), ops,
+                                       sksffi.join_layout_log_b, device="cuda", dst=None,
+                                       ani_ones=ones if with_ani else None)
+        if with_ani:
+            flat = res.ani.reshape(-1)
+            if host_ani is None or host_ani.numel() != flat.numel():
+                host_ani = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
+            host_ani.copy_(flat, non_blocking=True)
+        return res
 
-    t_sketch = t_pairs = 0.0
+    t_sketch = t_pairs = t_counts = 0.0
     timed = 0
-    res = None
+    res = ss = None
+    sizes = np.zeros(0, np.uint32)
     for it in range(warmup + steps):
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ss = None
-        local_sizes = np.zeros(0, np.uint32)
         if n_local:
             ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, C4_S)
-            local_sizes = ss.sizes().copy()
-        local_max = int(local_sizes.max()) if n_local else 0
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        # layouts of this rank's blocks, built into send buffers padded to the
-        # largest rank's total; the rank's own tiles counted while the layouts
-        # are all-gathered, then its cross-rank tiles; packed tiles to rank 0
-        build, count, bounds = sks_dist.join_layout_fns(ctx, ss, local_sizes, device=dev, cache=lay_bufs)
-        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, local_max,
-                                       int(local_sizes.astype(np.int64).sum()), sksffi.join_layout_log_b,
-                                       build, count, device=dev, out=mat if dev == "cuda" else None, dst=0,
-                                       bounds=bounds)
+        res = pair_step(ss)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         ts, tp = max_over_ranks(t1 - t0, world), max_over_ranks(t2 - t1, world)
@@ -739,54 +757,75 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
             t_sketch += ts
             t_pairs += tp
             timed += 1
-        del ss
-    if res is not None and dev != "cuda":
-        mat.copy_(res)
-    # containment + ANI for every ordered pair (host, double, from exact counts;
-    # kmer-sketching.cpp:195-200 with the first set of the pair as denominator)
-    # (the matrix exists on rank 0 only: the packed tiles were gathered there)
-    k_ms = ctx.last_intersect_ms()
+    k_ms = ctx.last_intersect_ms()  # the rank's last join launch (all tiles at N = 1)
+    sizes = ss.sizes().copy() if ss is not None else sizes
+    # counts alone (the fixed-cost figure: pair phase minus the join kernel)
+    for it in range(1 + steps):
+        barrier(world)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        pair_step(ss, with_ani=False)
+        torch.cuda.synchronize()
+        tc = max_over_ranks(time.perf_counter() - t1, world)
+        if it >= 1:
+            t_counts += tc
     t_sketch /= max(timed, 1)
     t_pairs /= max(timed, 1)
-    counts, ani = None, np.zeros(1)
-    if rank == 0:
-        counts = mat.cpu().numpy()
-        sizes = np.diag(counts).astype(np.int32)  # |S_i ∩ S_i| = |S_i|
-        size_first = np.repeat(sizes, C4_GENOMES)
-        kmer_ones = bin(mask).count("1") // 2
-        _, ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, kmer_ones)
+    t_counts /= max(steps, 1)
+    ani_mean = None
+    counts = None
+    if world == 1:
+        counts = res.matrix.cpu().numpy()
         assert (counts == counts.T).all() and counts[0, 1] > 0
-        assert (sizes[g0:g1] == local_sizes[:n_local]).all()
+        assert (np.diag(counts) == sizes).all()
+        ani = host_ani.numpy().reshape(C4_GENOMES, C4_GENOMES)
+        # the device ANI against the host's (kmer-sketching.cpp:195-200 on the exact counts)
+        size_first = np.repeat(np.diag(counts).astype(np.int32), C4_GENOMES)
+        _, h_ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones)
+        ani_err = float(np.abs(ani.reshape(-1) - h_ani).max())
+        assert ani_err <= 1e-9, ani_err
+        ani_mean = float(ani.mean())
+    else:
+        ani_err = None
+        # ANI sum over every ordered pair, from the tiles' two orientations (a
+        # diagonal tile's second block repeats its first)
+        a = res.ani.cpu().numpy()
+        tl = np.asarray(res.tiles).reshape(-1, 2)
+        tot = float(a[:, 0].sum()) + float(a[tl[:, 0] != tl[:, 1], 1].sum())
+        ani_mean = sum_over_ranks(tot, world) / (C4_GENOMES * C4_GENOMES)
     cpu = cpu_sk = None
     if cpu_pairs and rank == 0 and world == 1:
         cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
         cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask)
+    ani_bytes = (C4_GENOMES * C4_GENOMES * 8) if world == 1 else int(res.ani.numel()) * 8
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
-        "unit": "ordered pairs/s", "scaling": "strong",
+        "unit": "ordered pairs/s (count + containment + ANI, ANI in host memory)", "scaling": "strong",
         "ms_pair_phase": t_pairs * 1e3, "ms_sketch_phase": t_sketch * 1e3,
-        "pair_kernel_ms_rank0": k_ms,  # the rank's last join launch (all tiles at N = 1)
+        "ms_counts_phase": t_counts * 1e3,
+        "pair_kernel_ms_rank0": k_ms,
+        "fixed_cost_ms": (t_counts * 1e3 - k_ms) if k_ms else None,
+        "ani_readback_bytes_rank0": ani_bytes,
+        "ani_max_abs_err_vs_host": ani_err,
         # streamed-equivalent bytes of the pair kernel, 8 B per
         # element of both sets + 4 B per count, for every ordered pair this rank's
-        # tiles cover (symmetric tiles give both halves); the join reads each
-        # sketch from the layout once per tile row / column (LDS / L2 reuse), so
-        # this figure can exceed what HBM moves — it is labelled, not an HBM claim
+        # tiles cover; a measure of reuse, not an HBM claim (the join is bound by
+        # LDS round trips: see pairs_lds in the round's profile)
         "roofline_streamed_equivalent": {
             "bytes_per_pair": 8 * 2 * C4_S + 4,
             "pairs_this_rank": C4_GENOMES * C4_GENOMES / world,
             "achieved_GBps": (8 * 2 * C4_S + 4) * C4_GENOMES * C4_GENOMES / world / (k_ms * 1e-3) / 1e9
-            if k_ms else None,
-            "hbm_peak_GBps": HBM_PEAK_GBS},
+            if k_ms else None},
         "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - W + 1) / t_sketch,
-        "ani_mean_all_pairs": float(np.mean(ani)),
+        "ani_mean_all_pairs": ani_mean,
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
                    "genome_len": C4_LEN, "s": C4_S, "w": W, "k": K,
                    "pair_sharding": "block-aligned genomes per rank; tile plan: the rank's own "
-                                    "blocks' 64x64 join tiles (counted while the layouts are "
-                                    "gathered) + half of every cross-rank block pair",
-                   "collective": ("all_reduce MAX (largest sketch, element total) + "
-                                  "all_gather_into_tensor join layouts + gather of packed tiles "
-                                  f"to rank 0 ({backend_label()})" if collective() else "none")},
+                                    "blocks' 64x64 join tiles, then half of every cross-rank block "
+                                    "pair as the peer's sketches land",
+                   "collective": ("all_gather of (genomes, elements, largest sketch) + broadcast of "
+                                  "rank 0's group bounds + one broadcast of sketches and sizes per "
+                                  f"source rank ({backend_label()})" if collective() else "none")},
         "cpu_baseline": cpu,
         "cpu_baseline_sketch_phase": cpu_sk,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),

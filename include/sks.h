@@ -22,7 +22,8 @@
 extern "C" {
 #endif
 
-#define SKS_ABI_VERSION 1
+#define SKS_ABI_VERSION 2  /* 2: deduplicated join layout (masks, region ends), elem_words on
+                              the layout entry points, sks_ctx_set_join_check */
 
 typedef enum sks_status {
   SKS_OK = 0,
@@ -248,62 +249,103 @@ int sks_sketch_union_wide(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64
 
 /* ---- join layout: all-vs-all across GPUs ------------------------------------------------
  * The all-pairs join kernel (sks_intersect_all / _sym, SKS_INTERSECT_JOIN) reads
- * a "join layout": blocks of 64 consecutive sketches, their u64 elements
- * bucketed into 2^log_b buckets and stored block-major.  Buckets are two-level:
- * G = sks_join_layout_groups(log_b) value groups cut by bounds u64[G + 1]
- * (non-decreasing, bounds[0] = 0, bounds[G] = 2^64 - 1), each split into 16 (or
- * 2^log_b when log_b < 4) hash buckets.  Exposing the layout lets a multi-GPU
- * caller build the layout of its own sketches only and all-gather layouts
- * instead of raw sketches (no replicated build):
- *   data   u64[total]            elements, block-major (total = sum of sizes)
- *   ids    u8[total]             slot of each element's sketch in its block
- *   boff   u32[nb * (2^log_b+1)] bucket starts inside each block (nb = ceil(n/64))
- *   bstart u64[nb + 1]           first element of each block in data/ids; [nb] = total
+ * a "join layout": blocks of 64 consecutive sketches, each DISTINCT value of a
+ * block stored once with a 64-bit mask of the block's sketches holding it
+ * (bit s = sketch 64 * block + s).  Buckets are two-level: G =
+ * sks_join_layout_groups(log_b) value groups cut by bounds (G + 1 values of
+ * elem_words words each, non-decreasing, bounds[0] = 0, bounds[G] = the
+ * largest value), each split into 8 (or 2^log_b when log_b < 3) hash buckets;
+ * 8 consecutive groups form a region (NR = regions per block).  A region's
+ * entries start at its raw offset in the block (the block's sketch elements in
+ * earlier regions), so its tail up to the next region is unused.  Exposing the
+ * layout lets a multi-GPU caller build the layout of its own sketches only and
+ * all-gather layouts instead of raw sketches (no replicated build):
+ *   vals   u64[total * elem_words]  entry values, block-major (total = sum of sizes)
+ *   masks  u64[total]               sketch mask of each entry
+ *   boff   u32[nb * sks_join_layout_boff_words(log_b)]  per block (nb = ceil(n/64)):
+ *          2^log_b bucket starts, then NR region ends, relative to bstart[block]
+ *   bstart u64[nb + 1]              raw block starts (prefix of the sizes); [nb] = total
  * Layouts of consecutive sketch ranges that each start at a multiple of 64 can
- * be concatenated (append data/ids/boff and add the data offset to bstart) when
- * they were built with the same bounds. */
+ * be concatenated (append vals/masks/boff and add the data offset to bstart)
+ * when they were built with the same bounds.  elem_words: 1 (u64 k-mers,
+ * w <= 32) or 2 ((lo, hi) k-mers, 32 < w <= 64). */
 /* log_b for a largest sketch of max_sketch_size elements (all ranks must agree). */
 uint32_t sks_join_layout_log_b(uint32_t max_sketch_size);
-/* Block-bucket population one join chunk holds; larger buckets are joined in
- * sub-chunks (exact, slower). */
+/* Block-bucket population (entries) one join chunk holds; larger buckets are
+ * joined in sub-chunks (exact, slower). */
 uint32_t sks_join_layout_capacity(void);
-/* Value groups of a layout with 2^log_b buckets (bounds hold groups + 1 words). */
+/* Value groups of a layout with 2^log_b buckets (bounds hold groups + 1 values). */
 uint32_t sks_join_layout_groups(uint32_t log_b);
+/* Words of one block's boff row: 2^log_b bucket starts + the region ends. */
+uint32_t sks_join_layout_boff_words(uint32_t log_b);
 /* Group bounds balanced for the set (quantiles averaged over up to 64 sample
  * sketches), queued on the context stream.  Any bounds give exact counts. */
 int sks_join_layout_bounds(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
-                           const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_bounds);
-/* Builds the layout of sketches (d_data, d_starts, d_sizes)[0, n) (u64 elements)
- * into caller buffers (two launches).  d_bounds: the group bounds (NULL: the
- * set's own, sks_join_layout_bounds).  *max_block_bucket (host) receives the
- * largest block-bucket population (waits for the build); NULL skips that
- * read-back.  total_hint: the n sizes' sum when the caller knows it (the build
- * then never waits for the stream), UINT64_MAX to have the sizes read back. */
+                           const uint32_t* d_sizes, int elem_words, uint32_t n, uint32_t log_b,
+                           uint64_t* d_bounds);
+/* Builds the layout of sketches (d_data, d_starts, d_sizes)[0, n) into caller
+ * buffers (three launches: bounds + block starts, group positions, placement).
+ * d_bounds: the group bounds (NULL: the set's own, sks_join_layout_bounds).
+ * *max_block_bucket (host) receives the largest block-bucket population in
+ * entries, or UINT32_MAX when the build could not place a group (only for
+ * adversarial 128-bit values; the layout is then invalid) — it waits for the
+ * build; NULL skips that read-back.  total_hint: the n sizes' sum when the
+ * caller knows it (the build then never waits for the stream), UINT64_MAX to
+ * have the sizes read back. */
 int sks_join_layout_build(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
-                          const uint32_t* d_sizes, uint32_t n, uint64_t total_hint, uint32_t log_b,
-                          const uint64_t* d_bounds, uint64_t* d_out_data, uint8_t* d_out_ids,
-                          uint32_t* d_out_boff, uint64_t* d_out_bstart, uint32_t* max_block_bucket);
+                          const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t total_hint,
+                          uint32_t log_b, const uint64_t* d_bounds, uint64_t* d_out_vals,
+                          uint64_t* d_out_masks, uint32_t* d_out_boff, uint64_t* d_out_bstart,
+                          uint32_t* max_block_bucket);
 /* sks_intersect_sym over a join layout of n sketches: upper-triangle 64x64 tiles
  * [tile_begin, tile_end) into the n x n int32 matrix d_out (zeroed first). */
-int sks_intersect_sym_layout(sks_ctx* ctx, uint32_t n, uint32_t log_b, const uint64_t* d_data,
-                             const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+int sks_intersect_sym_layout(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_words, const uint64_t* d_vals,
+                             const uint64_t* d_masks, const uint32_t* d_boff, const uint64_t* d_bstart,
                              uint64_t tile_begin, uint64_t tile_end, int32_t* d_out);
 
 /* Tiles of the n x n matrix over a join layout whose block 0 is global block
  * blk0 (a rank's own blocks, or a gathered layout with blk0 = 0); every tile's
  * two blocks must lie in the layout.  Tiles: d_tiles == NULL -> upper-triangle
- * tiles [tile_begin, tile_end) (row-major, sks_intersect_sym_tiles); else the
- * list d_tiles[2t] = I, d_tiles[2t + 1] = J (I <= J, global block indices) for
- * t in [tile_begin, tile_end).  packed == 0: counts are ADDED to the n x n int32
- * matrix d_out at (i, j) and (j, i); packed != 0: to
- * d_out[(t - tile_begin) * 4096 + r * 64 + c] for row I*64 + r, column J*64 + c
- * (a diagonal tile holds both triangles).  The caller zeroes d_out.  A
- * multi-GPU caller counts the tiles of its own blocks on its own layout while
- * the others' layouts are still being gathered. */
-int sks_intersect_layout_tiles(sks_ctx* ctx, uint32_t n, uint32_t log_b, const uint64_t* d_data,
-                               const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+ * tiles [tile_begin, tile_end) (row-major, sks_intersect_sym_tiles; blk0 must
+ * be 0, else SKS_E_ARG); else the list d_tiles[2t] = I, d_tiles[2t + 1] = J
+ * (I <= J, global block indices) for t in [tile_begin, tile_end).  packed == 0:
+ * counts are ADDED to the n x n int32 matrix d_out at (i, j) and (j, i);
+ * packed != 0: to d_out[(t - tile_begin) * 4096 + r * 64 + c] for row I*64 + r,
+ * column J*64 + c (a diagonal tile holds both triangles).  The caller zeroes
+ * d_out.  A multi-GPU caller counts the tiles of its own blocks on its own
+ * layout while the others' layouts are still being gathered. */
+int sks_intersect_layout_tiles(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_words, const uint64_t* d_vals,
+                               const uint64_t* d_masks, const uint32_t* d_boff, const uint64_t* d_bstart,
                                uint32_t blk0, const uint32_t* d_tiles, uint64_t tile_begin,
                                uint64_t tile_end, int packed, int32_t* d_out);
+
+/* sks_intersect_layout_tiles with the row blocks and the column blocks in two
+ * layouts (built with the same bounds): tile (I, J) of the list joins row block
+ * I of the row layout (whose block 0 is global block r_blk0) with column block
+ * J of the column layout (block 0 = c_blk0).  A multi-GPU caller joins its own
+ * layout with each peer's as the peer's sketches arrive. */
+int sks_intersect_layout_pair_tiles(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_words,
+                                    const uint64_t* d_rvals, const uint64_t* d_rmasks, const uint32_t* d_rboff,
+                                    const uint64_t* d_rbstart, uint32_t r_blk0, const uint64_t* d_cvals,
+                                    const uint64_t* d_cmasks, const uint32_t* d_cboff, const uint64_t* d_cbstart,
+                                    uint32_t c_blk0, const uint32_t* d_tiles, uint64_t tile_begin,
+                                    uint64_t tile_end, int packed, int32_t* d_out);
+/* The set's sketches back to back (sizes[i] * elem_words words each, in order)
+ * and its sizes, copied into caller device buffers (a send buffer). */
+int sks_sketch_set_export_csr(const sks_sketch_set* set, uint64_t* d_data, uint32_t* d_sizes);
+
+/* ---- containment / ANI on the device: kmer-sketching.cpp:195-200 + ani_estimation.cpp:24-42 ----
+ * d_ani[i * n + j] = binomial_estimator(containment(counts[i][j], |S_i|), kmer_num_ones)
+ * for the n x n count matrix (|S_i| = counts[i][i]); d_cont (may be NULL) the
+ * containments.  Queued on the context stream. */
+int sks_ani_matrix(sks_ctx* ctx, const int32_t* d_counts, uint32_t n, int kmer_num_ones, double* d_cont,
+                   double* d_ani);
+/* Packed tiles (d_packed [n_tiles][64][64] of tiles d_tiles[2t] = I,
+ * d_tiles[2t + 1] = J, as sks_intersect_layout_tiles writes them):
+ * d_ani[t][0][r][c] = ANI of (64 I + r, 64 J + c), d_ani[t][1][c][r] = ANI of
+ * (64 J + c, 64 I + r); d_sizes[i] = |S_i| (int32). */
+int sks_ani_tiles(sks_ctx* ctx, const int32_t* d_packed, const uint32_t* d_tiles, uint64_t n_tiles, uint32_t n,
+                  const int32_t* d_sizes, int kmer_num_ones, double* d_ani);
 
 /* ---- FASTA ingress (device) — fasta_processing.cpp:79-133 on the GPU ------------------
  * d_raw: the n_raw bytes of one FASTA file in device memory (the host only reads
@@ -338,6 +380,15 @@ enum {
   SKS_INTERSECT_GLOBAL = 3    /* one wavefront per pair, straight from HBM */
 };
 int sks_ctx_set_intersect_kernel(sks_ctx* ctx, int kind);
+/* Diagnostics: on != 0 switches the context's join-layout builds and join
+ * launches to instrumented kernels that check, per element, the invariants the
+ * counts rest on (the layout's deduplication: every element's representative
+ * holds its value; the join table: every inserted value is found naming its
+ * own entry).  sks_ctx_join_check_violations waits for the context's stream
+ * and returns (and resets) the violations counted on the device since the
+ * last call; a correct build counts 0. */
+int sks_ctx_set_join_check(sks_ctx* ctx, int on);
+int sks_ctx_join_check_violations(sks_ctx* ctx, uint64_t* violations);
 
 /* ---- synthetic genomes (bench / test utility; no reference equivalent) ----------------- */
 /* Fills d_out[0..n) with ACGT bytes: base(p) = splitmix64(seed ^ (p * golden)) >> 62;

@@ -207,6 +207,7 @@ struct sks_ctx {
   sks_timings last{};
   int grid_override = 0;
   int intersect_algo = 0;  // sks::kIntersect*
+  bool join_check = false;  // invariant-checking join / layout kernels (sks_ctx_set_join_check)
 };
 
 struct sks_kmer_list {
@@ -633,6 +634,20 @@ int sks_ctx_set_intersect_kernel(sks_ctx* c, int kind) {
   if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_GLOBAL)
     return sks::fail(SKS_E_ARG, "sks_ctx_set_intersect_kernel: unknown kernel");
   c->intersect_algo = kind;
+  return SKS_OK;
+}
+
+int sks_ctx_set_join_check(sks_ctx* c, int on) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_set_join_check: null ctx");
+  c->join_check = on != 0;
+  return SKS_OK;
+}
+
+int sks_ctx_join_check_violations(sks_ctx* c, uint64_t* violations) {
+  if (!c || !violations) return sks::fail(SKS_E_ARG, "sks_ctx_join_check_violations: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipStreamSynchronize(c->stream));
+  *violations = sks::join_check_take() + sks::layout_check_take();
   return SKS_OK;
 }
 
@@ -1417,9 +1432,10 @@ int sks_intersect_all(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   DeviceGuard g(c->device);
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   bool done = false;
-  if (elem_words == 1 && c->intersect_algo != sks::kIntersectGlobal)
+  if (c->intersect_algo != sks::kIntersectGlobal)
     SKS_HIP(sks::launch_intersect_tiled(d_data, d_starts, d_sizes, n, false, row_begin, row_end, 0, 0,
-                                        d_out, c->iwork, c->stream, &done, c->intersect_algo));
+                                        d_out, c->iwork, c->stream, &done, c->intersect_algo, elem_words,
+                                        c->join_check));
   if (!done)
     SKS_HIP(sks::launch_intersect_all_global(d_data, d_starts, d_sizes, elem_words, n, row_begin,
                                              row_end, d_out, c->stream));
@@ -1440,14 +1456,14 @@ int sks_intersect_sym(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   const uint64_t all = sks::intersect_sym_tiles(n);
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   bool done = false;
-  if (elem_words == 1 && c->intersect_algo != sks::kIntersectGlobal)
+  if (c->intersect_algo != sks::kIntersectGlobal)
     SKS_HIP(sks::launch_intersect_tiled(d_data, d_starts, d_sizes, n, true, 0, n, tile_begin,
                                         tile_end, d_out, c->iwork, c->stream, &done,
-                                        c->intersect_algo));
+                                        c->intersect_algo, elem_words, c->join_check));
   if (!done) {
     if (tile_begin != 0 || tile_end < all)
       return sks::fail(SKS_E_UNSUPPORTED,
-                       "sks_intersect_sym: partial tile ranges need u64 sketches without extreme "
+                       "sks_intersect_sym: partial tile ranges need sketches without extreme "
                        "value skew; use sks_intersect_all row blocks");
     SKS_HIP(sks::launch_intersect_all_global(d_data, d_starts, d_sizes, elem_words, n, 0, n, d_out,
                                              c->stream));
@@ -1480,25 +1496,29 @@ int sks_sketch_union_wide(sks_ctx* c, const uint64_t* d_in, uint64_t n, uint64_t
 
 uint32_t sks_join_layout_log_b(uint32_t max_sketch_size) { return sks::join_log_b(max_sketch_size); }
 uint32_t sks_join_layout_capacity(void) { return sks::join_cap(); }
+uint32_t sks_join_layout_groups(uint32_t log_b) { return sks::join_layout_groups(log_b); }
+uint32_t sks_join_layout_boff_words(uint32_t log_b) { return log_b > 14 ? 0u : sks::join_layout_boff_words(log_b); }
 
 int sks_join_layout_bounds(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
-                           const uint32_t* d_sizes, uint32_t n, uint32_t log_b, uint64_t* d_bounds) {
+                           const uint32_t* d_sizes, int elem_words, uint32_t n, uint32_t log_b,
+                           uint64_t* d_bounds) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds: null ctx");
   if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds: log_b > 14");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
   if (!d_bounds || (n && (!d_starts || !d_sizes))) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds: null argument");
   DeviceGuard g(c->device);
-  SKS_HIP(sks::join_layout_bounds(d_data, d_starts, d_sizes, n, log_b, d_bounds, c->stream));
+  SKS_HIP(sks::join_layout_bounds(d_data, d_starts, d_sizes, n, log_b, elem_words, d_bounds, c->stream));
   return SKS_OK;
 }
 
-uint32_t sks_join_layout_groups(uint32_t log_b) { return sks::join_layout_groups(log_b); }
-
 int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
-                          const uint32_t* d_sizes, uint32_t n, uint64_t total_hint, uint32_t log_b,
-                          const uint64_t* d_bounds, uint64_t* d_out_data, uint8_t* d_out_ids,
-                          uint32_t* d_out_boff, uint64_t* d_out_bstart, uint32_t* max_block_bucket) {
+                          const uint32_t* d_sizes, int elem_words, uint32_t n, uint64_t total_hint,
+                          uint32_t log_b, const uint64_t* d_bounds, uint64_t* d_out_vals,
+                          uint64_t* d_out_masks, uint32_t* d_out_boff, uint64_t* d_out_bstart,
+                          uint32_t* max_block_bucket) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_join_layout_build: null ctx");
   if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_join_layout_build: log_b > 14");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
   if (!d_out_bstart || (n && (!d_starts || !d_sizes || !d_out_boff)))
     return sks::fail(SKS_E_ARG, "sks_join_layout_build: null argument");
   DeviceGuard g(c->device);
@@ -1513,30 +1533,31 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
   // bucket starts are u32: the layout must hold < 2^32 elements
   if (total >= (1ull << 32))
     return sks::fail(SKS_E_UNSUPPORTED, "sks_join_layout_build: >= 2^32 elements in one layout");
-  const size_t o_stat = (sks::join_layout_temp_bytes(n, log_b) + 15) & ~(size_t)15;
+  const size_t o_stat = (sks::join_layout_temp_bytes(n, log_b, elem_words) + 15) & ~(size_t)15;
   SKS_HIP(c->iwork.reserve(o_stat + 16));
   char* w = static_cast<char*>(c->iwork.ptr);
   uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
-  SKS_HIP(hipMemsetAsync(stat, 0, 4, c->stream));
+  SKS_HIP(hipMemsetAsync(stat, 0, 8, c->stream));
   if (n == 0) {
     SKS_HIP(hipMemsetAsync(d_out_bstart, 0, 8, c->stream));
   } else {
-    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, d_bounds, w, d_out_data, d_out_ids,
-                                   d_out_boff, d_out_bstart, stat, c->stream));
+    SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, elem_words, d_bounds, w, d_out_vals,
+                                   d_out_masks, d_out_boff, d_out_bstart, stat, c->join_check, c->stream));
   }
   if (max_block_bucket) {  // NULL: no read-back, the call does not wait for the build
-    uint32_t h = 0;
-    SKS_HIP(sks::pinned_d2h(&h, stat, 4, c->stream));
-    *max_block_bucket = h;
+    uint32_t h[2] = {0, 0};
+    SKS_HIP(sks::pinned_d2h(h, stat, 8, c->stream));
+    *max_block_bucket = h[1] ? UINT32_MAX : h[0];
   }
   return SKS_OK;
 }
 
-int sks_intersect_sym_layout(sks_ctx* c, uint32_t n, uint32_t log_b, const uint64_t* d_data,
-                             const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+int sks_intersect_sym_layout(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_words, const uint64_t* d_vals,
+                             const uint64_t* d_masks, const uint32_t* d_boff, const uint64_t* d_bstart,
                              uint64_t tile_begin, uint64_t tile_end, int32_t* d_out) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: null ctx");
   if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: log_b > 14");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
   if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: bad tile range");
   if (n && (!d_boff || !d_bstart || !d_out))
     return sks::fail(SKS_E_ARG, "sks_intersect_sym_layout: null argument");
@@ -1544,33 +1565,97 @@ int sks_intersect_sym_layout(sks_ctx* c, uint32_t n, uint32_t log_b, const uint6
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   SKS_HIP(hipMemsetAsync(d_out, 0, (uint64_t)n * n * sizeof(int32_t), c->stream));
   if (n) {
-    const sks::JoinLayout L{d_data, d_ids, d_boff, d_bstart};
-    SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, true, 0, n, tile_begin, tile_end, nullptr, false, d_out,
-                             c->stream));
+    const sks::JoinLayout L{d_vals, d_masks, d_boff, d_bstart};
+    SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, elem_words, true, 0, n, tile_begin, tile_end, nullptr, false,
+                             d_out, c->join_check, c->stream));
   }
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;
 }
 
-int sks_intersect_layout_tiles(sks_ctx* c, uint32_t n, uint32_t log_b, const uint64_t* d_data,
-                               const uint8_t* d_ids, const uint32_t* d_boff, const uint64_t* d_bstart,
+int sks_intersect_layout_tiles(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_words, const uint64_t* d_vals,
+                               const uint64_t* d_masks, const uint32_t* d_boff, const uint64_t* d_bstart,
                                uint32_t blk0, const uint32_t* d_tiles, uint64_t tile_begin,
                                uint64_t tile_end, int packed, int32_t* d_out) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: null ctx");
   if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: log_b > 14");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
   if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: bad tile range");
   if (!d_tiles && tile_end > sks::intersect_sym_tiles(n))
     return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: tile range beyond the upper triangle");
+  // the upper-triangle range starts at global block 0: a layout whose block 0
+  // is another block holds only part of it (a tile list names its blocks)
+  if (!d_tiles && blk0 != 0 && tile_end > tile_begin)
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: a tile range needs blk0 = 0 (pass a tile list)");
   if (tile_end > tile_begin && (!d_boff || !d_bstart || !d_out))
     return sks::fail(SKS_E_ARG, "sks_intersect_layout_tiles: null argument");
   DeviceGuard g(c->device);
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   if (n && tile_end > tile_begin) {
-    const sks::JoinLayout L{d_data, d_ids, d_boff, d_bstart};
-    SKS_HIP(sks::join_launch(L, 0u - blk0, L, 0u - blk0, n, log_b, true, 0, n, tile_begin, tile_end, d_tiles,
-                             packed != 0, d_out, c->stream));
+    const sks::JoinLayout L{d_vals, d_masks, d_boff, d_bstart};
+    SKS_HIP(sks::join_launch(L, 0u - blk0, L, 0u - blk0, n, log_b, elem_words, true, 0, n, tile_begin, tile_end,
+                             d_tiles, packed != 0, d_out, c->join_check, c->stream));
   }
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_intersect_layout_pair_tiles(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_words,
+                                    const uint64_t* d_rvals, const uint64_t* d_rmasks, const uint32_t* d_rboff,
+                                    const uint64_t* d_rbstart, uint32_t r_blk0, const uint64_t* d_cvals,
+                                    const uint64_t* d_cmasks, const uint32_t* d_cboff, const uint64_t* d_cbstart,
+                                    uint32_t c_blk0, const uint32_t* d_tiles, uint64_t tile_begin,
+                                    uint64_t tile_end, int packed, int32_t* d_out) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_layout_pair_tiles: null ctx");
+  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_layout_pair_tiles: log_b > 14");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_layout_pair_tiles: bad tile range");
+  if (tile_end > tile_begin && (!d_tiles || !d_rboff || !d_rbstart || !d_cboff || !d_cbstart || !d_out))
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_pair_tiles: null argument (a tile list is required)");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  if (n && tile_end > tile_begin) {
+    const sks::JoinLayout R{d_rvals, d_rmasks, d_rboff, d_rbstart}, C{d_cvals, d_cmasks, d_cboff, d_cbstart};
+    SKS_HIP(sks::join_launch(R, 0u - r_blk0, C, 0u - c_blk0, n, log_b, elem_words, true, 0, n, tile_begin,
+                             tile_end, d_tiles, packed != 0, d_out, c->join_check, c->stream));
+  }
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_ani_matrix(sks_ctx* c, const int32_t* d_counts, uint32_t n, int kmer_num_ones, double* d_cont,
+                   double* d_ani) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ani_matrix: null ctx");
+  if (kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_ani_matrix: kmer_num_ones must be positive");
+  if (n && (!d_counts || !d_ani)) return sks::fail(SKS_E_ARG, "sks_ani_matrix: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::launch_ani_matrix(d_counts, n, kmer_num_ones, d_cont, d_ani, c->stream));
+  return SKS_OK;
+}
+
+int sks_ani_tiles(sks_ctx* c, const int32_t* d_packed, const uint32_t* d_tiles, uint64_t n_tiles, uint32_t n,
+                  const int32_t* d_sizes, int kmer_num_ones, double* d_ani) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ani_tiles: null ctx");
+  if (kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_ani_tiles: kmer_num_ones must be positive");
+  if (n_tiles && (!d_packed || !d_tiles || !d_sizes || !d_ani))
+    return sks::fail(SKS_E_ARG, "sks_ani_tiles: null argument");
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::launch_ani_tiles(d_packed, d_tiles, n_tiles, n, d_sizes, kmer_num_ones, d_ani, c->stream));
+  return SKS_OK;
+}
+
+int sks_sketch_set_export_csr(const sks_sketch_set* set, uint64_t* d_data, uint32_t* d_sizes) {
+  if (!set) return sks::fail(SKS_E_ARG, "sks_sketch_set_export_csr: null set");
+  DeviceGuard g(set->device);
+  uint64_t total = 0;
+  for (uint32_t v : set->sizes) total += v;
+  if ((total && !d_data) || (set->n && !d_sizes))
+    return sks::fail(SKS_E_ARG, "sks_sketch_set_export_csr: null argument");
+  // the set's arrays are CSR in sketch order: one copy each
+  if (total)
+    SKS_HIP(hipMemcpy(d_data, set->d_data + set->starts[0] * set->elem_words,
+                      total * set->elem_words * sizeof(uint64_t), hipMemcpyDeviceToDevice));
+  if (set->n) SKS_HIP(hipMemcpy(d_sizes, set->d_sizes, set->n * sizeof(uint32_t), hipMemcpyDeviceToDevice));
   return SKS_OK;
 }
 

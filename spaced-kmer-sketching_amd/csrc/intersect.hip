@@ -4,11 +4,13 @@
 // the larger hash map (kmer_set.cpp:23-41), one pair per cilk_for iteration
 // (kmer_set.cpp:167-184).  Sketches here are sorted unique arrays, so a pair
 // is a sorted-merge count — the same integer the reference computes.
-//   * k_tiles: the all-pairs path for u64 sketches (bucketed, LDS-tiled; see
-//     the comment above it).
+//   * k_join (join.hip, over the join layout of layout.hip): the all-pairs
+//     path (u64 and 128-bit k-mers); launch_intersect_tiled below builds the
+//     layout and dispatches.
+//   * k_tiles: 64 x 64 tiles of pairwise LDS merges (u64; SKS_INTERSECT_MERGE,
+//     and the fallback when a join layout cannot be built).
 //   * k_pairs / k_all: one 64-lane wavefront per pair straight from global
-//     memory — pair lists, 128-bit k-mers, and the fallback for pathological
-//     value skew.  The smaller sketch is split evenly over the lanes, each lane
+//     memory — pair lists, and the fallback for pathological value skew.  The smaller sketch is split evenly over the lanes, each lane
 //     lower_bounds its first element in the larger one and merges forward.
 #include <hip/hip_runtime.h>
 
@@ -28,12 +30,6 @@ namespace sks {
 
 namespace {
 
-using jc::fp_slot;
-using jc::fp_tag;
-using jc::join_chain;
-using jc::kFFree;
-using jc::kFLog;
-using jc::kFSlots;
 using jc::sym_tile;
 
 constexpr int kB = 256;
@@ -358,400 +354,6 @@ __global__ __launch_bounds__(kB) void k_tiles(TileArgs a) {
 }
 
 
-// ---- join all-pairs kernel (u64 sketches) ----------------------------------------------
-//
-// Same 64 x 64 tiles as k_tiles, but a workgroup joins the two blocks instead
-// of merging 4096 pairs: the column block's elements go into an LDS hash table
-// value -> 64-bit mask of the columns holding it, every row element probes it
-// once, and a hit with mask m adds 1 to cnt[row][c] for each set bit c
-// (ds_add into an LDS 64 x 65 matrix).  Work per tile is
-// (row + column elements) + Σ_pairs |S_i ∩ S_j| instead of
-// Σ_pairs (|S_i| + |S_j|): 64x fewer steps for unrelated sketches and still
-// fewer when every pair is identical.
-//
-// Layout (built per call by k_hb_count / scan / k_hb_scatter): elements are
-// hash-bucketed — masked k-mers sit on a lattice (the mask's don't-care bits
-// are 0), so value-range buckets are lumpy, while a hash of the value gives
-// Poisson parts — and stored block-major: for each 64-sketch block, bucket by
-// bucket, sketch by sketch, with the sketch's slot in the block in a u8 id
-// array.  A run of buckets of one block is one contiguous range, so a
-// workgroup streams the column block in coalesced chunks of whole buckets
-// that fit the table (<= kJCap elements; a larger bucket is cut into
-// sub-chunks) and the row block's same buckets with them.  off[(blk * B + b) * 64 + slot] = start of (blk, b, slot).
-#ifndef SKS_JOIN_DIAG  // diagnostics only (wrong counts): 1 no probes / hit adds,
-#define SKS_JOIN_DIAG 0  // 2 no count flush, 4 probes without hit adds
-#endif
-// 512 threads (8 waves): with the table's LDS allowing 3 workgroups per CU,
-// 24 waves per CU instead of 12 hide the LDS round trips of the insert and
-// probe chains (config 4: k_join 0.86 -> 0.69 ms; 1024 threads 0.72)
-#ifndef SKS_JOIN_THREADS
-#define SKS_JOIN_THREADS 512
-#endif
-constexpr int kJB = SKS_JOIN_THREADS;       // threads per k_join workgroup
-constexpr int kJCap = 1024;                  // column elements per chunk
-constexpr int kJMade = kJCap / kJB;         // column elements per thread per chunk
-constexpr int kJWin = 256;                  // bucket offsets staged per window
-constexpr uint32_t kJMaxLogB = 14;          // B <= 16384 (LDS histogram of k_hb_count)
-// Hit counts as bit-sliced counters: plane b of
-// tile row r is the 64-bit word of bit b of the row's 64 column counts, and a
-// hit with column mask m is a carry chain of atomic XORs (m &= old after each
-// plane: a plane bit that was set carries).  A mask of k columns then costs
-// about log2(k) + 2 LDS atomics instead of k (a 32-bit count matrix with one
-// ds_add per set bit, rounds 1-2: 0.653 -> 0.604 ms on config 4).
-constexpr int kPlanes = 32;
-constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
-
-struct JoinArgs {
-  JoinLayout r, c;  // row blocks (tile row I = block r_blk0 + I) and column blocks
-  uint32_t r_blk0, c_blk0;  // (tile column J = block c_blk0 + J; uint32 arithmetic, -blk0 works)
-  uint32_t B, n, n_col_blocks, n_groups, buckets_per_group;
-  int sym;
-  uint32_t row_begin, row_end;
-  uint64_t tile_begin;
-  const uint32_t* tiles;  // optional (I, J) list (global block indices), sym semantics
-  int32_t* out;
-  uint64_t ld;
-  uint32_t cap;  // column elements per chunk (<= kJCap): table load <= cap / kFSlots
-  int packed;    // out = [tile - tile_begin][64][64]
-};
-
-// Elements of one chunk held in registers: column elements k = cs + tid + kJB * u
-// (u < kJMade: a chunk holds <= kJCap) and the first kJRowPf * kJB row elements;
-// the rest of a (rare) larger row range is read in the probe loop.
-constexpr int kJRowPf = 1536 / kJB;
-// s_waitcnt immediate for gfx9 "vmcnt(0)" with expcnt / lgkmcnt left at their
-// maxima: vmcnt = imm[3:0] | imm[15:14] << 4, expcnt = imm[6:4], lgkmcnt = imm[11:8]
-constexpr int kWaitVmcnt0 = 0x0F70;
-struct JoinChunk {
-  uint64_t cv[kJMade];
-  uint32_t cid[kJMade];
-  uint64_t rv[kJRowPf];
-  uint32_t rid[kJRowPf];
-};
-
-__device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cdata,
-                                           const uint8_t* __restrict__ cids,
-                                           const uint64_t* __restrict__ rdata,
-                                           const uint8_t* __restrict__ rids, uint32_t cs,
-                                           uint32_t ce, uint32_t rs, uint32_t re, int tid,
-                                           JoinChunk& c) {
-#pragma unroll
-  for (int u = 0; u < kJMade; ++u) {
-    const uint32_t k = cs + tid + kJB * u;
-    c.cv[u] = k < ce ? cdata[k] : 0;
-    c.cid[u] = k < ce ? cids[k] : 0xFFu;
-  }
-#pragma unroll
-  for (int u = 0; u < kJRowPf; ++u) {
-    const uint32_t k = rs + tid + kJB * u;
-    c.rv[u] = k < re ? rdata[k] : 0;
-    c.rid[u] = k < re ? rids[k] : 0xFFu;
-  }
-}
-
-#ifdef SKS_JOIN_STAMPS  // diagnostic build: cycles per k_join phase, wave 0 of each workgroup
-__device__ unsigned long long g_join_stamps[8];
-#define JSTAMP(i)                                              \
-  do {                                                         \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
-    st_acc[i] += t_ - st_last;                                 \
-    st_last = t_;                                              \
-  } while (0)
-#else
-#define JSTAMP(i) do {} while (0)
-#endif
-
-// ---- k_join: the join kernel ----------------------------------------------------------------
-//
-// Each chunk's column elements are first staged as entries {value, column
-// bit} in LDS (plain stores); the hash table then holds 32-bit slots
-// (fingerprint << 10 | entry index).  An insert is one 32-bit compare-swap
-// (the 64-bit one runs at about half its rate) and, for a value already present,
-// a check of the entry it names plus an OR of the column bit into that entry;
-// a probe reads 32-bit slots and, on a fingerprint match, the 16-byte entry.
-// Values need no reserved "empty" key (the empty marker lives in the slot), and
-// the entries need no reset: the next chunk's staging overwrites them.
-static_assert(kJCap == 1024, "entry index: 10 bits; join_chain reads entry x & 1023 of any slot word");
-
-__global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
-#ifdef SKS_JOIN_STAMPS
-  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
-  uint64_t st_last = __builtin_amdgcn_s_memtime();
-#endif
-  __shared__ uint32_t s_slot[kFSlots];
-  __shared__ ulonglong2 s_ent[kJCap];  // {value, mask of the columns holding it}
-  __shared__ unsigned long long s_pl[kPlanes * kTile];  // plane b of row r at [b * 64 + r]
-  __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
-  __shared__ uint16_t s_next[kJWin];
-
-  const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
-  const uint32_t grp = blockIdx.x % a.n_groups;
-  uint32_t I, J;
-  if (a.tiles) {
-    I = a.tiles[2 * t];
-    J = a.tiles[2 * t + 1];
-  } else if (a.sym) {
-    sym_tile(t, a.n_col_blocks, I, J);
-  } else {
-    I = (uint32_t)(t / a.n_col_blocks);
-    J = (uint32_t)(t % a.n_col_blocks);
-  }
-  const bool rows_mode = !a.sym && !a.tiles;
-  const uint32_t row0 = (rows_mode ? a.row_begin : 0) + I * kTile;
-  const uint32_t row_lim = rows_mode ? a.row_end : a.n;
-  const uint32_t col0 = J * kTile;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const uint32_t rblk = a.r_blk0 + I, cblk = a.c_blk0 + J;
-  const uint64_t rb = a.r.bstart[rblk], cb = a.c.bstart[cblk];
-  const uint64_t* rdata = a.r.data + rb;
-  const uint8_t* rids = a.r.ids + rb;
-  const uint64_t* cdata = a.c.data + cb;
-  const uint8_t* cids = a.c.ids + cb;
-  const uint32_t* roff = a.r.boff + (uint64_t)rblk * (a.B + 1);
-  const uint32_t* coff = a.c.boff + (uint64_t)cblk * (a.B + 1);
-  const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);
-
-  for (int i = tid; i < kFSlots / 4; i += kJB)
-    reinterpret_cast<uint4*>(s_slot)[i] = make_uint4(kFFree, kFFree, kFFree, kFFree);
-  // a tile on the diagonal: row block = column block, in the same layout (rows
-  // taken from a separate layout start off a block boundary, so never match)
-  const bool self_tile = row0 == col0;
-  for (int i = tid; i < kPlanes * kTile / 2; i += kJB) reinterpret_cast<uint4*>(s_pl)[i] = make_uint4(0, 0, 0, 0);
-  __shared__ uint32_t s_top;  // planes used (the highest carry chain)
-  // A tile on the diagonal (row block = column block) finds every row element in
-  // its own column: those self-hits are counted per row with plain adds, outside
-  // the carry chains (unrelated sketches would otherwise run a chain per element)
-  __shared__ uint32_t s_self[kTile];
-  if (tid < kTile) s_self[tid] = 0;
-  if (tid == 0) s_top = 0;
-  uint32_t top = 0;
-  auto add_hits = [&](uint32_t r, unsigned long long m) {
-    if (self_tile && ((m >> r) & 1ull)) {  // (a sub-chunk of a large bucket may not hold it)
-      atomicAdd(&s_self[r], 1u);
-      m &= ~(1ull << r);
-    }
-    unsigned long long* p = &s_pl[r];
-    uint32_t b = 0;
-    for (; m && b < kPlanes; ++b) m &= atomicXor(p + b * kTile, m);
-    top = max(top, b);
-  };
-  // columns holding v (0 if none)
-  auto lookup = [&](uint64_t v, uint32_t h, uint32_t x) -> unsigned long long {
-    if (x != kFFree) x = join_chain(x, h, fp_tag(v), v, 0u, s_slot, s_ent, false);
-    return x == kFFree ? 0ull : s_ent[x & 1023u].y;
-  };
-
-  uint32_t diag_acc = 0;  // SKS_JOIN_DIAG & 4: hits counted, not added
-  uint32_t made[kJMade];  // slots this thread created in the current chunk
-#pragma unroll
-  for (int u = 0; u < kJMade; ++u) made[u] = kNoSlot;
-
-  const uint32_t b0 = grp * a.buckets_per_group;
-  const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
-  for (uint32_t wb = b0; wb < b1; wb += kJWin) {
-    const uint32_t we = min(b1, wb + kJWin);
-    __syncthreads();  // previous window fully consumed
-    for (uint32_t i = tid; i <= we - wb; i += kJB) {
-      s_roff[i] = roff[wb + i];
-      s_coff[i] = coff[wb + i];
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < we - wb; i += kJB) {
-      const uint32_t cs = s_coff[i];
-      uint32_t lo = i + 1, hi = we - wb;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (s_coff[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
-      }
-      s_next[i] = (uint16_t)lo;
-    }
-    __syncthreads();
-    JSTAMP(0);
-    // chunks and oversized-bucket sub-chunks exactly as in k_join
-    auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
-    uint32_t bs = wb, be = chunk_end(wb);
-    uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
-    // a chunk of whole buckets of a diagonal tile needs no row elements: its
-    // rows are its columns (step 2 below)
-    auto rows_end = [&](uint32_t bs_, uint32_t be_, uint32_t cs_, uint32_t ce_) {
-      const bool whole = cs_ == s_coff[bs_ - wb] && ce_ == s_coff[be_ - wb];
-      return self_tile && whole ? s_roff[bs_ - wb] : s_roff[be_ - wb];
-    };
-    JoinChunk cur;
-    join_fetch(cdata, cids, rdata, rids, cs, ce, s_roff[0], rows_end(bs, be, cs, ce), tid, cur);
-    while (bs < we) {
-      const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // this chunk's elements have landed
-      uint32_t nbs, nbe, ncs, nce;
-      if (ce < s_coff[be - wb]) {
-        nbs = bs;
-        nbe = be;
-        ncs = ce;
-      } else {
-        nbs = be;
-        nbe = nbs < we ? chunk_end(nbs) : nbs;
-        ncs = s_coff[nbs - wb];
-      }
-      nce = min(s_coff[nbe - wb], ncs + a.cap);
-      JoinChunk nxt;
-      if (nbs < we)
-        join_fetch(cdata, cids, rdata, rids, ncs, nce, s_roff[nbs - wb], rows_end(nbs, nbe, ncs, nce), tid,
-                   nxt);
-
-      // 0) free the previous chunk's slots (its probes are done: barrier below
-      //    the probe loop) and stage this chunk's entries
-#pragma unroll
-      for (int u = 0; u < kJMade; ++u) {
-        if (made[u] != kNoSlot) s_slot[made[u]] = kFFree;
-        made[u] = kNoSlot;
-        const uint32_t e = tid + kJB * u;
-        if (cs + e < ce) s_ent[e] = make_ulonglong2(cur.cv[u], 1ull << cur.cid[u]);
-      }
-      __syncthreads();
-      // 1) insert: one 32-bit compare-swap per element; a value already
-      //    present adds its column bit to the entry the slot names
-      uint32_t hs[kJMade], prev[kJMade], tags[kJMade], ent[kJMade];
-#pragma unroll
-      for (int u = 0; u < kJMade; ++u) {
-        hs[u] = kNoSlot;
-        ent[u] = 0;
-        const uint32_t e = tid + kJB * u;
-        if (cs + e < ce) {
-          hs[u] = fp_slot(cur.cv[u]);
-          tags[u] = fp_tag(cur.cv[u]);
-          prev[u] = atomicCAS(&s_slot[hs[u]], kFFree, (tags[u] << 10) | e);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kJMade; ++u) {
-        if (hs[u] == kNoSlot) continue;
-        const uint64_t v = cur.cv[u];
-        const uint32_t e = tid + kJB * u;
-        uint32_t h = hs[u], x = prev[u];
-        if (x != kFFree) x = join_chain(x, h, tags[u], v, (tags[u] << 10) | e, s_slot, s_ent, true);
-        if (x == kFFree) {  // created slot h naming entry e
-          made[u] = h;
-          ent[u] = e;
-        } else {  // v is present: add the column bit to its entry
-          ent[u] = x & 1023u;
-          atomicOr(&s_ent[ent[u]].y, 1ull << cur.cid[u]);
-        }
-      }
-      __syncthreads();
-      JSTAMP(1);
-      // 2) probe with the row elements: first slots read together. A diagonal
-      //    tile's chunk of whole buckets has the column elements as its row
-      //    elements: each one's hits are the final mask of the entry it joined
-      if (self_tile && cs == s_coff[bs - wb] && ce == s_coff[be - wb]) {
-#pragma unroll
-        for (int u = 0; u < kJMade; ++u) {
-          const uint32_t r = cur.cid[u];
-          if (hs[u] == kNoSlot || r >= r_valid) continue;
-          const unsigned long long m = s_ent[ent[u]].y;
-#ifdef SKS_JOIN_CHECK  // diagnostic build: an element's entry holds its value and its column bit
-          if (s_ent[ent[u]].x != cur.cv[u] || !((m >> r) & 1ull))
-            printf("join check: tile %u,%u buckets [%u,%u) cols [%u,%u) e=%u ent=%u v=%llx entv=%llx m=%llx r=%u "
-                   "slot=%u made=%u prev=%x\n", I, J, bs, be, cs, ce, (uint32_t)(tid + kJB * u), ent[u],
-                   (unsigned long long)cur.cv[u], (unsigned long long)s_ent[ent[u]].x, m, r, hs[u], made[u],
-                   prev[u]);
-#endif
-          if (SKS_JOIN_DIAG & 1) continue;
-          if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
-          add_hits(r, m);
-        }
-        __syncthreads();
-        JSTAMP(2);
-        cur = nxt;
-        bs = nbs;
-        be = nbe;
-        cs = ncs;
-        ce = nce;
-        continue;
-      }
-      uint32_t sl[kJRowPf], sh[kJRowPf];
-#pragma unroll
-      for (int u = 0; u < kJRowPf; ++u) {
-        sl[u] = kFFree;
-        sh[u] = 0;
-        if (cur.rid[u] < r_valid) {
-          sh[u] = fp_slot(cur.rv[u]);
-          sl[u] = s_slot[sh[u]];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kJRowPf; ++u) {
-        const uint32_t r = cur.rid[u];
-        if (r >= r_valid) continue;
-        const unsigned long long m = lookup(cur.rv[u], sh[u], sl[u]);
-        if (SKS_JOIN_DIAG & 1) continue;
-        if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
-        if (m) add_hits(r, m);
-      }
-      for (uint32_t k = rs + tid + kJB * kJRowPf; k < re; k += kJB) {
-        const uint32_t r = rids[k];
-        if (r >= r_valid) continue;
-        const uint64_t v = rdata[k];
-        const uint32_t h = fp_slot(v);
-        const unsigned long long m = lookup(v, h, s_slot[h]);
-        if (SKS_JOIN_DIAG & 4) { diag_acc += __popcll(m); continue; }
-        if (m) add_hits(r, m);
-      }
-      __syncthreads();
-      JSTAMP(2);
-      cur = nxt;
-      bs = nbs;
-      be = nbe;
-      cs = ncs;
-      ce = nce;
-    }
-  }
-  __syncthreads();
-  JSTAMP(5);
-  if (SKS_JOIN_DIAG & 4) atomicAdd(&s_slot[0], diag_acc);
-  if (SKS_JOIN_DIAG & 2) return;
-  // planes the carry chains reached (unrelated tiles: none or one)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) top = max(top, (uint32_t)__shfl_xor(top, o, 64));
-  if (lane == 0 && top) atomicMax(&s_top, top);
-  __syncthreads();
-  const int np = (int)s_top;
-  for (uint32_t r = tid >> 6; r < kTile; r += kJB / 64) {  // a wave per row, a lane per column
-    const uint32_t c = lane;
-    uint32_t cnt = 0;
-    for (int b = 0; b < np; ++b) cnt |= (uint32_t)((s_pl[b * kTile + r] >> c) & 1ull) << b;
-    if (self_tile && c == r) cnt += s_self[r];
-    if (!cnt) continue;
-    const uint32_t gr = row0 + r, gc = col0 + c;
-    if (gr >= row_lim || gc >= a.n) continue;
-    if (a.packed) {
-      atomicAdd(&a.out[(t - a.tile_begin) * (kTile * kTile) + r * kTile + c], (int32_t)cnt);
-      continue;
-    }
-    const uint64_t orow = rows_mode ? (gr - a.row_begin) : gr;
-    atomicAdd(&a.out[orow * a.ld + gc], (int32_t)cnt);
-  }
-  // the mirror (j, i) of an off-diagonal symmetric tile: a wave per column, a lane
-  // per row, so each wave's atomics fall on one output row (contiguous), as above.
-  // (Round 2 added it in the loop above, lanes over columns: 64 rows, 64 lines
-  // per wave instruction.  Config 5, 200 related genomes, every tile dense: whole
-  // call 0.180 -> 0.125 ms; config 4 unchanged, 0.671 ms, most tiles sparse.)
-  if (!a.packed && !rows_mode && I != J) {
-    for (uint32_t c = tid >> 6; c < kTile; c += kJB / 64) {
-      const uint32_t r = lane;
-      uint32_t cnt = 0;
-      for (int b = 0; b < np; ++b) cnt |= (uint32_t)((s_pl[b * kTile + r] >> c) & 1ull) << b;
-      const uint32_t gr = row0 + r, gc = col0 + c;
-      if (!cnt || gr >= row_lim || gc >= a.n) continue;
-      atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
-    }
-  }
-#ifdef SKS_JOIN_STAMPS
-  JSTAMP(4);
-  if (tid == 0)
-    for (int i = 0; i < 6; ++i) atomicAdd(&g_join_stamps[i], (unsigned long long)st_acc[i]);
-#endif
-}
-
 }  // namespace
 
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,
@@ -796,105 +398,16 @@ hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* sta
 
 namespace sks {
 
-uint32_t join_cap() {  // SKS_JOIN_CAP (diagnostics) is clamped to [64, kJCap]
-  static const uint32_t cap = std::max<uint32_t>(
-      64, std::min<uint32_t>(kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP"))
-                                                           : kJCap));
-  return cap;
-}
-
-// Bucket count for the join: mean block-bucket population ~ cap / 6, so a
-// chunk holds several whole buckets.
-uint32_t join_log_b(uint32_t max_size) {
-  uint32_t log_b = 0;
-  while ((1ull << log_b) * (join_cap() / 6) < 64ull * max_size && log_b < kJMaxLogB) ++log_b;
-  return log_b;
-}
-
-hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
-                       uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
-                       uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
-                       int32_t* out, hipStream_t s) {
-  const uint32_t n_cb = (n + kTile - 1) / kTile;
-  const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
-  if (!d_tiles) {
-    const uint64_t all_tiles = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
-    if (!sym) { tile_begin = 0; tile_end = all_tiles; }
-    tile_end = std::min(tile_end, all_tiles);
-  }
-  if (tile_begin >= tile_end) return hipSuccess;
-  const uint64_t tiles = tile_end - tile_begin;
-  const uint32_t B = 1u << log_b;
-  JoinArgs ja{};
-  ja.r = rows;
-  ja.c = cols;
-  ja.r_blk0 = r_blk0;
-  ja.c_blk0 = c_blk0;
-  ja.tiles = d_tiles;
-  ja.packed = packed ? 1 : 0;
-  ja.B = B;
-  ja.n = n;
-  ja.n_col_blocks = n_cb;
-  ja.sym = (sym || d_tiles) ? 1 : 0;
-  ja.row_begin = row_begin;
-  ja.row_end = row_end;
-  ja.tile_begin = tile_begin;
-  ja.out = out;
-  ja.ld = n;
-  ja.cap = join_cap();
-  // bucket groups per tile: ~128 buckets per workgroup (a workgroup's start-up —
-  // clearing its table and count planes — and its count flush, up to 4096 global
-  // atomics on a tile of related genomes, are then small beside its chunks), at
-  // least ~1024 workgroups in all, at least 16 buckets each.  Config 4 (136
-  // tiles, B = 4096), round 3 sweep of SKS_JOIN_WGS, whole call family /
-  // unrelated genomes: 1088 workgroups 0.870 / 0.792 ms, 2176 0.705 / 0.691,
-  // 4352 (this rule) 0.681 / 0.674, 8704 (round 2's ~64 buckets) 0.742 / 0.681,
-  // 17408 0.900 / 0.734.  Config 5 (10 tiles): the 1024 floor, 1030.
-  // SKS_JOIN_WGS (diagnostics) sets the total instead.
-  // The ~128-buckets floor only applies while the grid is small (<= 64K
-  // workgroups); with very many tiles a tile gets fewer, larger groups (down to
-  // one), and the launch is cut into tile slices of at most kMaxGrid workgroups
-  // (HIP caps a grid at 2^32 - 1 work-items).
-  static const uint64_t wgs_env = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 0;
-  uint64_t want = wgs_env ? (wgs_env + tiles - 1) / tiles
-                          : std::max<uint64_t>(std::min<uint64_t>((B + 127) / 128, (65536 + tiles - 1) / tiles),
-                                               (1024 + tiles - 1) / tiles);
-  if (!wgs_env) want = std::min<uint64_t>(want, std::max<uint32_t>(1, B / 16));
-  const uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, want));
-  ja.buckets_per_group = (B + groups - 1) / groups;
-  ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
-  const uint64_t tiles_per_launch = std::max<uint64_t>(1, kMaxGrid / ja.n_groups);
-  for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
-    const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
-    ja.tile_begin = t0;
-    if (packed) ja.out = out + (t0 - tile_begin) * (uint64_t)(kTile * kTile);
-    hipLaunchKernelGGL(k_join, dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-#ifdef SKS_JOIN_STAMPS
-  {
-    unsigned long long h[8] = {0};
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_join_stamps), sizeof h);
-    const unsigned long long z[8] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_join_stamps), z, sizeof z);
-    const double wgs = (double)(tile_end - tile_begin) * ja.n_groups;
-    fprintf(stderr, "[k_join stamps] cycles per workgroup: setup %.0f insert %.0f probe %.0f reset %.0f "
-            "flush %.0f tail-barrier %.0f (%.0f workgroups)\n", h[0] / wgs, h[1] / wgs, h[2] / wgs,
-            h[3] / wgs, h[4] / wgs, h[5] / wgs, wgs);
-  }
-#endif
-  return hipSuccess;
-}
-
-// Tiled all-pairs for u64 sketches.  Host-synchronous (reads sizes and bucket
-// positions back to pick the bucket count).  mode: sym (upper-triangle tiles
-// [tile_begin, tile_end) into a full n x n matrix) or rows.
+// Tiled all-pairs (ew = 1: u64 k-mers, join or merge tiles; ew = 2: 128-bit
+// k-mers, join only).  Host-synchronous (reads the sizes and the layout's
+// statistics back to pick the bucket count).  mode: sym (upper-triangle tiles
+// [tile_begin, tile_end) into a full n x n matrix) or rows.  check: the
+// invariant-checking kernel builds (sks_ctx_set_join_check).
 hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                                   uint32_t n, bool sym, uint32_t row_begin, uint32_t row_end,
                                   uint64_t tile_begin, uint64_t tile_end, int32_t* out,
-                                  Scratch& work, hipStream_t s, bool* used_tiles, int algo) {
+                                  Scratch& work, hipStream_t s, bool* used_tiles, int algo, int ew,
+                                  bool check) {
   *used_tiles = false;
   hipError_t e;
   const uint64_t out_words = sym ? (uint64_t)n * n : (uint64_t)(row_end - row_begin) * n;
@@ -961,9 +474,9 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
   for (uint32_t i = 0; i < n; ++i) total += h_sizes[i];
   // the layout's bucket starts are u32 (< 2^32 elements per layout)
   const bool join_fits = total < (1ull << 32);
-  if (algo != kIntersectMerge && join_fits) {
-    // hash-bucketed block-major copy of the column sketches (and of the row
-    // range when its blocks are not aligned with the column blocks), then k_join
+  if ((algo != kIntersectMerge || ew == 2) && join_fits) {
+    // the join layout of the column sketches (and of the row range when its
+    // blocks are not aligned with the column blocks), then k_join
     const bool sep_rows = !sym && (row_begin % kTile) != 0;
     const uint32_t rn = row_end - row_begin;
     uint64_t r_total = 0;
@@ -971,57 +484,59 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       for (uint32_t i = row_begin; i < row_end; ++i) r_total += h_sizes[i];
     uint32_t log_b = join_log_b(max_size);
     for (;;) {
-      const uint32_t B = 1u << log_b;
-      const size_t tmp_c = join_layout_temp_bytes(n, log_b);
-      const size_t tmp_r = !sep_rows ? 0 : join_layout_temp_bytes(rn, log_b);
+      const uint32_t BW = jc::lay_boff_words(log_b), G = jc::lay_groups(log_b);
+      const size_t tmp_c = join_layout_temp_bytes(n, log_b, ew);
+      const size_t tmp_r = !sep_rows ? 0 : join_layout_temp_bytes(rn, log_b, ew);
       size_t o = 0;
-      const size_t o_cdat = o; o = align16(o + total * 8);
-      const size_t o_cids = o; o = align16(o + total);
-      const size_t o_cbof = o; o = align16(o + (size_t)n_cb * (B + 1) * 4);
+      const size_t o_cval = o; o = align16(o + total * 8 * ew);
+      const size_t o_cmsk = o; o = align16(o + total * 8);
+      const size_t o_cbof = o; o = align16(o + (size_t)n_cb * BW * 4);
       const size_t o_cbst = o; o = align16(o + (size_t)(n_cb + 1) * 8);
-      const size_t o_rdat = o; o = align16(o + r_total * 8);
-      const size_t o_rids = o; o = align16(o + r_total);
-      const size_t o_rbof = o; o = align16(o + (sep_rows ? (size_t)n_rb * (B + 1) * 4 : 0));
+      const size_t o_rval = o; o = align16(o + r_total * 8 * ew);
+      const size_t o_rmsk = o; o = align16(o + r_total * 8);
+      const size_t o_rbof = o; o = align16(o + (sep_rows ? (size_t)n_rb * BW * 4 : 0));
       const size_t o_rbst = o; o = align16(o + (sep_rows ? (size_t)(n_rb + 1) * 8 : 0));
       const size_t o_stat = o; o = align16(o + 16);
-      const size_t o_bnd = o; o = align16(o + (size_t)(B + 1) * 8);
+      const size_t o_bnd = o; o = align16(o + (size_t)(G + 1) * 8 * ew);
       const size_t o_tmp = o; o = align16(o + std::max(tmp_c, tmp_r));
       if ((e = work.reserve(o)) != hipSuccess) return e;
       char* w = static_cast<char*>(work.ptr);
-      JoinLayout cl{reinterpret_cast<uint64_t*>(w + o_cdat), reinterpret_cast<uint8_t*>(w + o_cids),
-                    reinterpret_cast<uint32_t*>(w + o_cbof), reinterpret_cast<uint64_t*>(w + o_cbst)};
-      JoinLayout rl = cl;
+      auto lay_at = [&](size_t ov, size_t om, size_t ob, size_t os) {
+        return JoinLayout{reinterpret_cast<uint64_t*>(w + ov), reinterpret_cast<uint64_t*>(w + om),
+                          reinterpret_cast<uint32_t*>(w + ob), reinterpret_cast<uint64_t*>(w + os)};
+      };
+      const JoinLayout cl = lay_at(o_cval, o_cmsk, o_cbof, o_cbst);
+      const JoinLayout rl = sep_rows ? lay_at(o_rval, o_rmsk, o_rbof, o_rbst) : cl;
       uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
-      if ((e = hipMemsetAsync(stat, 0, 4, s)) != hipSuccess) return e;
+      if ((e = hipMemsetAsync(stat, 0, 8, s)) != hipSuccess) return e;
       // a separate row layout shares the column set's group bounds; a single
       // layout computes its own in the build's first launch (three in all)
       uint64_t* gbounds = sep_rows ? reinterpret_cast<uint64_t*>(w + o_bnd) : nullptr;
-      if (sep_rows && (e = join_layout_bounds(data, starts, sizes, n, log_b, gbounds, s)) != hipSuccess)
+      if (sep_rows && (e = join_layout_bounds(data, starts, sizes, n, log_b, ew, gbounds, s)) != hipSuccess)
         return e;
-      auto build_layout = [&](uint32_t first, uint32_t cnt, uint64_t tot, const JoinLayout& L,
-                              size_t tmp_bytes) -> hipError_t {
-        return join_layout_build(data, starts + first, sizes + first, cnt, log_b, gbounds, w + o_tmp,
-                                 const_cast<uint64_t*>(L.data), const_cast<uint8_t*>(L.ids),
-                                 const_cast<uint32_t*>(L.boff), const_cast<uint64_t*>(L.bstart), stat, s);
+      auto build_layout = [&](uint32_t first, uint32_t cnt, const JoinLayout& L) -> hipError_t {
+        return join_layout_build(data, starts + first, sizes + first, cnt, log_b, ew, gbounds, w + o_tmp,
+                                 const_cast<uint64_t*>(L.vals), const_cast<uint64_t*>(L.masks),
+                                 const_cast<uint32_t*>(L.boff), const_cast<uint64_t*>(L.bstart), stat, check, s);
       };
-      if ((e = build_layout(0, n, total, cl, tmp_c)) != hipSuccess) return e;
-      if (sep_rows) {
-        rl = JoinLayout{reinterpret_cast<uint64_t*>(w + o_rdat), reinterpret_cast<uint8_t*>(w + o_rids),
-                        reinterpret_cast<uint32_t*>(w + o_rbof), reinterpret_cast<uint64_t*>(w + o_rbst)};
-        if ((e = build_layout(row_begin, rn, r_total, rl, tmp_r)) != hipSuccess) return e;
-      }
-      uint32_t h_stat = 0;
-      if ((e = pinned_d2h(&h_stat, stat, 4, s)) != hipSuccess) return e;
+      if ((e = build_layout(0, n, cl)) != hipSuccess) return e;
+      if (sep_rows && (e = build_layout(row_begin, rn, rl)) != hipSuccess) return e;
+      uint32_t h_stat[2] = {0, 0};
+      if ((e = pinned_d2h(h_stat, stat, 8, s)) != hipSuccess) return e;
       if (dbg)
-        fprintf(stderr, "[sks intersect] join n=%u B=%u max block bucket %u tiles=%llu\n", n, B,
-                h_stat, (unsigned long long)tiles);
+        fprintf(stderr, "[sks intersect] join n=%u ew=%d B=%u max block bucket %u invalid %u tiles=%llu\n", n, ew,
+                1u << log_b, h_stat[0], h_stat[1], (unsigned long long)tiles);
+      if (h_stat[1]) {  // a layout group the build could not place (adversarial 128-bit values)
+        if (log_b < jc::kMaxLogB) { ++log_b; continue; }
+        break;
+      }
       // buckets above the table's capacity are joined in sub-chunks (exact, but
-      // the bucket's row elements are probed once per sub-chunk), so more
+      // the bucket's row entries are probed once per sub-chunk), so more
       // buckets are tried first while the count matrix allows
-      if (h_stat <= join_cap() || log_b >= kJMaxLogB) {
+      if (h_stat[0] <= join_cap() || log_b >= jc::kMaxLogB) {
         const uint32_t r_blk0 = sep_rows ? 0 : (sym ? 0 : row_begin / kTile);
-        if ((e = join_launch(rl, r_blk0, cl, 0, n, log_b, sym, row_begin, row_end, tile_begin, tile_end, nullptr, false,
-                             out, s)) != hipSuccess)
+        if ((e = join_launch(rl, r_blk0, cl, 0, n, log_b, ew, sym, row_begin, row_end, tile_begin, tile_end,
+                             nullptr, false, out, check, s)) != hipSuccess)
           return e;
         *used_tiles = true;
         return hipSuccess;
@@ -1029,6 +544,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       ++log_b;
     }
   }
+  if (ew != 1) return hipSuccess;  // the merge tiles take u64 k-mers: one wavefront per pair
 
   // merge tiles: value-range buckets (parts must stay sorted)
   uint32_t B = 1;

@@ -1,0 +1,586 @@
+// Kernel 2 — k_join: |S_i ∩ S_j| for all pairs of a 64 x 64 tile of (row,
+// column) sketches, as one LDS hash join of the two 64-sketch blocks instead of
+// 4096 pairwise merges.
+//
+// The reference counts one pair at a time: iterate the smaller kmer_set, probe
+// the larger hash map (kmer_set.cpp:23-41), one pair per cilk_for iteration of
+// the all-pairs list (kmer_set.cpp:167-184, generators.hpp:44-58).  Here the
+// input is the join layout (layout.hip; format in join_common.hpp): per block,
+// each distinct value once with the mask of the block's sketches holding it.
+//   * Off-diagonal tile (I != J): per chunk of the column block's entries, every
+//     entry {value, column mask C} is staged in LDS and inserted into a
+//     fingerprint table (one 32-bit compare-swap: the entries of a block are
+//     distinct, so an insert only looks for a free slot); every row entry
+//     {value, row mask R} probes it once, and a hit adds C to each row r of R.
+//   * Diagonal tile (I == J): no table.  An entry held by the sketches M is in
+//     the intersection of every pair (r, c) of M: for each r of M it adds M to
+//     row r (the (r, r) bit as a plain per-row count).
+// Counts are bit-sliced: plane b of tile row r is the 64-bit word of bit b of
+// the row's 64 column counts, and adding a column mask m is a carry chain of
+// LDS atomic XORs (m &= old after each plane), about log2(|m|) + 2 atomics.
+// The result equals the reference's count for every pair: a value shared by
+// sketches i and j is one entry in each block (or one entry holding both bits
+// in a diagonal tile), and it meets its partner exactly once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+
+#include "join_common.hpp"
+#include "sks_internal.hpp"
+
+namespace sks {
+
+namespace {
+
+using jc::fp_slot;
+using jc::fp_tag;
+using jc::kFFree;
+using jc::kFSlots;
+using jc::KV;
+using jc::kv_eq;
+using jc::kv_load;
+using jc::sym_tile;
+
+constexpr int kTile = 64;
+// workgroups per launch at most (HIP caps a grid at 2^32 - 1 work-items);
+// larger grids are cut into slices
+constexpr uint64_t kMaxGrid = 1ull << 22;
+// 512 threads (8 waves): with the table's LDS allowing 3 workgroups per CU,
+// 24 waves per CU hide the LDS round trips of the insert and probe chains
+constexpr int kJB = 512;
+constexpr int kJCap = 1024;             // column entries per chunk (10-bit entry index)
+constexpr int kJMade = kJCap / kJB;     // column entries per thread per chunk
+constexpr int kJRowPf = 1536 / kJB;     // row entries per thread held in registers per chunk
+constexpr int kJWin = 1 << (jc::kGLog + jc::kRGLog);  // buckets per region (a window)
+// 16 planes hold counts below 2^16 per workgroup; a carry out of the top plane
+// (a pair sharing >= 65536 values in one workgroup's buckets) is added to the
+// output directly
+constexpr int kPlanes = 16;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+// hit items with more rows than this are spread over the wave's lanes (rows_add)
+constexpr uint32_t kLight = 2;
+static_assert(kJCap == 1024, "entry index: 10 bits of the slot word");
+
+// s_waitcnt immediate for gfx9 "vmcnt(0)" with expcnt / lgkmcnt left at their
+// maxima: vmcnt = imm[3:0] | imm[15:14] << 4, expcnt = imm[6:4], lgkmcnt = imm[11:8]
+constexpr int kWaitVmcnt0 = 0x0F70;
+
+struct JoinArgs {
+  JoinLayout r, c;          // row blocks (tile row I = block r_blk0 + I) and column blocks
+  uint32_t r_blk0, c_blk0;  // (tile column J = block c_blk0 + J; uint32 arithmetic, -blk0 works)
+  uint32_t log_b, B, BW, rb_log, n, n_col_blocks, n_groups, buckets_per_group;
+  int sym;
+  uint32_t row_begin, row_end;
+  uint64_t tile_begin;
+  const uint32_t* tiles;  // optional (I, J) list (global block indices), sym semantics
+  int32_t* out;
+  uint64_t ld;
+  uint32_t cap;  // column entries per chunk (<= kJCap): table load <= cap / kFSlots
+  int packed;    // out = [tile - tile_begin][64][64]
+};
+
+template <int EW>
+struct JoinChunk {
+  KV cv[kJMade];
+  unsigned long long cm[kJMade];  // 0: no entry
+  KV rv[kJRowPf];
+  unsigned long long rm[kJRowPf];
+};
+
+template <int EW>
+__device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cvals,
+                                           const unsigned long long* __restrict__ cmasks,
+                                           const uint64_t* __restrict__ rvals,
+                                           const unsigned long long* __restrict__ rmasks, uint32_t cs,
+                                           uint32_t ce, uint32_t rs, uint32_t re, int tid, JoinChunk<EW>& c) {
+#pragma unroll
+  for (int u = 0; u < kJMade; ++u) {
+    const uint32_t k = cs + tid + kJB * u;
+    c.cv[u] = k < ce ? kv_load<EW>(cvals, k) : KV{0, 0};
+    c.cm[u] = k < ce ? cmasks[k] : 0ull;
+  }
+#pragma unroll
+  for (int u = 0; u < kJRowPf; ++u) {
+    const uint32_t k = rs + tid + kJB * u;
+    c.rv[u] = k < re ? kv_load<EW>(rvals, k) : KV{0, 0};
+    c.rm[u] = k < re ? rmasks[k] : 0ull;
+  }
+}
+
+__device__ unsigned long long g_join_check;  // SKS check build: table invariant violations
+
+// inclusive prefix sum over the 64 lanes of a wave (DPP; no LDS)
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long x, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// index of the k-th set bit (k < popcount(x)) of x
+__device__ __forceinline__ uint32_t nth_bit(unsigned long long x, uint32_t k) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(x & ((1ull << w) - 1));
+    if (k >= c) {
+      k -= c;
+      x >>= w;
+      r += w;
+    }
+  }
+  return r;
+}
+
+// end of window [.., we) in a block's boff row: the next bucket's start, or the
+// region's end when we closes a region
+__device__ __forceinline__ uint32_t window_end(const uint32_t* off, uint32_t we, uint32_t B, uint32_t rb_log) {
+  return (we & ((1u << rb_log) - 1)) == 0 ? off[B + ((we - 1) >> rb_log)] : off[we];
+}
+
+template <int EW, bool CHECK>
+__global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
+  __shared__ uint32_t s_slot[kFSlots];
+  __shared__ uint64_t s_ev[kJCap * EW];          // staged column entries: values
+  __shared__ unsigned long long s_em[kJCap];     // ... and column masks
+  __shared__ unsigned long long s_pl[kPlanes * kTile];  // plane b of row r at [b * 64 + r]
+  __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
+  __shared__ uint8_t s_next[kJWin];
+  __shared__ uint32_t s_self[kTile];
+  __shared__ uint32_t s_top;  // planes used (the highest carry chain)
+
+  const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
+  const uint32_t grp = blockIdx.x % a.n_groups;
+  uint32_t I, J;
+  if (a.tiles) {
+    I = a.tiles[2 * t];
+    J = a.tiles[2 * t + 1];
+  } else if (a.sym) {
+    sym_tile(t, a.n_col_blocks, I, J);
+  } else {
+    I = (uint32_t)(t / a.n_col_blocks);
+    J = (uint32_t)(t % a.n_col_blocks);
+  }
+  const bool rows_mode = !a.sym && !a.tiles;
+  const uint32_t row0 = (rows_mode ? a.row_begin : 0) + I * kTile;
+  const uint32_t row_lim = rows_mode ? a.row_end : a.n;
+  const uint32_t col0 = J * kTile;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t rblk = a.r_blk0 + I, cblk = a.c_blk0 + J;
+  const uint64_t rb = a.r.bstart[rblk], cb = a.c.bstart[cblk];
+  const uint64_t* rvals = a.r.vals + rb * EW;
+  const unsigned long long* rmasks = reinterpret_cast<const unsigned long long*>(a.r.masks) + rb;
+  const uint64_t* cvals = a.c.vals + cb * EW;
+  const unsigned long long* cmasks = reinterpret_cast<const unsigned long long*>(a.c.masks) + cb;
+  const uint32_t* roff = a.r.boff + (uint64_t)rblk * a.BW;
+  const uint32_t* coff = a.c.boff + (uint64_t)cblk * a.BW;
+  const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);
+  const unsigned long long rvm = r_valid >= 64 ? ~0ull : ((1ull << r_valid) - 1);
+  // a tile on the diagonal: row block = column block of the same layout (rows
+  // taken from a separate layout start off a block boundary, so never match)
+  const bool self_tile = row0 == col0 && a.r.vals == a.c.vals;
+
+  for (int i = tid; i < kFSlots / 4; i += kJB)
+    reinterpret_cast<uint4*>(s_slot)[i] = make_uint4(kFFree, kFFree, kFFree, kFFree);
+  for (int i = tid; i < kPlanes * kTile / 2; i += kJB) reinterpret_cast<uint4*>(s_pl)[i] = make_uint4(0, 0, 0, 0);
+  if (tid < kTile) s_self[tid] = 0;
+  if (tid == 0) s_top = 0;
+  uint32_t top = 0;
+  __syncthreads();  // table, planes and self counts cleared before any chain (the diagonal path has no other barrier)
+
+  // output of count `cnt` for tile cell (r, c) (both halves of a symmetric
+  // off-diagonal tile): the carry-out path of add_hits
+  auto emit = [&](uint32_t r, uint32_t c, uint32_t cnt) {
+    const uint32_t gr = row0 + r, gc = col0 + c;
+    if (gr >= row_lim || gc >= a.n) return;
+    if (a.packed) {
+      atomicAdd(&a.out[(t - a.tile_begin) * (kTile * kTile) + r * kTile + c], (int32_t)cnt);
+      return;
+    }
+    atomicAdd(&a.out[(uint64_t)(rows_mode ? gr - a.row_begin : gr) * a.ld + gc], (int32_t)cnt);
+    if (!rows_mode && I != J) atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
+  };
+  auto add_hits = [&](uint32_t r, unsigned long long m) {
+    unsigned long long* p = &s_pl[r];
+    uint32_t b = 0;
+    for (; m && b < kPlanes; ++b) m &= atomicXor(p + b * kTile, m);
+    top = max(top, b);
+    while (m) {  // carried out of the top plane: 2^kPlanes per column
+      const uint32_t c = __builtin_ctzll(m);
+      m &= m - 1;
+      emit(r, c, 1u << kPlanes);
+    }
+  };
+  // Wave-uniform: for every lane l with an item (row mask R_l, column mask
+  // C_l), add C_l to each row of R_l.  An item of at most kLight rows runs them
+  // in its own lane; the rows of heavier items (an entry held by many sketches
+  // of a related block) are spread over the lanes, one (item, row) per lane:
+  // the wave walks its heavy items in lane order (readlanes, no LDS), giving
+  // each window of 64 (item, row) pairs to its 64 lanes, instead of one lane
+  // running up to 64 rows one after another.  diag: the (r, r) bit is counted
+  // in s_self[r] instead (a diagonal tile's entry is in its own row).
+  auto row_add = [&](uint32_t r, unsigned long long C, bool diag) {
+    if (diag) {
+      atomicAdd(&s_self[r], 1u);
+      const unsigned long long m = C & ~(1ull << r);
+      if (m) add_hits(r, m);
+    } else {
+      add_hits(r, C);
+    }
+  };
+  auto rows_add = [&](unsigned long long R, unsigned long long C, bool diag) {
+    const uint32_t cnt = (uint32_t)__popcll(R);
+    // light items (<= kLight rows) run their rows in their own lane
+    const bool heavy = cnt > kLight;
+    if (!heavy) {
+      while (R) {
+        const uint32_t r = (uint32_t)__builtin_ctzll(R);
+        R &= R - 1;
+        row_add(r, C, diag);
+      }
+    }
+    unsigned long long pend = __ballot(heavy);
+    if (!pend) return;
+    const uint32_t hc = heavy ? cnt : 0;
+    const uint32_t incl = wave_scan(hc), excl = incl - hc;
+    for (uint32_t t = 0; pend; t += 64) {
+      unsigned long long myR = 0, myC = 0;
+      uint32_t myk = 0;
+      const uint32_t g = t + lane;
+      while (pend) {
+        const uint32_t o = (uint32_t)__builtin_ctzll(pend);
+        const uint32_t eo = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)o);
+        if (eo >= t + 64) break;
+        const uint32_t co = (uint32_t)__builtin_amdgcn_readlane((int)hc, (int)o);
+        const unsigned long long Ro = readlane64(R, o), Co = readlane64(C, o);
+        if (g >= eo && g < eo + co) {
+          myR = Ro;
+          myC = Co;
+          myk = g - eo;
+        }
+        if (eo + co > t + 64) break;  // continues in the next window
+        pend &= pend - 1;
+      }
+      if (myR) row_add(nth_bit(myR, myk), myC, diag);
+    }
+  };
+  auto ent_val = [&](uint32_t e) -> KV {
+    if constexpr (EW == 1) return KV{s_ev[e], 0};
+    else return KV{s_ev[2 * e], s_ev[2 * e + 1]};
+  };
+  // slot word naming v's entry, or kFFree (one exit edge; the stop test reads
+  // the named entry whether or not the tag matches: see layout.hip dd_insert)
+  auto chain = [&](const KV& v, uint32_t h, uint32_t x) -> uint32_t {
+    const uint32_t tag = fp_tag<EW>(v);
+    for (;;) {
+      const KV u = ent_val(x & 1023u);
+      if ((x == kFFree) | (((x >> 10) == tag) & kv_eq<EW>(u, v))) return x;
+      h = (h + 1) & (kFSlots - 1);
+      x = s_slot[h];
+    }
+  };
+
+  const uint32_t b0 = grp * a.buckets_per_group;
+  const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
+  if (self_tile) {
+    // ---- diagonal tile: every entry's hits are its own mask ----------------------------------
+    for (uint32_t wb = b0; wb < b1;) {
+      const uint32_t we = min(b1, ((wb >> a.rb_log) + 1) << a.rb_log);
+      const uint32_t es = coff[wb], ee = window_end(coff, we, a.B, a.rb_log);
+      for (uint32_t k0 = es; k0 < ee; k0 += 4 * kJB) {
+        unsigned long long m[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t k = k0 + tid + u * kJB;
+          m[u] = k < ee ? cmasks[k] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rows_add(m[u] & rvm, m[u], true);
+      }
+      wb = we;
+    }
+  } else {
+    // ---- off-diagonal tile: chunks of the column block's entries -----------------------------
+    uint32_t made[kJMade];  // slots this thread created in the current chunk
+#pragma unroll
+    for (int u = 0; u < kJMade; ++u) made[u] = kNoSlot;
+    for (uint32_t wb = b0; wb < b1;) {
+      const uint32_t we = min(b1, ((wb >> a.rb_log) + 1) << a.rb_log);
+      const uint32_t nw = we - wb;
+      __syncthreads();  // previous window fully consumed
+      for (uint32_t i = tid; i <= nw; i += kJB) {
+        s_roff[i] = i < nw ? roff[wb + i] : window_end(roff, we, a.B, a.rb_log);
+        s_coff[i] = i < nw ? coff[wb + i] : window_end(coff, we, a.B, a.rb_log);
+      }
+      __syncthreads();
+      // chunk ends: the most whole buckets from bucket i on that fit cap
+      for (uint32_t i = tid; i < nw; i += kJB) {
+        const uint32_t cs = s_coff[i];
+        uint32_t lo = i + 1, hi = nw;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_coff[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
+        }
+        s_next[i] = (uint8_t)lo;
+      }
+      __syncthreads();
+      // chunks of whole buckets; a bucket above cap is cut into sub-chunks of
+      // cap column entries, each joined with all of the bucket's row entries
+      // (its column entries are distinct, so each hit is counted once)
+      auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
+      uint32_t bs = wb, be = chunk_end(wb);
+      uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
+      JoinChunk<EW> cur;
+      join_fetch<EW>(cvals, cmasks, rvals, rmasks, cs, ce, s_roff[0], s_roff[be - wb], tid, cur);
+      while (bs < we) {
+        const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
+        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // this chunk's entries have landed
+        uint32_t nbs, nbe, ncs, nce;
+        if (ce < s_coff[be - wb]) {
+          nbs = bs;
+          nbe = be;
+          ncs = ce;
+        } else {
+          nbs = be;
+          nbe = nbs < we ? chunk_end(nbs) : nbs;
+          ncs = s_coff[nbs - wb];
+        }
+        nce = min(s_coff[nbe - wb], ncs + a.cap);
+        JoinChunk<EW> nxt;
+        if (nbs < we) join_fetch<EW>(cvals, cmasks, rvals, rmasks, ncs, nce, s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
+
+        // 0) free the previous chunk's slots (its probes are done: barrier below
+        //    the probe loop) and stage this chunk's entries
+#pragma unroll
+        for (int u = 0; u < kJMade; ++u) {
+          if (made[u] != kNoSlot) s_slot[made[u]] = kFFree;
+          made[u] = kNoSlot;
+          const uint32_t e = tid + kJB * u;
+          if (cur.cm[u]) {
+            if constexpr (EW == 1) s_ev[e] = cur.cv[u].lo;
+            else { s_ev[2 * e] = cur.cv[u].lo; s_ev[2 * e + 1] = cur.cv[u].hi; }
+            s_em[e] = cur.cm[u];
+          }
+        }
+        __syncthreads();
+        // 1) insert: the chunk's values are distinct, so a compare-swap walk to
+        //    the first free slot
+#pragma unroll
+        for (int u = 0; u < kJMade; ++u) {
+          if (!cur.cm[u]) continue;
+          const uint32_t e = tid + kJB * u;
+          const uint32_t word = (fp_tag<EW>(cur.cv[u]) << 10) | e;
+          uint32_t h = fp_slot<EW>(cur.cv[u]);
+          uint32_t x = atomicCAS(&s_slot[h], kFFree, word);
+          while (x != kFFree) {
+            h = (h + 1) & (kFSlots - 1);
+            x = atomicCAS(&s_slot[h], kFFree, word);
+          }
+          made[u] = h;
+        }
+        __syncthreads();
+        if (CHECK) {  // every inserted value is found, naming its own entry
+#pragma unroll
+          for (int u = 0; u < kJMade; ++u) {
+            if (!cur.cm[u]) continue;
+            const uint32_t h = fp_slot<EW>(cur.cv[u]);
+            const uint32_t x = chain(cur.cv[u], h, s_slot[h]);
+            if (x == kFFree || (x & 1023u) != tid + kJB * u) atomicAdd(&g_join_check, 1ull);
+          }
+        }
+        // 2) probe with the row entries: first slots read together; a hit with
+        //    column mask C adds C to each row of the entry's row mask
+        uint32_t sl[kJRowPf], sh[kJRowPf];
+#pragma unroll
+        for (int u = 0; u < kJRowPf; ++u) {
+          sl[u] = kFFree;
+          sh[u] = 0;
+          if (cur.rm[u] & rvm) {
+            sh[u] = fp_slot<EW>(cur.rv[u]);
+            sl[u] = s_slot[sh[u]];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kJRowPf; ++u) {
+          const unsigned long long rows = cur.rm[u] & rvm;
+          unsigned long long m = 0;
+          if (rows && sl[u] != kFFree) {
+            const uint32_t x = chain(cur.rv[u], sh[u], sl[u]);
+            if (x != kFFree) m = s_em[x & 1023u];
+          }
+          rows_add(m ? rows : 0ull, m, false);
+        }
+        for (uint32_t k0 = rs + kJB * kJRowPf; k0 < re; k0 += kJB) {  // (rare) rows beyond the prefetch
+          const uint32_t k = k0 + tid;
+          const unsigned long long rows = k < re ? rmasks[k] & rvm : 0ull;
+          unsigned long long m = 0;
+          if (rows) {
+            const KV v = kv_load<EW>(rvals, k);
+            const uint32_t h = fp_slot<EW>(v);
+            const uint32_t x0 = s_slot[h];
+            if (x0 != kFFree) {
+              const uint32_t x = chain(v, h, x0);
+              if (x != kFFree) m = s_em[x & 1023u];
+            }
+          }
+          rows_add(m ? rows : 0ull, m, false);
+        }
+        __syncthreads();
+        cur = nxt;
+        bs = nbs;
+        be = nbe;
+        cs = ncs;
+        ce = nce;
+      }
+      wb = we;
+    }
+  }
+  __syncthreads();
+  // planes the carry chains reached (unrelated tiles: none or one)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) top = max(top, (uint32_t)__shfl_xor(top, o, 64));
+  if (lane == 0 && top) atomicMax(&s_top, top);
+  __syncthreads();
+  const int np = (int)s_top;
+  for (uint32_t r = tid >> 6; r < kTile; r += kJB / 64) {  // a wave per row, a lane per column
+    const uint32_t c = lane;
+    uint32_t cnt = 0;
+    for (int b = 0; b < np; ++b) cnt |= (uint32_t)((s_pl[b * kTile + r] >> c) & 1ull) << b;
+    if (self_tile && c == r) cnt += s_self[r];
+    if (!cnt) continue;
+    const uint32_t gr = row0 + r, gc = col0 + c;
+    if (gr >= row_lim || gc >= a.n) continue;
+    if (a.packed) {
+      atomicAdd(&a.out[(t - a.tile_begin) * (kTile * kTile) + r * kTile + c], (int32_t)cnt);
+      continue;
+    }
+    const uint64_t orow = rows_mode ? (gr - a.row_begin) : gr;
+    atomicAdd(&a.out[orow * a.ld + gc], (int32_t)cnt);
+  }
+  // the mirror (j, i) of an off-diagonal symmetric tile: a wave per column, a lane
+  // per row, so each wave's atomics fall on one output row (contiguous), as above.
+  // (Round 2 added it in the loop above, lanes over columns: 64 rows, 64 lines
+  // per wave instruction.  Config 5, 200 related genomes, every tile dense: whole
+  // call 0.180 -> 0.125 ms; config 4 unchanged, most tiles sparse.)
+  if (!a.packed && !rows_mode && I != J) {
+    for (uint32_t c = tid >> 6; c < kTile; c += kJB / 64) {
+      const uint32_t r = lane;
+      uint32_t cnt = 0;
+      for (int b = 0; b < np; ++b) cnt |= (uint32_t)((s_pl[b * kTile + r] >> c) & 1ull) << b;
+      const uint32_t gr = row0 + r, gc = col0 + c;
+      if (!cnt || gr >= row_lim || gc >= a.n) continue;
+      atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
+    }
+  }
+}
+
+template <int EW, bool CHECK>
+hipError_t launch_join_slices(JoinArgs ja, uint64_t tile_begin, uint64_t tile_end, bool packed, int32_t* out,
+                              hipStream_t s) {
+  const uint64_t tiles_per_launch = std::max<uint64_t>(1, kMaxGrid / ja.n_groups);
+  for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
+    const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
+    ja.tile_begin = t0;
+    if (packed) ja.out = out + (t0 - tile_begin) * (uint64_t)(kTile * kTile);
+    hipLaunchKernelGGL((k_join<EW, CHECK>), dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+uint32_t join_cap() {  // SKS_JOIN_CAP (diagnostics) is clamped to [64, kJCap]
+  static const uint32_t cap = std::max<uint32_t>(
+      64, std::min<uint32_t>(kJCap, getenv("SKS_JOIN_CAP") ? (uint32_t)atoi(getenv("SKS_JOIN_CAP"))
+                                                           : kJCap));
+  return cap;
+}
+
+// Bucket count for the join: mean raw block-bucket population ~ cap / 6, so a
+// chunk holds several whole buckets (fewer after deduplication).
+uint32_t join_log_b(uint32_t max_size) {
+  uint32_t log_b = 0;
+  while ((1ull << log_b) * (join_cap() / 6) < 64ull * max_size && log_b < jc::kMaxLogB) ++log_b;
+  return log_b;
+}
+
+unsigned long long join_check_take() {
+  unsigned long long h = 0;
+  (void)hipMemcpyFromSymbol(&h, HIP_SYMBOL(g_join_check), sizeof h);
+  const unsigned long long z = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_join_check), &z, sizeof z);
+  return h;
+}
+
+hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
+                       uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,
+                       uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
+                       int32_t* out, bool check, hipStream_t s) {
+  if (log_b > jc::kMaxLogB || (ew != 1 && ew != 2)) return hipErrorInvalidValue;
+  const uint32_t n_cb = (n + kTile - 1) / kTile;
+  const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
+  if (!d_tiles) {
+    const uint64_t all_tiles = sym ? (uint64_t)n_cb * (n_cb + 1) / 2 : (uint64_t)n_rb * n_cb;
+    if (!sym) { tile_begin = 0; tile_end = all_tiles; }
+    tile_end = std::min(tile_end, all_tiles);
+  }
+  if (tile_begin >= tile_end) return hipSuccess;
+  const uint64_t tiles = tile_end - tile_begin;
+  const uint32_t B = 1u << log_b;
+  JoinArgs ja{};
+  ja.r = rows;
+  ja.c = cols;
+  ja.r_blk0 = r_blk0;
+  ja.c_blk0 = c_blk0;
+  ja.tiles = d_tiles;
+  ja.packed = packed ? 1 : 0;
+  ja.log_b = log_b;
+  ja.B = B;
+  ja.BW = jc::lay_boff_words(log_b);
+  ja.rb_log = jc::lay_rb_log(log_b);
+  ja.n = n;
+  ja.n_col_blocks = n_cb;
+  ja.sym = (sym || d_tiles) ? 1 : 0;
+  ja.row_begin = row_begin;
+  ja.row_end = row_end;
+  ja.out = out;
+  ja.ld = n;
+  ja.cap = join_cap();
+  // bucket groups per tile: ~128 buckets per workgroup (a workgroup's start-up —
+  // clearing its table and count planes — and its count flush, up to 4096 global
+  // atomics on a tile of related genomes, are then small beside its chunks), at
+  // least ~1024 workgroups in all, at least 16 buckets each (round 3 sweep,
+  // config 4: 4352 workgroups 0.681 ms against 2176: 0.705, 8704: 0.742).
+  // SKS_JOIN_WGS (diagnostics) sets the total instead.  The ~128-buckets floor
+  // only applies while the grid is small (<= 64K workgroups); with very many
+  // tiles a tile gets fewer, larger groups (down to one).
+  static const uint64_t wgs_env = getenv("SKS_JOIN_WGS") ? strtoull(getenv("SKS_JOIN_WGS"), 0, 10) : 0;
+  uint64_t want = wgs_env ? (wgs_env + tiles - 1) / tiles
+                          : std::max<uint64_t>(std::min<uint64_t>((B + 127) / 128, (65536 + tiles - 1) / tiles),
+                                               (1024 + tiles - 1) / tiles);
+  if (!wgs_env) want = std::min<uint64_t>(want, std::max<uint32_t>(1, B / 16));
+  const uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, want));
+  ja.buckets_per_group = (B + groups - 1) / groups;
+  ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
+  if (ew == 1)
+    return check ? launch_join_slices<1, true>(ja, tile_begin, tile_end, packed, out, s)
+                 : launch_join_slices<1, false>(ja, tile_begin, tile_end, packed, out, s);
+  return check ? launch_join_slices<2, true>(ja, tile_begin, tile_end, packed, out, s)
+               : launch_join_slices<2, false>(ja, tile_begin, tile_end, packed, out, s);
+}
+
+}  // namespace sks

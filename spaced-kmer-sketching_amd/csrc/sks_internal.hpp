@@ -142,14 +142,17 @@ hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* sta
                                        const uint32_t* sizes, int elem_words, uint32_t n,
                                        uint32_t row_begin, uint32_t row_end, int32_t* out,
                                        hipStream_t s);
-// Tiled u64 all-pairs (intersect.hip).  sym: upper-triangle tiles
-// [tile_begin, tile_end) written to both halves of an n x n matrix; otherwise
-// rows [row_begin, row_end) x n.  Zeroes `out` first.  *used_tiles = false
-// means the value distribution was too skewed: use the global kernel.
+// Tiled all-pairs (intersect.hip + join.hip): ew = 1 (u64) or 2 (128-bit)
+// k-mers.  sym: upper-triangle tiles [tile_begin, tile_end) written to both
+// halves of an n x n matrix; otherwise rows [row_begin, row_end) x n.  Zeroes
+// `out` first.  *used_tiles = false means no tiled kernel could take the set
+// (extreme value skew, or 128-bit k-mers without a join layout): use the
+// global kernel.  check: the invariant-checking kernel builds.
 hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                                   uint32_t n, bool sym, uint32_t row_begin, uint32_t row_end,
                                   uint64_t tile_begin, uint64_t tile_end, int32_t* out,
-                                  Scratch& work, hipStream_t s, bool* used_tiles, int algo);
+                                  Scratch& work, hipStream_t s, bool* used_tiles, int algo, int ew,
+                                  bool check);
 // intersection kernel choice (sks_ctx_set_intersect_kernel)
 constexpr int kIntersectAuto = 0;    // join when the bucket sizes allow, else merge tiles
 constexpr int kIntersectMerge = 1;   // k_tiles (pairwise LDS merges)
@@ -165,34 +168,35 @@ hipError_t launch_bucket_pos(const uint64_t* data, const uint64_t* starts, const
                              uint32_t n, uint32_t B, const uint64_t* bounds, uint32_t* pos,
                              hipStream_t s);
 
-// Join layout (input of k_join, intersect.hip): blocks of 64 consecutive
-// sketches, elements hash-bucketed into B = 2^log_b buckets and stored block-major.
-// Block k's elements are data[bstart[k] ..] / ids[bstart[k] ..] (ids = slot
-// in the block); its bucket b starts boff[k * (B + 1) + b] elements in.
+// Join layout (layout.hip builds it, join.hip's k_join reads it; format in
+// join_common.hpp): per 64-sketch block, each distinct value once with the mask
+// of the block's sketches holding it, in value groups x hash buckets, regions
+// of groups at their raw offsets.
 struct JoinLayout {
-  const uint64_t* data;
-  const uint8_t* ids;
-  const uint32_t* boff;
-  const uint64_t* bstart;
+  const uint64_t* vals;    // [T * ew] entry values
+  const uint64_t* masks;   // [T] sketch masks
+  const uint32_t* boff;    // [nb * (B + NR)] bucket starts, then region ends (block-relative)
+  const uint64_t* bstart;  // [nb + 1] raw block starts
 };
-uint32_t join_cap();                       // elements per join chunk (table capacity)
+uint32_t join_cap();                       // entries per join chunk (table capacity)
 uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch of max_size
-// total = elements of the `count` sketches (sizes the staging array)
-// Join layout (layout.hip): value groups of 64 hash buckets.  join_layout_groups:
-// G = 2^log_b / 64 (>= 1); bounds u64[G + 1].  join_layout_bounds computes the
-// group bounds of a set (quantiles averaged over up to 64 samples).
-// join_layout_build: the layout of sketches (data, starts, sizes)[0, count)
-// with the caller's bounds, or (d_bounds null) bounds computed from these
-// sketches; temp: join_layout_temp_bytes; *d_stat is raised to the largest
-// block-bucket population.  Three launches, no host synchronisation.
+// G = 2^log_b / 8 value groups (>= 1); bounds: (G + 1) values of ew words.
+// join_layout_bounds computes the group bounds of a set (quantiles averaged
+// over up to 64 samples).  join_layout_build: the layout of sketches (data,
+// starts, sizes)[0, count) with the caller's bounds, or (d_bounds null)
+// bounds computed from these sketches; temp: join_layout_temp_bytes;
+// d_stat[0] is raised to the largest block-bucket population (entries),
+// d_stat[1] counts groups the build could not place (layout invalid).  Three
+// launches, no host synchronisation.
 uint32_t join_layout_groups(uint32_t log_b);
+uint32_t join_layout_boff_words(uint32_t log_b);  // B + NR: one block's boff row
 hipError_t join_layout_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                              uint32_t count, uint32_t log_b, uint64_t* bounds, hipStream_t s);
-size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b);
+                              uint32_t count, uint32_t log_b, int ew, uint64_t* bounds, hipStream_t s);
+size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, int ew);
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
-                             uint32_t count, uint32_t log_b, const uint64_t* d_bounds, void* temp,
-                             uint64_t* out_data, uint8_t* out_ids, uint32_t* out_boff,
-                             uint64_t* out_bstart, uint32_t* d_stat, hipStream_t s);
+                             uint32_t count, uint32_t log_b, int ew, const uint64_t* d_bounds, void* temp,
+                             uint64_t* out_vals, uint64_t* out_masks, uint32_t* out_boff,
+                             uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s);
 // Tiles of the n x n (sym: upper-triangle range [tile_begin, tile_end), or
 // with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
 // written) or rows x n matrix; tile (I, J) reads row block r_blk0 + I of
@@ -200,9 +204,21 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
 // maps global block indices onto a layout whose block 0 is blk0).  packed:
 // out = [tile - tile_begin][64][64].  Counts are added to `out`.
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
-                       uint32_t n, uint32_t log_b, bool sym, uint32_t row_begin, uint32_t row_end,
+                       uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
-                       int32_t* out, hipStream_t s);
+                       int32_t* out, bool check, hipStream_t s);
+// SKS check builds: invariant violations counted since the last call (and reset)
+unsigned long long join_check_take();
+unsigned long long layout_check_take();
+
+// ---- containment / ANI (ani.hip) ------------------------------------------------------------
+// Dense: ani[i * n + j] from the n x n count matrix (|S_i| on its diagonal).
+hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, int kmer_num_ones, double* cont, double* ani,
+                             hipStream_t s);
+// Packed symmetric tiles (I, J) = tiles[2t], tiles[2t + 1]: out [t][2][64][64]
+// (both orientations of each pair); sizes[i] = |S_i|.
+hipError_t launch_ani_tiles(const int32_t* packed, const uint32_t* tiles, uint64_t n_tiles, uint32_t n,
+                            const int32_t* sizes, int kmer_num_ones, double* out, hipStream_t s);
 
 // ---- device FASTA ingress (ingress.hip) -------------------------------------------------
 // strings_from_fasta on the device: writes the host parser's record stream

@@ -1,14 +1,19 @@
 """Multi-GPU orchestration for all-vs-all ANI (one process per GPU).
 
 The reference parallelises with cilk_for over files (kmer_set.cpp:124) and over
-pairs (kmer_set.cpp:179) inside one process.  Here:
-  * genomes are sharded across ranks (each rank sketches its own; no collective),
-  * the padded per-rank sketches are all-gathered (RCCL over xGMI for "nccl"),
-  * the upper-triangle 64x64 tiles of the N x N pair matrix are split evenly
-    across ranks (sks_intersect_sym writes each count to both halves), and
-  * the per-rank partial matrices are summed with one all-reduce.
-The functions take the count kernel as a callable so the same orchestration is
-exercised on CPU with gloo in tests/test_dist_cpu.py.
+pairs (kmer_set.cpp:179) inside one process.  Here (all_vs_all_join):
+  * genomes are sharded across ranks in whole 64-sketch blocks; each rank
+    sketches its own and builds the join layout of its own blocks,
+  * every rank's sketches are broadcast by their owner (RCCL over xGMI for
+    "nccl"), and each receiver joins its blocks with the source's as they land
+    (a fixed tile plan splits the upper-triangle 64x64 tiles between ranks),
+  * containment / ANI are computed per tile on the rank that counted it, and
+    the packed count tiles are assembled into the n x n matrix on one rank
+    only when asked.
+Config 5 shards seeds (seed_sweep: one all-reduce of ANI sums) and config 3
+shards genomes or one genome's chunks (sketch_genome_sharded).  The functions
+take the kernels as callables so the same orchestration is exercised on CPU
+with gloo in tests/test_dist_cpu.py.
 """
 import functools
 
@@ -98,32 +103,6 @@ def all_vs_all(local, local_sizes, n_genomes, world, rank, count_sym, out=None):
     return out
 
 
-def row_shard(n, world, rank):
-    return rank * n // world, (rank + 1) * n // world
-
-
-def all_vs_all_rows(local, local_sizes, n_genomes, world, rank, count_rows):
-    """Row-block form of all_vs_all for sketches of any element width — (lo, hi)
-    k-mers for 32 < w <= 64, which the join / merge tiles do not take: the padded
-    sketches are all-gathered as in all_vs_all, rank r counts rows [r0, r1) against
-    every column with count_rows(sketches, sizes, n, r0, r1, out_rows) (the contract
-    of sks_intersect_all: out_rows[(i - r0) * n + j] = |S_i ∩ S_j|), and the row
-    blocks are all-gathered.  Returns the full n x n int32 matrix on every rank."""
-    src, src_sz = gather_sketches(local, local_sizes, world)
-    r0, r1 = row_shard(n_genomes, world, rank)
-    rows = torch.zeros((r1 - r0, n_genomes), dtype=torch.int32, device=local.device)
-    if r1 > r0:
-        count_rows(src, src_sz, n_genomes, r0, r1, rows)
-    if _solo(world):
-        return rows
-    per = (n_genomes + world - 1) // world
-    pad = torch.zeros((per, n_genomes), dtype=torch.int32, device=local.device)
-    pad[: r1 - r0] = rows
-    g = _gather_flat(pad.reshape(-1), world).view(world, per, n_genomes)
-    return torch.cat([g[r, : row_shard(n_genomes, world, r)[1] - row_shard(n_genomes, world, r)[0]]
-                      for r in range(world)])
-
-
 # ---- seed sweep (BASELINE config 5) ----------------------------------------------------
 # The reference sweeps (w, k) configurations serially, re-sketching every file
 # per configuration (kmer-sketching.cpp:214-239 around :151-212).  Config 5 runs
@@ -154,14 +133,12 @@ def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
     return acc, mine
 
 
-# ---- tile plan, packed tiles, one receiving rank ------------------------------------------
+# ---- stream ordering, packed tiles, one receiving rank ---------------------------------------
 # Each rank counts a fixed plan of upper-triangle 64x64 tiles (tile_plan): the
 # tiles of its own blocks first — from its own data, while the exchange is in
 # flight — then its half of every cross-rank block pair.  Counts stay packed
-# ([tile][64][64] int32, 16 KB per tile) and go to ONE rank (dst), where the
-# n x n matrix is assembled: no rank holds a matrix it does not need and no
-# collective carries n^2 words (a dense all-reduce moves 2 (N-1)/N n^2 words
-# through every rank).
+# ([tile][64][64] int32, 16 KB per tile); when asked they go to ONE rank (dst),
+# where the n x n matrix is assembled: no collective carries n^2 words.
 
 def _ctx_waits_for_torch(ctx):
     """Order the context's HIP stream after work queued so far on torch's current
@@ -185,74 +162,9 @@ def _ctx_torch_stream(ctx):
     return torch.cuda.default_stream() if h == 0 else torch.cuda.ExternalStream(h)
 
 
-@functools.lru_cache(maxsize=64)
-def tile_plan(n_genomes, world, rank):
-    """(local, remote) int64 arrays [T, 2] of the upper-triangle tiles (I, J) that
-    `rank` counts.  local: both blocks in the rank's own block range
-    (block_shard), countable from its own sketches; remote: for every other rank
-    q, half of the tiles pairing the two ranks' blocks (row-major over the pair,
-    the lower rank takes the first half).  Every tile of the n x n upper
-    triangle is in exactly one rank's plan; per-rank counts differ by at most
-    one tile per rank pair (plus a short last rank)."""
-    nb = (n_genomes + TILE - 1) // TILE
-    bpr = block_shard(n_genomes, world, rank)[0]
-
-    def blocks(q):
-        return np.arange(min(nb, q * bpr), min(nb, (q + 1) * bpr), dtype=np.int64)
-
-    mine = blocks(rank)
-    I, J = np.meshgrid(mine, mine, indexing="ij")
-    keep = I <= J
-    local = np.stack([I[keep], J[keep]], axis=1) if mine.size else np.zeros((0, 2), np.int64)
-    remote = [np.zeros((0, 2), np.int64)]
-    for q in range(world):
-        if q == rank:
-            continue
-        a, b = min(rank, q), max(rank, q)
-        ba, bb = blocks(a), blocks(b)
-        if not ba.size or not bb.size:
-            continue
-        I, J = np.meshgrid(ba, bb, indexing="ij")
-        pairs = np.stack([I.reshape(-1), J.reshape(-1)], axis=1)
-        h = (len(pairs) + 1) // 2
-        remote.append(pairs[:h] if rank == a else pairs[h:])
-    local, remote = local.reshape(-1, 2), np.concatenate(remote).reshape(-1, 2)
-    local.flags.writeable = False  # cached: shared by every caller
-    remote.flags.writeable = False
-    return local, remote
-
-
-def _max_over_many(xs, world, device):
-    if _solo(world):
-        return [int(x) for x in xs]
-    t = torch.tensor([int(x) for x in xs], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return [int(v) for v in t.tolist()]
-
-
-def _gather_start(ts, world):
-    """Starts the all-gathers of flat tensors (rank-major); returns a function
-    that waits for them and returns the gathered tensors.  With RCCL the
-    gathers run on the collective stream while the caller queues other work."""
-    if dist.get_backend() == "nccl":
-        outs, works = [], []
-        for t in ts:
-            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
-            works.append(dist.all_gather_into_tensor(out, t.contiguous(), async_op=True))
-            outs.append(out)
-
-        def finish():
-            for w in works:
-                w.wait()
-            return outs
-        return finish
-    res = _gather_many(ts, world)  # gloo: through host memory, synchronously
-    return lambda: res
-
-
 def _gather_tiles(parts, world, dst):
-    """parts: int32 [Tmax, 64, 64] (padded) of this rank -> [world, Tmax, 64, 64]
-    on dst (None elsewhere), or on every rank when dst is None."""
+    """parts: [Tmax, 64, 64] (padded) of this rank -> [world, Tmax, 64, 64] on dst
+    (None elsewhere), or on every rank when dst is None."""
     if dst is None:
         return _gather_flat(parts.reshape(-1), world).view((world,) + tuple(parts.shape))
     nccl = dist.get_backend() == "nccl"
@@ -297,14 +209,22 @@ def place_tiles(mat, tiles, parts, n):
     return mat
 
 
-# ---- all-vs-all over gathered join layouts ------------------------------------------------
-# The join kernel's input (sks_join_layout_build) is built per 64-sketch block,
-# so each rank builds the layout of its OWN block-aligned genome range, counts
-# the tiles of its own blocks on it while the ranks all-gather their layouts
-# (9 B per element + bucket starts, about the padded sketches' bytes; nothing
-# is rebuilt on every rank), then counts its cross-rank tiles on the gathered
-# layout.  Block k of the gathered layout is block k - r*bpr of rank r, so its
-# start is shifted by r * (padded layout size).
+# ---- all-vs-all over join layouts, sketches exchanged per source rank ---------------------
+# The join kernel's input (sks_join_layout_build) is built per 64-sketch block.
+# Each rank owns whole blocks (block_shard), sketches them and builds the layout
+# of its own blocks; it counts its own blocks' tiles on that layout at once.
+# Every rank's sketches are then broadcast by their owner (all ranks issue the
+# broadcasts in rank order; with RCCL they run on the collective stream), and
+# as source q's sketches land, the receiver builds q's block layout and counts
+# its share of the (own, q) tiles (tile_plan), while the later sources are
+# still in flight.  Raw sketches travel (8 B per element, or 16 B for 128-bit
+# k-mers) rather than layouts: a deduplicated layout keeps its regions at raw
+# offsets (16 B per raw element with the mask), and rebuilding a peer's layout
+# (~90 us for all of config 4) costs less than moving twice the bytes.  All
+# layouts share rank 0's value-group bounds (broadcast first), so every pair of
+# blocks is bucketed alike.  Counts stay packed per tile; containment / ANI are
+# computed per tile on the rank that counted it (sks_ani_tiles); the count
+# tiles are assembled into the n x n matrix only where asked (dst).
 
 def block_shard(n_genomes, world, rank):
     """(blocks per rank, g0, g1): genome range of `rank`, whole 64-sketch blocks."""
@@ -312,6 +232,197 @@ def block_shard(n_genomes, world, rank):
     bpr = max(1, (n_blk + world - 1) // world)
     g0 = min(n_genomes, rank * bpr * TILE)
     return bpr, g0, min(n_genomes, g0 + bpr * TILE)
+
+
+@functools.lru_cache(maxsize=64)
+def tile_plan_by_peer(n_genomes, world, rank):
+    """(local, remote): local int64 [T, 2] — the upper-triangle tiles (I, J)
+    with both blocks in the rank's own block range; remote — a list over ranks
+    q of the tiles pairing the two ranks' blocks that `rank` counts (row-major
+    over the pair, the lower rank takes the first half; I is in the lower
+    rank's blocks, J in the higher's; empty for q == rank)."""
+    nb = (n_genomes + TILE - 1) // TILE
+    bpr = block_shard(n_genomes, world, rank)[0]
+
+    def blocks(q):
+        return np.arange(min(nb, q * bpr), min(nb, (q + 1) * bpr), dtype=np.int64)
+
+    mine = blocks(rank)
+    I, J = np.meshgrid(mine, mine, indexing="ij")
+    keep = I <= J
+    local = np.stack([I[keep], J[keep]], axis=1).reshape(-1, 2) if mine.size else np.zeros((0, 2), np.int64)
+    remote = []
+    for q in range(world):
+        a, b = min(rank, q), max(rank, q)
+        ba, bb = blocks(a), blocks(b)
+        if q == rank or not ba.size or not bb.size:
+            remote.append(np.zeros((0, 2), np.int64))
+            continue
+        I, J = np.meshgrid(ba, bb, indexing="ij")
+        pairs = np.stack([I.reshape(-1), J.reshape(-1)], axis=1)
+        h = (len(pairs) + 1) // 2
+        remote.append(pairs[:h] if rank == a else pairs[h:])
+    local.flags.writeable = False  # cached: shared by every caller
+    for r in remote:
+        r.flags.writeable = False
+    return local, tuple(remote)
+
+
+def tile_plan(n_genomes, world, rank):
+    """(local, remote) int64 arrays [T, 2] of the upper-triangle tiles (I, J) that
+    `rank` counts: its own blocks' tiles, then its share of every cross-rank
+    block pair (tile_plan_by_peer, concatenated in rank order).  Every tile of
+    the n x n upper triangle is in exactly one rank's plan."""
+    local, remote = tile_plan_by_peer(n_genomes, world, rank)
+    return local, np.concatenate(remote).reshape(-1, 2)
+
+
+class Sketches:
+    """A rank's sketch set as tensors: data int64 [total * ew] (sketches back to
+    back), sizes int32 [n], starts int64 [n] (element index of each sketch)."""
+
+    def __init__(self, data, sizes, ew=1, starts=None):
+        self.data, self.sizes, self.ew = data, sizes, ew
+        self.n = int(sizes.numel())
+        if starts is None:
+            starts = torch.zeros(self.n, dtype=torch.int64, device=sizes.device)
+            if self.n > 1:
+                starts[1:] = torch.cumsum(sizes[:-1].to(torch.int64), 0)
+        self.starts = starts
+        self.total = int(data.numel()) // ew
+
+
+def _exchange_start(own, ns, totals, world, rank):
+    """Starts one broadcast per source rank (in rank order, on every rank) of
+    the source's sketches; returns wait(q) -> Sketches of rank q.  With RCCL the
+    broadcasts run on the collective stream and wait(q) only orders torch's
+    current stream after source q's (the host does not block); with gloo the
+    data goes through host memory, synchronously."""
+    ew, dev = own.ew, own.data.device
+    nccl = dist.get_backend() == "nccl"
+    bufs = []
+    for q in range(world):
+        if q == rank:
+            bufs.append((own.data, own.sizes))
+        else:
+            bufs.append((torch.empty(max(totals[q] * ew, 1), dtype=torch.int64, device=dev if nccl else "cpu"),
+                         torch.empty(max(ns[q], 1), dtype=torch.int32, device=dev if nccl else "cpu")))
+    works = []
+    for q in range(world):
+        d, sz = bufs[q]
+        nd, nz = totals[q] * ew, ns[q]
+        if not nccl and q == rank:
+            d, sz = d.cpu(), sz.cpu()
+        ws = []
+        for t, k in ((d, nd), (sz, nz)):
+            if k:  # every rank knows the sizes: all skip empty sources alike
+                ws.append(dist.broadcast(t[:k], src=q, async_op=nccl))
+        works.append(ws)
+        if not nccl:
+            bufs[q] = (d, sz)
+
+    def wait(q):
+        if q == rank:
+            return own
+        for w in works[q]:
+            if nccl and w is not None:
+                w.wait()
+        d, sz = bufs[q]
+        if not nccl:
+            d, sz = d.to(dev), sz.to(dev)
+        return Sketches(d[:totals[q] * ew], sz[:ns[q]], ew)
+    return wait
+
+
+class JoinResult:
+    """What all_vs_all_join leaves on a rank.  tiles: int64 [T, 2] (None for one
+    rank without a process group, whose counts / ani are the dense n x n
+    matrices); counts: packed int32 [T, 64, 64]; ani: float64 [T, 2, 64, 64]
+    (both orientations, sks_ani_tiles) or dense, when asked; matrix: the n x n
+    int32 counts on the assembling rank(s), else None."""
+
+    def __init__(self):
+        self.tiles = self.counts = self.ani = self.matrix = None
+
+
+def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None):
+    """All-vs-all intersection counts (kmer_set.cpp:143-184 over the
+    generate_all_pairs_from_vector list, generators.hpp:44-58), and ANI when
+    ani_ones (the k of binomial_estimator) is given.
+
+    mine: Sketches of this rank's block-aligned genomes (block_shard).
+    ops: the kernels (GpuJoinOps on the GPU; a numpy restatement in the CPU
+    tests): ew; bounds(src, log_b) -> group bounds tensor; build(src, log_b,
+    bounds, key) -> layout (cached by key); count(n, log_b, rows, r_blk0, cols,
+    c_blk0, tiles, out) — the contract of sks_intersect_layout_pair_tiles
+    (tiles None: every upper-triangle tile into the dense matrix out);
+    ani_matrix(counts, n, k); ani_tiles(tiles, packed, sizes, n, k).
+    dst: the rank that assembles the n x n count matrix (None: none, "all":
+    every rank).  Returns a JoinResult."""
+    res = JoinResult()
+    bpr, g0, g1 = block_shard(n_genomes, world, rank)
+    solo = _solo(world)
+    mx = int(mine.sizes.max().item()) if mine.n else 0
+    if solo:
+        ns, totals, mxs = [mine.n], [mine.total], [mx]
+    else:
+        meta = _gather_flat(torch.tensor([mine.n, mine.total, mx], dtype=torch.int64, device=device), world)
+        meta = meta.view(world, 3).tolist()
+        ns, totals, mxs = [m[0] for m in meta], [m[1] for m in meta], [m[2] for m in meta]
+    log_b = log_b_for(max(max(mxs), 1))
+    if solo:
+        lay = ops.build(mine, log_b, None, "own")
+        out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+        if n_genomes:
+            ops.count(n_genomes, log_b, lay, 0, lay, 0, None, out)
+        res.counts = res.matrix = out
+        if ani_ones is not None:
+            res.ani = ops.ani_matrix(out, n_genomes, ani_ones)
+        return res
+    # rank 0's group bounds, shared by every layout (blocks of different ranks
+    # are joined bucket by bucket)
+    gb = ops.bounds(mine, log_b) if rank == 0 else ops.bounds_like(log_b)
+    gb = _broadcast(gb, 0, world)
+    local, remote = tile_plan_by_peer(n_genomes, world, rank)
+    T = len(local) + sum(len(r) for r in remote)
+    parts = torch.zeros((max(T, 1), TILE, TILE), dtype=torch.int32, device=device)
+    wait = _exchange_start(mine, ns, totals, world, rank)
+    own = ops.build(mine, log_b, gb, "own") if mine.n else None
+    if len(local):  # the rank's own tiles while the peers' sketches travel
+        ops.count(n_genomes, log_b, own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
+    off = len(local)
+    srcs = [None] * world
+    for q in range(world):
+        srcs[q] = wait(q)
+        tq = remote[q]
+        if q == rank or not len(tq):
+            continue
+        lq = ops.build(srcs[q], log_b, gb, ("peer", q))
+        bq = block_shard(n_genomes, world, q)[1] // TILE
+        if rank < q:
+            ops.count(n_genomes, log_b, own, g0 // TILE, lq, bq, tq, parts[off:off + len(tq)])
+        else:
+            ops.count(n_genomes, log_b, lq, bq, own, g0 // TILE, tq, parts[off:off + len(tq)])
+        off += len(tq)
+    res.tiles = np.concatenate([local] + list(remote)).reshape(-1, 2)
+    res.counts = parts[:T]
+    if ani_ones is not None:
+        sizes_all = torch.cat([srcs[q].sizes for q in range(world)])
+        res.ani = ops.ani_tiles(res.tiles, res.counts, sizes_all, n_genomes, ani_ones)
+    if dst is None:
+        return res
+    plans = [tile_plan(n_genomes, world, q) for q in range(world)]
+    counts = [len(pl[0]) + len(pl[1]) for pl in plans]
+    pad = torch.zeros((max(max(counts), 1), TILE, TILE), dtype=torch.int32, device=device)
+    pad[:T] = res.counts
+    gathered = _gather_tiles(pad, world, None if dst == "all" else dst)
+    if gathered is None:
+        return res
+    tiles = np.concatenate([np.concatenate(pl) for pl in plans]).reshape(-1, 2)
+    got = torch.cat([gathered[q, :counts[q]] for q in range(world)])
+    out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+    res.matrix = place_tiles(out, tiles, got, n_genomes)
+    return res
 
 
 def _max_over(x, world, device):
@@ -361,152 +472,97 @@ def _broadcast(t, src, world):
     return t
 
 
-def layout_groups(log_b):
-    """Value groups of a join layout with 2^log_b buckets (sks_join_layout_groups)."""
-    return 1 << (log_b - 4) if log_b > 4 else 1
+class GpuJoinOps:
+    """The kernels of all_vs_all_join on the GPU through libsks: a context `ctx`
+    and the k-mer width (ew = 1: u64, 2: 128-bit).  Layout buffers persist per
+    build key across calls of the same shape; the context's HIP stream is
+    ordered after torch's current stream before its kernels and torch's after
+    them, so a context on any stream works with the collectives on torch's."""
 
+    def __init__(self, ctx, ew=1):
+        import sksffi
+        self.sksffi, self.ctx, self.ew = sksffi, ctx, ew
+        self.bufs, self.tile_cache, self.keep = {}, {}, {}
 
-def all_vs_all_join(n_genomes, world, rank, local_max_size, local_total, log_b_for, build, count,
-                    device="cpu", out=None, dst=0, bounds=None):
-    """n x n int32 intersection matrix on rank `dst` (None on the others; on
-    every rank when dst is None).
+    def bounds_like(self, log_b):
+        return torch.empty((self.sksffi.join_layout_groups(log_b) + 1) * self.ew, dtype=torch.int64, device="cuda")
 
-    build(log_b, pad, bounds) -> (data u64[], ids u8[], boff u32[], bstart u64[]):
-    the join layout of this rank's block-aligned genomes (block_shard), with the
-    value-group bounds `bounds` (an int64 tensor of layout_groups(log_b) + 1
-    words; None: the rank's own).  Layouts joined with each other must share
-    bounds: with a process group, rank 0 computes them (bounds(log_b) -> tensor)
-    and broadcasts them before the builds.  pad is None
-    for one rank without a process group; otherwise (cap_e, bpr), and the
-    buffers must have exactly cap_e data / id entries, bpr * (B + 1) bucket
-    starts and bpr + 1 block starts (entries past the rank's own blocks are never
-    read), so they are all-gathered as they are.  cap_e is the largest rank's
-    element total (one all-reduce carries it with the largest sketch size).
-    count(n, log_b, layout, blk0, tiles, out) adds the counts of `tiles` (int64
-    [T, 2] global block indices, I <= J) to out — the packed int32 [T, 64, 64],
-    or the n x n int32 matrix (both halves) when out is 2-D — reading a layout
-    whose block 0 is global block blk0: the contract of
-    sks_intersect_layout_tiles.  One rank without a process group counts every
-    tile straight into the matrix.
+    def bounds(self, src, log_b):
+        b = self.bounds_like(log_b)
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.join_layout_bounds(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n, log_b,
+                                    b.data_ptr(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+        self.keep["bounds"] = src
+        return b
 
-    The rank counts its tile_plan: its own blocks' tiles from its own layout
-    while the layouts are being gathered, then its share of the cross-rank
-    tiles; the packed tiles go to dst, which assembles the matrix.  The bucket
-    count comes from the largest sketch (counts are exact at any: k_join cuts a
-    bucket above its table into sub-chunks)."""
-    bpr, g0, g1 = block_shard(n_genomes, world, rank)
-    solo = _solo(world)
-    max_all, cap_e = _max_over_many([local_max_size, local_total], world, device)
-    log_b = log_b_for(max(max_all, 1))
-    local, remote = tile_plan(n_genomes, world, rank)
-    T = len(local) + len(remote)
-    gb = None
-    if not solo and bounds is not None:
-        gb = bounds(log_b) if rank == 0 else \
-            torch.empty(layout_groups(log_b) + 1, dtype=torch.int64, device=device)
-        gb = _broadcast(gb, 0, world)
-    lay = build(log_b, None if solo else (max(1, cap_e), bpr), gb)
-    if solo:
-        if out is None:
-            out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+    def build(self, src, log_b, gb, key):
+        nb = (src.n + TILE - 1) // TILE
+        shape = (max(src.total, 1), log_b, max(nb, 1))
+        if self.bufs.get(key, (None,))[0] != shape:
+            BW = self.sksffi.join_layout_boff_words(log_b)
+            self.bufs[key] = (shape, (torch.empty(shape[0] * self.ew, dtype=torch.int64, device="cuda"),
+                                      torch.empty(shape[0], dtype=torch.int64, device="cuda"),
+                                      torch.zeros(shape[2] * BW, dtype=torch.int32, device="cuda"),
+                                      torch.zeros(shape[2] + 1, dtype=torch.int64, device="cuda")))
+        lay = self.bufs[key][1]
+        if src.n:
+            _ctx_waits_for_torch(self.ctx)  # the buffers' previous readers, the source's writers
+            self.ctx.join_layout_build(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
+                                       log_b, *(t.data_ptr() for t in lay), stat=False, total=src.total,
+                                       bounds=gb.data_ptr() if gb is not None else None, elem_words=self.ew)
+            _torch_waits_for_ctx(self.ctx)
+        self.keep[key] = (src, gb)  # alive until torch's stream is past the build
+        return lay
+
+    def _tiles(self, tiles):
+        key = tiles.tobytes()  # the plan repeats every step: upload it once
+        if key not in self.tile_cache:
+            if len(self.tile_cache) > 64:
+                self.tile_cache.clear()
+            self.tile_cache[key] = torch.from_numpy(np.array(tiles, dtype=np.int32)).reshape(-1, 2).to("cuda")
+        return self.tile_cache[key]
+
+    def count(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, out):
+        _ctx_waits_for_torch(self.ctx)
+        if tiles is None:
+            self.ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in rows), 0, 0, 0,
+                                            self.sksffi.intersect_sym_tiles(n), False, out.data_ptr(),
+                                            elem_words=self.ew)
         else:
-            out.zero_()
-        if T:
-            count(n_genomes, log_b, lay, 0, local, out)
+            tl = self._tiles(tiles)
+            self.ctx.intersect_layout_pair_tiles(n, log_b, [t.data_ptr() for t in rows], r_blk0,
+                                                 [t.data_ptr() for t in cols], c_blk0, tl.data_ptr(), 0,
+                                                 tl.shape[0], out.dim() == 3, out.data_ptr(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+
+    def ani_matrix(self, counts, n, k):
+        ani = torch.empty((n, n), dtype=torch.float64, device="cuda")
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.ani_matrix(counts.data_ptr(), n, k, ani.data_ptr())
+        _torch_waits_for_ctx(self.ctx)
+        return ani
+
+    def ani_tiles(self, tiles, packed, sizes, n, k):
+        out = torch.empty((len(tiles), 2, TILE, TILE), dtype=torch.float64, device="cuda")
+        if len(tiles):
+            tl = self._tiles(tiles)
+            sz = sizes.to(device="cuda", dtype=torch.int32).contiguous()
+            _ctx_waits_for_torch(self.ctx)
+            self.ctx.ani_tiles(packed.data_ptr(), tl.data_ptr(), len(tiles), n, sz.data_ptr(), k, out.data_ptr())
+            _torch_waits_for_ctx(self.ctx)
+            self.keep["ani_sizes"] = sz
         return out
-    plans = [tile_plan(n_genomes, world, q) for q in range(world)]
-    sizes = [len(pl[0]) + len(pl[1]) for pl in plans]
-    # the rank's packed tiles, padded to the largest plan: the gather's send buffer
-    parts = torch.zeros((max(max(sizes), 1), TILE, TILE), dtype=torch.int32, device=device)
-    cap_e = max(1, cap_e)
-    finish = _gather_start(list(lay), world)
-    if len(local):  # the rank's own tiles while the layouts travel
-        count(n_genomes, log_b, lay, g0 // TILE, local, parts[:len(local)])
-    g_data, g_ids, g_boff, g_bst = finish()
-    # block k of rank r starts at r * cap_e in the gathered data
-    g_bst = g_bst.view(world, bpr + 1)[:, :bpr] + \
-        torch.arange(world, device=g_bst.device, dtype=torch.int64).view(world, 1) * cap_e
-    g_bst = torch.cat([g_bst.reshape(-1),
-                       torch.full((1,), world * cap_e, dtype=torch.int64, device=g_bst.device)])
-    if len(remote):
-        count(n_genomes, log_b, (g_data, g_ids, g_boff, g_bst), 0, remote, parts[len(local):T])
-    gathered = _gather_tiles(parts, world, dst)
-    if gathered is None:
-        return None
-    tiles = np.concatenate([np.concatenate(pl) for pl in plans]).reshape(-1, 2)
-    got = torch.cat([gathered[q, :sizes[q]] for q in range(world)])
-    if out is None:
-        out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
-    else:
-        out.zero_()
-    return place_tiles(out, tiles, got, n_genomes)
 
 
-def join_layout_fns(ctx, ss, local_sizes, device="cuda", cache=None):
-    """The build / count / bounds callables of all_vs_all_join for this rank's sketches
-    on the GPU: `ss` is the rank's SketchSet (None when it holds no genome),
-    `local_sizes` its sizes (numpy).  build(log_b, pad) runs
-    sks_join_layout_build into device buffers (kept in `cache` across calls of
-    the same shape) and returns them on `device`; count(...) runs
-    sks_intersect_layout_tiles (on the GPU, staging through `device` tensors
-    when that is the CPU, as with gloo).  The context's stream is ordered after
-    torch's current stream before its kernels and torch's after them, so a
-    context on any stream works with the collectives on torch's."""
-    n_local = len(local_sizes)
-    nb_local = (n_local + TILE - 1) // TILE
-    data, starts, sizes = ss.device_ptrs() if ss is not None else (0, 0, 0)
-    tot = int(local_sizes.astype("int64").sum()) if n_local else 0
-    cache = {} if cache is None else cache
-    tile_cache = cache.setdefault("_tiles", {}) if isinstance(cache, dict) else {}
-    keep = {}
-
-    def bounds(log_b):
-        b = torch.empty(layout_groups(log_b) + 1, dtype=torch.int64, device="cuda")
-        _ctx_waits_for_torch(ctx)
-        ctx.join_layout_bounds(data, starts, sizes, n_local, log_b, b.data_ptr())
-        _torch_waits_for_ctx(ctx)
-        keep["bounds"] = b
-        return b.to(device)
-
-    def build(log_b, pad=None, gbounds=None):
-        B1 = (1 << log_b) + 1
-        gb = gbounds.to("cuda").contiguous() if gbounds is not None else None
-        # padded (all_vs_all_join with a process group): the send buffers
-        # themselves, cap_e elements and bpr blocks, gathered as they are
-        cap_e, nb = pad if pad is not None else (max(tot, 1), max(nb_local, 1))
-        key = (cap_e, log_b, nb)
-        if key not in cache:  # layout buffers persist across steps
-            for k in [k for k in cache if k != "_tiles"]:
-                del cache[k]
-            cache[key] = (torch.empty(cap_e, dtype=torch.int64, device="cuda"),
-                          torch.empty(cap_e, dtype=torch.uint8, device="cuda"),
-                          torch.zeros(nb * B1, dtype=torch.int32, device="cuda"),
-                          torch.zeros(nb + 1, dtype=torch.int64, device="cuda"))
-        out = cache[key]
-        _ctx_waits_for_torch(ctx)  # the buffers' previous readers (gathers, joins)
-        ctx.join_layout_build(data, starts, sizes, n_local, log_b, *(t.data_ptr() for t in out), stat=False,
-                              total=tot, bounds=gb.data_ptr() if gb is not None else None)
-        _torch_waits_for_ctx(ctx)
-        keep["gb"] = gb
-        return tuple(t.to(device) for t in out)
-
-    def count(n, log_b, lay, blk0, tiles, out):
-        lay = [t.to("cuda") for t in lay]
-        key = ("tiles", tiles.tobytes())  # the plan repeats every step: upload it once
-        if key not in tile_cache:
-            if len(tile_cache) > 8:
-                tile_cache.clear()
-            tile_cache[key] = torch.from_numpy(np.array(tiles, dtype=np.int32)).reshape(-1, 2).to("cuda").contiguous()
-        tl = tile_cache[key]
-        tgt = out if out.is_cuda else torch.zeros(out.shape, dtype=out.dtype, device="cuda")
-        _ctx_waits_for_torch(ctx)
-        ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in lay), blk0, tl.data_ptr(), 0,
-                                   tl.shape[0], out.dim() == 3, tgt.data_ptr())
-        _torch_waits_for_ctx(ctx)
-        keep["last"] = (lay, tl)  # alive until torch's stream is past the kernel
-        if tgt is not out:
-            out.copy_(tgt.cpu())
-    return build, count, bounds
+def sketches_of(ss, ew=None):
+    """Sketches (zero-copy device views) of a SketchSet, or an empty set for None."""
+    if ss is None:
+        e = ew or 1
+        return Sketches(torch.zeros(0, dtype=torch.int64, device="cuda"),
+                        torch.zeros(0, dtype=torch.int32, device="cuda"), e)
+    d, st, sz = ss.device_tensors(torch.cuda.current_device())
+    return Sketches(d, sz, ss.elem_words, starts=st)
 
 
 # ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------

@@ -60,7 +60,9 @@ EXPORTED = [
     "sks_kmer_list_copy", "sks_ctx_device", "sks_sketch_set_info", "sks_sketch_set_set_names",
     "sks_sketch_set_name", "sks_sketch_set_save", "sks_sketch_set_load", "sks_sketch_set_concat",
     "sks_intersect_layout_tiles",
-    "sks_join_layout_bounds", "sks_join_layout_groups",
+    "sks_join_layout_bounds", "sks_join_layout_groups", "sks_join_layout_boff_words",
+    "sks_ctx_set_join_check", "sks_ctx_join_check_violations", "sks_intersect_layout_pair_tiles",
+    "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_tiles",
 ]
 
 _lib = None
@@ -119,15 +121,25 @@ def lib():
     L.sks_join_layout_log_b.restype = C.c_uint32
     L.sks_join_layout_capacity.argtypes = []
     L.sks_join_layout_capacity.restype = C.c_uint32
-    L.sks_join_layout_build.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint64, C.c_uint32, vp, vp, vp,
-                                        vp, vp, C.POINTER(C.c_uint32)]
-    L.sks_join_layout_bounds.argtypes = [vp, vp, vp, vp, C.c_uint32, C.c_uint32, vp]
+    L.sks_join_layout_build.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, vp,
+                                        vp, vp, vp, vp, C.POINTER(C.c_uint32)]
+    L.sks_join_layout_bounds.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32, vp]
     L.sks_join_layout_groups.argtypes = [C.c_uint32]
     L.sks_join_layout_groups.restype = C.c_uint32
-    L.sks_intersect_sym_layout.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint64,
+    L.sks_join_layout_boff_words.argtypes = [C.c_uint32]
+    L.sks_join_layout_boff_words.restype = C.c_uint32
+    L.sks_intersect_sym_layout.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_uint64,
                                            C.c_uint64, vp]
-    L.sks_intersect_layout_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp,
-                                             C.c_uint64, C.c_uint64, C.c_int, vp]
+    L.sks_intersect_layout_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_uint32,
+                                             vp, C.c_uint64, C.c_uint64, C.c_int, vp]
+    L.sks_intersect_layout_pair_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int, vp, vp, vp, vp,
+                                                  C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp, C.c_uint64,
+                                                  C.c_uint64, C.c_int, vp]
+    L.sks_sketch_set_export_csr.argtypes = [vp, vp, vp]
+    L.sks_ani_matrix.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, vp]
+    L.sks_ani_tiles.argtypes = [vp, vp, vp, C.c_uint64, C.c_uint32, vp, C.c_int, vp]
+    L.sks_ctx_set_join_check.argtypes = [vp, C.c_int]
+    L.sks_ctx_join_check_violations.argtypes = [vp, u64p]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_device.argtypes = [vp]
@@ -215,6 +227,11 @@ def join_layout_capacity():
 
 def join_layout_groups(log_b):
     return int(lib().sks_join_layout_groups(log_b))
+
+
+def join_layout_boff_words(log_b):
+    """u32 words of one block's boff row (2^log_b bucket starts + region ends)."""
+    return int(lib().sks_join_layout_boff_words(log_b))
 
 
 def intersect_sym_tiles(n):
@@ -317,41 +334,71 @@ class Context:
         check(fn(self.h, C.c_void_p(d_in), n, C.c_void_p(d_out), C.byref(k)))
         return int(k.value)
 
-    def join_layout_build(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_data, out_ids,
-                          out_boff, out_bstart, stat=True, total=None, bounds=None):
-        """sks_join_layout_build; returns the largest block-bucket population, or
-        None with stat=False (no read-back).  total: the sizes' sum when known
-        (with stat=False the call then does not wait for the stream at all);
-        bounds: device pointer of the group bounds (None: the set's own)."""
+    def join_layout_build(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_vals, out_masks,
+                          out_boff, out_bstart, stat=True, total=None, bounds=None, elem_words=1):
+        """sks_join_layout_build; returns the largest block-bucket population
+        (entries; 2**32 - 1: layout invalid), or None with stat=False (no
+        read-back).  total: the sizes' sum when known (with stat=False the call
+        then does not wait for the stream at all); bounds: device pointer of the
+        group bounds (None: the set's own)."""
         mx = C.c_uint32(0)
         check(lib().sks_join_layout_build(self.h, C.c_void_p(data_ptr), C.c_void_p(starts_ptr),
-                                          C.c_void_p(sizes_ptr), n,
+                                          C.c_void_p(sizes_ptr), elem_words, n,
                                           (1 << 64) - 1 if total is None else int(total), log_b,
                                           C.c_void_p(bounds) if bounds else None,
-                                          C.c_void_p(out_data), C.c_void_p(out_ids), C.c_void_p(out_boff),
+                                          C.c_void_p(out_vals), C.c_void_p(out_masks), C.c_void_p(out_boff),
                                           C.c_void_p(out_bstart), C.byref(mx) if stat else None))
         return mx.value if stat else None
 
-    def join_layout_bounds(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_bounds):
+    def join_layout_bounds(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_bounds, elem_words=1):
         """sks_join_layout_bounds: the set's group bounds (device pointer out_bounds,
-        join_layout_groups(log_b) + 1 words)."""
+        (join_layout_groups(log_b) + 1) * elem_words words)."""
         check(lib().sks_join_layout_bounds(self.h, C.c_void_p(data_ptr), C.c_void_p(starts_ptr),
-                                           C.c_void_p(sizes_ptr), n, log_b, C.c_void_p(out_bounds)))
+                                           C.c_void_p(sizes_ptr), elem_words, n, log_b, C.c_void_p(out_bounds)))
 
-    def intersect_sym_layout(self, n, log_b, data, ids, boff, bstart, tile_begin, tile_end, out):
-        check(lib().sks_intersect_sym_layout(self.h, n, log_b, C.c_void_p(data), C.c_void_p(ids),
+    def intersect_sym_layout(self, n, log_b, vals, masks, boff, bstart, tile_begin, tile_end, out,
+                             elem_words=1):
+        check(lib().sks_intersect_sym_layout(self.h, n, log_b, elem_words, C.c_void_p(vals), C.c_void_p(masks),
                                              C.c_void_p(boff), C.c_void_p(bstart), tile_begin,
                                              tile_end, C.c_void_p(out)))
 
-    def intersect_layout_tiles(self, n, log_b, data, ids, boff, bstart, blk0, tiles, tile_begin, tile_end,
-                               packed, out):
+    def intersect_layout_tiles(self, n, log_b, vals, masks, boff, bstart, blk0, tiles, tile_begin, tile_end,
+                               packed, out, elem_words=1):
         """sks_intersect_layout_tiles: join tiles over a layout whose block 0 is
         global block blk0; counts ADDED to `out` (n x n both halves, or packed
         [tile][64][64]); tiles: device pointer of (I, J) u32 pairs, or 0."""
-        check(lib().sks_intersect_layout_tiles(self.h, n, log_b, C.c_void_p(data), C.c_void_p(ids),
+        check(lib().sks_intersect_layout_tiles(self.h, n, log_b, elem_words, C.c_void_p(vals), C.c_void_p(masks),
                                                C.c_void_p(boff), C.c_void_p(bstart), blk0,
                                                C.c_void_p(tiles) if tiles else None, tile_begin, tile_end,
                                                1 if packed else 0, C.c_void_p(out)))
+
+    def intersect_layout_pair_tiles(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, tile_begin, tile_end,
+                                    packed, out, elem_words=1):
+        """sks_intersect_layout_pair_tiles: rows / cols are (vals, masks, boff, bstart)
+        device pointers of two layouts; tiles: device pointer of (I, J) u32 pairs."""
+        check(lib().sks_intersect_layout_pair_tiles(self.h, n, log_b, elem_words,
+                                                    *(C.c_void_p(p) for p in rows), r_blk0,
+                                                    *(C.c_void_p(p) for p in cols), c_blk0, C.c_void_p(tiles),
+                                                    tile_begin, tile_end, 1 if packed else 0, C.c_void_p(out)))
+
+    def ani_matrix(self, counts, n, kmer_num_ones, ani, cont=None):
+        """sks_ani_matrix (device pointers): ANI of every ordered pair of the n x n counts."""
+        check(lib().sks_ani_matrix(self.h, C.c_void_p(counts), n, kmer_num_ones,
+                                   C.c_void_p(cont) if cont else None, C.c_void_p(ani)))
+
+    def ani_tiles(self, packed, tiles, n_tiles, n, sizes, kmer_num_ones, ani):
+        """sks_ani_tiles (device pointers): both orientations of every pair of packed tiles."""
+        check(lib().sks_ani_tiles(self.h, C.c_void_p(packed), C.c_void_p(tiles), n_tiles, n, C.c_void_p(sizes),
+                                  kmer_num_ones, C.c_void_p(ani)))
+
+    def set_join_check(self, on):
+        """sks_ctx_set_join_check: instrumented layout / join kernels (diagnostics)."""
+        check(lib().sks_ctx_set_join_check(self.h, 1 if on else 0))
+
+    def join_check_violations(self):
+        v = C.c_uint64(0)
+        check(lib().sks_ctx_join_check_violations(self.h, C.byref(v)))
+        return int(v.value)
 
     def set_intersect_kernel(self, kind):
         """INTERSECT_AUTO / _MERGE / _JOIN / _GLOBAL (sks.h); all give identical counts."""
@@ -553,13 +600,12 @@ class SketchSet:
                 L.sks_sketch_set_device_sizes(self.h))
 
     def device_tensors(self, device=0):
-        """Zero-copy torch views of the set's device arrays (u64 sketches only):
-        (data int64 [total], starts int64 [n], sizes int32 [n]).  The views do
+        """Zero-copy torch views of the set's device arrays: (data int64
+        [total * elem_words], starts int64 [n], sizes int32 [n]).  The views do
         not keep the set alive: use them while the set is."""
         import torch
-        assert self.elem_words == 1, "device_tensors: u64 sketches only"
         d, st, sz = self.device_ptrs()
-        total = int(self.sizes().astype(np.int64).sum())
+        total = int(self.sizes().astype(np.int64).sum()) * self.elem_words
         dev = torch.device("cuda", device)
 
         def view(ptr, n, typestr, dtype):

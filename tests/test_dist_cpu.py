@@ -1,8 +1,10 @@
-"""CPU (gloo, world_size 2 and 3): the multi-GPU all-vs-all orchestration of
-spaced-kmer-sketching_amd/sks_dist.py — genome sharding, the all-gather of
-padded sketches, the symmetric tile split and the all-reduce — assembles
-exactly the single-process matrix.  The count kernel is replaced by the
-oracle's merge count over the same tile contract (sks_intersect_sym)."""
+"""CPU (gloo, world_size 2 and 3): the multi-GPU orchestration of
+spaced-kmer-sketching_amd/sks_dist.py — genome / block sharding, the per-source
+sketch broadcasts and tile plan of all_vs_all_join, the padded-sketch gather of
+all_vs_all, the seed sweep and the sharded genome — assembles exactly the
+single-process result.  The kernels are replaced by numpy restatements of the
+same contracts (sks_join_layout_build / sks_intersect_layout_pair_tiles /
+sks_ani_tiles, sks_intersect_sym)."""
 import os
 import socket
 
@@ -83,67 +85,6 @@ def test_all_vs_all_gloo_matches_single_process(world):
         assert np.array_equal(results[r], want)
 
 
-# ---- all-vs-all in row blocks, (lo, hi) k-mers (w > 32): sks_dist.all_vs_all_rows ------
-WIDE_N, WIDE_W, WIDE_K, WIDE_STRIDE = 45, 40, 30, 160
-
-
-def _wide_sketches():
-    m = O.mask(WIDE_W, WIDE_K, 0)
-    out = []
-    for g in range(WIDE_N):
-        seq = synth.bases(2500, seed=60 + g % 3, mut_seed=700 + g, mut_rate=0.004 * (g % 6))
-        sk, _ = O.sketch(O.cut_runs(seq.tobytes()), WIDE_W, m, "frac", 20)
-        out.append(sk)  # (k, 2) uint64 (lo, hi)
-    return out
-
-
-def _oracle_count_rows(src, sizes, n, r0, r1, out):
-    """count_rows contract (sks_intersect_all row blocks) on padded (lo, hi) rows."""
-    a = src.numpy().view(np.uint64).reshape(src.shape[0], -1, 2)
-    sz = sizes.numpy()
-    for i in range(r0, r1):
-        for j in range(n):
-            out[i - r0, j] = O.intersect(a[i, : sz[i]], a[j, : sz[j]])
-
-
-def _rows_worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    sk = _wide_sketches()
-    per, g0, g1 = sks_dist.genome_shard(WIDE_N, world, rank)
-    local = torch.full((per, 2 * WIDE_STRIDE), -1, dtype=torch.int64)
-    local_sz = torch.zeros(per, dtype=torch.int32)
-    for i, g in enumerate(range(g0, g1)):
-        assert len(sk[g]) <= WIDE_STRIDE
-        local[i, : 2 * len(sk[g])] = torch.from_numpy(sk[g].reshape(-1).view(np.int64))
-        local_sz[i] = len(sk[g])
-    mat = sks_dist.all_vs_all_rows(local, local_sz, WIDE_N, world, rank, _oracle_count_rows)
-    q.put((rank, mat.numpy()))
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_all_vs_all_rows_wide_gloo(world):
-    """w = 40 (128-bit k-mers): padded (lo, hi) sketches gathered, each rank counts its
-    row block, row blocks gathered; every rank ends with the single-process matrix."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = dict(q.get(timeout=240) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    sk = _wide_sketches()
-    want = np.array([[O.intersect(sk[i], sk[j]) for j in range(WIDE_N)] for i in range(WIDE_N)])
-    assert want[0, 3] > 0  # related genomes share 128-bit k-mers
-    for r in range(world):
-        assert np.array_equal(results[r], want)
-
-
 def test_shard_arithmetic():
     for n in (1, 63, 64, 65, 1000):
         T = sks_dist.sym_tiles(n)
@@ -219,139 +160,180 @@ def test_seed_sweep_gloo_matches_single_process(world):
     assert want[0, 0] == 1.0 and 0 < want[0, 2] < 1
 
 
-# ---- config 4 over gathered join layouts (sks_dist.all_vs_all_join) ------------------
-PHI = np.uint64(0x9E3779B97F4A7C15)
+# ---- config 4 over per-source sketch broadcasts (sks_dist.all_vs_all_join) -----------------
+M64 = (1 << 64) - 1
 
 
-def _np_layout(sketches, log_b):
-    """numpy restatement of sks_join_layout_build: blocks of 64, hash buckets
-    (v * phi) >> (64 - log_b), block-major; returns torch tensors like the ABI."""
-    B = 1 << log_b
-    data, ids, boff, bstart, mx = [], [], [], [0], 0
-    for b0 in range(0, len(sketches), 64):
-        blk = sketches[b0:b0 + 64]
-        with np.errstate(over="ignore"):
-            hb = [(s * PHI) >> np.uint64(64 - log_b) if log_b else np.zeros(len(s), np.uint64)
-                  for s in blk]
-        start = len(data)
-        offs = []
-        for b in range(B):
-            offs.append(len(data) - start)
-            here = 0
-            for slot, (s, h) in enumerate(zip(blk, hb)):
-                sel = s[h == b]
-                data.extend(sel.tolist())
-                ids.extend([slot] * len(sel))
-                here += len(sel)
-            mx = max(mx, here)
-        offs.append(len(data) - start)
-        boff.extend(offs)
-        bstart.append(len(data))
-    as_t = lambda x, dt: torch.tensor(np.array(x, dtype=np.uint64).view(np.int64) if dt == torch.int64
-                                       else np.array(x), dtype=dt)
-    return (as_t(data, torch.int64), torch.tensor(ids, dtype=torch.uint8),
-            torch.tensor(boff, dtype=torch.int32), as_t(bstart, torch.int64), mx)
+def _ival(data, ew, i):
+    """element i of a flat int64 tensor of ew-word values, as a Python int (hi << 64 | lo)"""
+    if ew == 1:
+        return int(data[i]) & M64
+    return ((int(data[2 * i + 1]) & M64) << 64) | (int(data[2 * i]) & M64)
 
 
-def _np_count_tiles_layout(n, log_b, lay, blk0, tiles, out):
-    """The contract of sks_intersect_layout_tiles (packed, counts added), from a
-    layout whose block 0 is global block blk0 (decodes block k's sketches by id)."""
-    data, ids, boff, bstart = lay
-    B1 = (1 << log_b) + 1
-    d = data.numpy().view(np.uint64)
+class NpJoinOps:
+    """numpy restatement of the join layout's contract: per 64-sketch block, each
+    distinct value once with the mask of the block's sketches holding it, keyed
+    by (value group from the GIVEN bounds, hash bucket in the group).  count()
+    joins blocks bucket key by bucket key, so layouts built with different
+    bounds miss shared values and show up as count errors."""
 
-    def sketches_of(k):
-        kk = k - blk0
-        a = int(bstart[kk])
-        e = a + int(boff[kk * B1 + B1 - 1])
-        vals, sl = d[a:e], ids[a:e].numpy()
-        return [np.sort(vals[sl == i]) for i in range(64)]
-    for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
-        ri, cj = sketches_of(I), sketches_of(J)
-        for a in range(64):
-            for b in range(64):
-                i, j = I * 64 + a, J * 64 + b
-                if i < n and j < n:
-                    out[t, a, b] += np.intersect1d(ri[a], cj[b], assume_unique=True).size
+    def __init__(self, ew, rank):
+        self.ew, self.rank = ew, rank
+        self.built, self.calls = [], []
+
+    def bounds_like(self, log_b):
+        return torch.zeros((sks_dist_groups(log_b) + 1) * self.ew, dtype=torch.int64)
+
+    def bounds(self, src, log_b):
+        # rank 0's own quantile-ish bounds from its first sketch (rank-specific
+        # values: every layout must end up with exactly these)
+        assert self.rank == 0
+        G = sks_dist_groups(log_b)
+        vals = sorted(_ival(src.data, self.ew, i) for i in range(min(src.total, 500))) or [0]
+        b = [0] + [vals[(g * len(vals)) // G] + g for g in range(1, G)] + [(1 << (64 * self.ew)) - 1]
+        b = sorted(b)
+        out = []
+        for v in b:
+            out += [v & M64] if self.ew == 1 else [v & M64, v >> 64]
+        return torch.tensor(np.array(out, dtype=np.uint64).view(np.int64))
+
+    def build(self, src, log_b, gb, key):
+        G = sks_dist_groups(log_b)
+        bnd = [_ival(gb, self.ew, g) for g in range(G + 1)]
+        self.built.append((key, log_b, tuple(bnd)))
+        starts = src.starts.tolist()
+        sizes = src.sizes.tolist()
+        blocks = []
+        for b0 in range(0, src.n, 64):
+            ent = {}
+            for slot in range(min(64, src.n - b0)):
+                i = b0 + slot
+                for e in range(sizes[i]):
+                    v = _ival(src.data, self.ew, starts[i] + e)
+                    g = int(np.searchsorted(bnd[1:G], v, side="right")) if G > 1 else 0
+                    h = ((v & M64) * 0x9E3779B97F4A7C15 & M64) >> 61
+                    ent.setdefault((g, h), {}).setdefault(v, 0)
+                    ent[(g, h)][v] |= 1 << slot
+            blocks.append(ent)
+        return blocks
+
+    def count(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, out):
+        self.calls.append((r_blk0, c_blk0, len(tiles)))
+        for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
+            R, C = rows[I - r_blk0], cols[J - c_blk0]
+            for key, rv in R.items():
+                cv = C.get(key, {})
+                for v, rm in rv.items():
+                    cm = cv.get(v, 0)
+                    if not cm:
+                        continue
+                    for r in range(64):
+                        if rm >> r & 1:
+                            for c in range(64):
+                                if cm >> c & 1:
+                                    out[t, r, c] += 1
+
+    def ani_tiles(self, tiles, packed, sizes, n, k):
+        out = torch.zeros((len(tiles), 2, 64, 64), dtype=torch.float64)
+        for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
+            for r in range(64):
+                for c in range(64):
+                    i, j = I * 64 + r, J * 64 + c
+                    if i < n and j < n:
+                        x = int(packed[t, r, c])
+                        out[t, 0, r, c] = O.binomial_estimator(O.containment(x, int(sizes[i])), k)
+                        out[t, 1, c, r] = O.binomial_estimator(O.containment(x, int(sizes[j])), k)
+        return out
 
 
-def _join_worker(rank, world, port, q, dst, n_genomes):
+def sks_dist_groups(log_b):
+    """value groups of a layout with 2^log_b buckets (sks_join_layout_groups: 8 buckets a group)"""
+    return 1 << (log_b - 3) if log_b > 3 else 1
+
+
+def _join_worker(rank, world, port, q, dst, n_genomes, ew):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    sk = [s.astype(np.uint64) for s in (_sketches() if n_genomes == N_GENOMES else _sketches_200())]
+    sk = _join_sketches(n_genomes, ew)
     _, g0, g1 = sks_dist.block_shard(n_genomes, world, rank)
     mine = sk[g0:g1]
-    built, calls = [], []
-
-    def bounds(lb):  # rank 0's bounds are broadcast: rank-specific values show it
-        assert rank == 0
-        return torch.arange(sks_dist.layout_groups(lb) + 1, dtype=torch.int64) * 1000 + 7
-
-    def build(lb, pad, gb):
-        built.append((lb, pad))
-        assert torch.equal(gb, bounds.__wrapped__(lb)), gb  # every rank got rank 0's
-        d, i, b, s, _ = _np_layout(mine, lb)
-        if pad is None:
-            return d, i, b, s
-        cap_e, bpr = pad  # the padded send-buffer shape all_vs_all_join gathers
-        assert d.numel() <= cap_e and b.numel() <= bpr * ((1 << lb) + 1)
-        totals = [sum(len(x) for x in sk[sks_dist.block_shard(n_genomes, world, r)[1]:
-                                         sks_dist.block_shard(n_genomes, world, r)[2]]) for r in range(world)]
-        assert cap_e == max(max(totals), 1), (cap_e, totals)  # the largest rank's total, exactly
-        pd = torch.full((cap_e,), -7, dtype=torch.int64)
-        pi = torch.full((cap_e,), 99, dtype=torch.uint8)
-        pb = torch.full((bpr * ((1 << lb) + 1),), -3, dtype=torch.int32)
-        ps = torch.full((bpr + 1,), -5, dtype=torch.int64)  # junk past the own blocks
-        pd[:d.numel()], pi[:i.numel()], pb[:b.numel()], ps[:s.numel()] = d, i, b, s
-        return pd, pi, pb, ps
-
-    def count(n, lb, lay, blk0, tiles, out):
-        calls.append((blk0, len(tiles)))
-        _np_count_tiles_layout(n, lb, lay, blk0, tiles, out)
-    bounds.__wrapped__ = lambda lb: torch.arange(sks_dist.layout_groups(lb) + 1, dtype=torch.int64) * 1000 + 7
-    mat = sks_dist.all_vs_all_join(
-        n_genomes, world, rank, max((len(s) for s in mine), default=0), sum(len(s) for s in mine),
-        lambda m: 3, build, count, dst=dst, bounds=bounds)
-    q.put((rank, None if mat is None else mat.numpy(), built, calls))
+    flat = np.concatenate([x.reshape(-1) for x in mine] + [np.zeros(0, np.uint64)]).view(np.int64)
+    src = sks_dist.Sketches(torch.from_numpy(flat.copy()), torch.tensor([len(x) for x in mine], dtype=torch.int32),
+                            ew)
+    ops = NpJoinOps(ew, rank)
+    res = sks_dist.all_vs_all_join(n_genomes, world, rank, src, ops, lambda m: 5, dst=dst, ani_ones=21)
+    q.put((rank, None if res.matrix is None else res.matrix.numpy(), ops.built, ops.calls,
+           res.tiles, res.counts.numpy(), res.ani.numpy()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,dst,n_genomes", [(2, 0, N_GENOMES), (3, None, N_GENOMES), (2, 1, 200),
-                                                 (3, 0, 200)])
-def test_all_vs_all_join_layout_gather_gloo(world, dst, n_genomes):
-    """Ranks build layouts of their own block-aligned genomes into send buffers
-    padded to the largest rank's element total, count their own blocks' tiles
-    on their own layout (first call, blk0 = their first block) while the layouts
-    are gathered, then their share of the cross-rank tiles on the gathered
-    layout; the packed tiles go to dst (every rank for None), whose matrix equals
-    the single-process merge counts; the others return None.  n = 200 at world 3
-    leaves the last rank without genomes."""
+def _join_sketches(n_genomes, ew):
+    if ew == 1:
+        return [s.astype(np.uint64) for s in (_sketches() if n_genomes == N_GENOMES else _sketches_200())]
+    m = O.mask(40, 30, 0)
+    out = []
+    for g in range(n_genomes):
+        seq = synth.bases(2500, seed=60 + g % 3, mut_seed=700 + g, mut_rate=0.004 * (g % 6))
+        s, _ = O.sketch(O.cut_runs(seq.tobytes()), 40, m, "frac", 20)
+        out.append(s)  # (k, 2) uint64 (lo, hi)
+    return out
+
+
+@pytest.mark.parametrize("world,dst,n_genomes,ew", [(2, 0, N_GENOMES, 1), (3, "all", N_GENOMES, 1),
+                                                    (2, 1, 200, 1), (3, 0, 200, 1), (3, 0, 130, 2)])
+def test_all_vs_all_join_broadcasts_gloo(world, dst, n_genomes, ew):
+    """Ranks build the layout of their own block-aligned genomes with rank 0's
+    bounds, count their own blocks' tiles first, then — as each source rank's
+    broadcast sketches land — build that source's layout and count their share
+    of the tiles pairing the two (rows from the lower rank's blocks); the
+    packed tiles go to dst (every rank for "all"), whose matrix equals the
+    single-process merge counts; the per-tile ANI of both orientations equals
+    the reference formula.  n = 200 at world 3 leaves the last rank without
+    genomes; ew = 2 moves 128-bit (lo, hi) k-mers (w = 40)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes))
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes, ew))
              for r in range(world)]
     for p in procs:
         p.start()
-    results = {r: (m, b, c) for r, m, b, c in (q.get(timeout=300) for _ in range(world))}
+    results = {r[0]: r[1:] for r in (q.get(timeout=600) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    sk = _sketches() if n_genomes == N_GENOMES else _sketches_200()
-    want = np.array([[len(np.intersect1d(sk[i], sk[j])) for j in range(n_genomes)]
-                     for i in range(n_genomes)])
+    sk = _join_sketches(n_genomes, ew)
+    want = np.array([[O.intersect(_w(sk[i]), _w(sk[j])) for j in range(n_genomes)] for i in range(n_genomes)])
+    sizes = [len(x) for x in sk]
+    bnds = {b for r in range(world) for (_, _, b) in results[r][1]}
+    assert len(bnds) == 1  # every layout on every rank used rank 0's bounds
     for r in range(world):
-        mat, built, calls = results[r]
-        if dst is None or r == dst:
+        mat, built, calls, tiles, counts, ani = results[r]
+        if dst == "all" or r == dst:
             assert np.array_equal(mat, want), r
         else:
             assert mat is None
-        assert [lb for lb, _ in built] == [3]
-        loc, rem = sks_dist.tile_plan(n_genomes, world, r)
+        loc, rem = sks_dist.tile_plan_by_peer(n_genomes, world, r)
         _, g0, _ = sks_dist.block_shard(n_genomes, world, r)
-        expect = ([(g0 // 64, len(loc))] if len(loc) else []) + ([(0, len(rem))] if len(rem) else [])
-        assert calls == expect, (r, calls)
+        expect = [(g0 // 64, g0 // 64, len(loc))] if len(loc) else []
+        for qq in range(world):
+            if len(rem[qq]):
+                bq = sks_dist.block_shard(n_genomes, world, qq)[1] // 64
+                expect.append((g0 // 64, bq, len(rem[qq])) if r < qq else (bq, g0 // 64, len(rem[qq])))
+        assert calls == expect, (r, calls, expect)
+        for t, (I, J) in enumerate(tiles):
+            for a, b in ((0, 0), (3, 7), (63, 62)):
+                i, j = I * 64 + a, J * 64 + b
+                if i < n_genomes and j < n_genomes:
+                    assert counts[t, a, b] == want[i, j]
+                    assert ani[t, 0, a, b] == O.binomial_estimator(O.containment(int(want[i, j]), sizes[i]), 21)
+                    assert ani[t, 1, b, a] == O.binomial_estimator(O.containment(int(want[i, j]), sizes[j]), 21)
+
+
+def _w(x):
+    x = np.asarray(x, dtype=np.uint64)
+    return x if x.ndim == 2 else np.stack([x, 0 * x], 1)
 
 
 def test_block_shard_covers_whole_blocks():
@@ -441,6 +423,12 @@ def _sketches_200():
 
 @pytest.mark.parametrize("n,world", [(1000, 8), (1000, 3), (200, 3), (64, 2), (1, 4), (5000, 7)])
 def test_tile_plan_partitions_upper_triangle(n, world):
+    for r in range(world):  # remote tiles by peer: rows in the lower rank's blocks
+        _, rem = sks_dist.tile_plan_by_peer(n, world, r)
+        for q, tq in enumerate(rem):
+            lo, hi = sks_dist.block_shard(n, world, min(r, q)), sks_dist.block_shard(n, world, max(r, q))
+            for I, J in tq:
+                assert lo[1] // 64 <= I < (lo[2] + 63) // 64 and hi[1] // 64 <= J < (hi[2] + 63) // 64
     nb = (n + 63) // 64
     seen = {}
     sizes = []

@@ -1,0 +1,157 @@
+"""GPU parity of the deduplicated join layout (layout.hip) and the join kernel
+over it (join.hip): 128-bit k-mers (32 < w <= 64) through the tiled join, the
+layout build's slow path and slice splits (forced with a small
+SKS_LAYOUT_GROUP_CAP), and the instrumented check kernels at config-4 scale
+(kmer_set.cpp:23-41, 143-184: every count equals the reference's)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spaced-kmer-sketching_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import sksffi  # noqa: E402
+import pyoracle as O  # noqa: E402
+import synth  # noqa: E402
+from test_gpu_parity import build, _device_sketch_arrays, torch_cuda, ctx  # noqa: E402,F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _all_ways(torch, ctx, d, st, sz, ew, n, split=True):
+    """all-pairs via sks_intersect_all (whole and two row blocks, one unaligned)
+    and sks_intersect_sym split into two tile ranges (one range for the global
+    kernel, which takes no partial tile ranges)"""
+    out = torch.full((n * n,), -3, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_all(d, st, sz, ew, n, 0, n, out.data_ptr())
+    torch.cuda.synchronize()
+    res = [out.cpu().numpy().reshape(n, n)]
+    rows = []
+    for r0, r1 in ((0, 70), (70, n)):
+        o = torch.full(((r1 - r0) * n,), -5, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_all(d, st, sz, ew, n, r0, r1, o.data_ptr())
+        torch.cuda.synchronize()
+        rows.append(o.cpu().numpy().reshape(r1 - r0, n))
+    res.append(np.concatenate(rows))
+    T = sksffi.intersect_sym_tiles(n)
+    acc = np.zeros((n, n), dtype=np.int64)
+    for a, b in (((0, 2), (2, T)) if split else ((0, T),)):
+        o = torch.full((n * n,), 9, dtype=torch.int32, device="cuda:0")
+        ctx.intersect_sym(d, st, sz, ew, n, a, b, o.data_ptr())
+        torch.cuda.synchronize()
+        acc += o.cpu().numpy().reshape(n, n)
+    res.append(acc)
+    return res
+
+
+@pytest.mark.parametrize("w,k", [(45, 30), (33, 33), (64, 40)])
+def test_wide_join_matches_oracle(torch_cuda, ctx, w, k):
+    """130 genomes in 5 families at 32 < w <= 64: the 128-bit join (layout of
+    (lo, hi) entries, sym tiles and row blocks) equals the oracle's counts, as
+    does the one-wavefront-per-pair kernel."""
+    torch = torch_cuda
+    n = 130
+    genomes = [synth.bases(3000 + 53 * (i % 11), seed=40 + i % 5, mut_seed=300 + i,
+                           mut_rate=0.004 * (i % 6)).tobytes() if i % 29 else b"" for i in range(n)]
+    m = O.mask(w, k, 1)
+    ss, _ = build(torch, ctx, genomes, w, m, "frac", 4)
+    assert ss.elem_words == 2
+    sk = [O.sketch(O.cut_runs(g), w, m, "frac", 4)[0] for g in genomes]
+    want = np.array([[O.intersect(sk[i], sk[j]) for j in range(n)] for i in range(n)])
+    assert want[1, 6] > 0 and want[0].sum() == 0  # genome 0 is empty
+    d, st, sz = ss.device_ptrs()
+    for kind in (sksffi.INTERSECT_AUTO, sksffi.INTERSECT_GLOBAL):
+        ctx.set_intersect_kernel(kind)
+        try:
+            for got in _all_ways(torch, ctx, d, st, sz, 2, n, split=kind != sksffi.INTERSECT_GLOBAL):
+                assert np.array_equal(got, want), kind
+        finally:
+            ctx.set_intersect_kernel(sksffi.INTERSECT_AUTO)
+
+
+def _wide_arrays(rng, n, base_n, fams, extra):
+    """sorted unique (lo, hi) arrays [k, 2] (hi-major) of related families"""
+    out = []
+    base = []
+    for _ in range(fams):
+        v = rng.integers(0, 2**63, size=(base_n, 2), dtype=np.uint64)
+        base.append(v)
+    for i in range(n):
+        b = base[i % fams]
+        keep = b[rng.random(len(b)) < 0.3 + 0.6 * ((i * 7) % 10) / 10]
+        ex = rng.integers(0, 2**63, size=(extra, 2), dtype=np.uint64)
+        a = np.unique(np.concatenate([keep, ex]), axis=0)
+        a = a[np.lexsort((a[:, 0], a[:, 1]))]
+        out.append(a)
+    return out
+
+
+def _wide_count(a, b):
+    va = a.view([("lo", np.uint64), ("hi", np.uint64)]).reshape(-1)
+    vb = b.view([("lo", np.uint64), ("hi", np.uint64)]).reshape(-1)
+    return np.intersect1d(va, vb, assume_unique=True).size
+
+
+@pytest.mark.parametrize("gcap", [None, "64"])
+def test_wide_join_caller_arrays_and_slow_path(torch_cuda, ctx, monkeypatch, gcap):
+    """Caller-provided 128-bit arrays whose words differ in either half (so a
+    hi- or lo-only comparison would miscount), 150 sketches in 3 families, with
+    the layout's fast path and (group cap 64) its slow path for every group."""
+    torch = torch_cuda
+    if gcap:
+        monkeypatch.setenv("SKS_LAYOUT_GROUP_CAP", gcap)
+    rng = np.random.default_rng(5)
+    n = 150
+    sk = _wide_arrays(rng, n, 1500, 3, 200)
+    sk[7] = np.zeros((0, 2), np.uint64)
+    # values equal in lo but not hi (and the reverse) across sketches
+    sk[10] = np.concatenate([sk[10], np.array([[5, 2**63 + 1]], np.uint64)])
+    sk[11] = np.concatenate([sk[11], np.array([[5, 2**63 + 2]], np.uint64)])
+    for i in (10, 11):
+        sk[i] = sk[i][np.lexsort((sk[i][:, 0], sk[i][:, 1]))]
+    want = np.array([[_wide_count(sk[i], sk[j]) for j in range(n)] for i in range(n)])
+    sizes = np.array([len(x) for x in sk], dtype=np.uint32)
+    starts = np.zeros(n, dtype=np.uint64)
+    starts[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    flat = np.concatenate([x.reshape(-1) for x in sk] + [np.zeros(2, np.uint64)])
+    d = torch.from_numpy(flat.view(np.int64)).to("cuda:0")
+    st = torch.from_numpy(starts.view(np.int64)).to("cuda:0")
+    sz = torch.from_numpy(sizes.view(np.int32)).to("cuda:0")
+    for got in _all_ways(torch, ctx, d.data_ptr(), st.data_ptr(), sz.data_ptr(), 2, n):
+        assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("shape", ["identical", "families", "extremes"])
+def test_layout_slow_path_slice_splits(torch_cuda, ctx, monkeypatch, shape):
+    """Group cap 64: every layout group takes the slow path; identical sketches
+    put 64 copies of each value in a slice, so slices split down to single
+    values.  With the check kernels on, no invariant is violated and the counts
+    equal numpy's."""
+    torch = torch_cuda
+    monkeypatch.setenv("SKS_LAYOUT_GROUP_CAP", "64")
+    rng = np.random.default_rng({"identical": 1, "families": 2, "extremes": 3}[shape])
+    n = 140
+    if shape == "identical":
+        one = np.unique(rng.integers(0, 2**64 - 1, size=3000, dtype=np.uint64))
+        sk = [one.copy() for _ in range(n)]
+    elif shape == "families":
+        base = [np.unique(rng.integers(0, 2**62, size=3000, dtype=np.uint64)) for _ in range(3)]
+        sk = [np.unique(np.concatenate([base[i % 3][rng.random(base[i % 3].size) < 0.5],
+                                        rng.integers(0, 2**62, size=100, dtype=np.uint64)])) for i in range(n)]
+    else:
+        core = np.unique(np.concatenate([np.array([0, 1, 2**64 - 2, 2**64 - 1], np.uint64),
+                                         rng.integers(0, 2**64 - 1, size=2000, dtype=np.uint64)]))
+        sk = [core[rng.random(core.size) < 0.5] if i % 13 else np.zeros(0, np.uint64) for i in range(n)]
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)]
+                     for i in range(n)])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    ctx.set_join_check(True)
+    try:
+        for got in _all_ways(torch, ctx, d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n):
+            assert np.array_equal(got, want)
+        assert ctx.join_check_violations() == 0
+    finally:
+        ctx.set_join_check(False)

@@ -3,9 +3,11 @@
 The driver runs N > 1 (one process per GPU); a 1-GPU box cannot.  Here a
 process group of size 1 on the "nccl" backend (RCCL) is started, so
 sks_dist takes its collective path (`_solo` is False) and every exchange the
-N > 1 runs make — all_gather_into_tensor of int64 / uint8 / int32 join layouts,
-of padded sketches and chunk sketches, all_reduce of the count matrix, of the
-ANI sums and of scalars — runs through RCCL on device memory.  Each result is
+N > 1 runs make — the per-source broadcasts of int64 sketches and int32 sizes,
+the bounds broadcast, the metadata gather and the packed tile gather of
+all_vs_all_join, all_gather_into_tensor of padded sketches and chunk sketches,
+all_reduce of the count matrix, of the ANI sums and of scalars — runs through
+RCCL on device memory.  Each result is
 compared with the same computation without a process group, and with the
 oracle (oracle/sks_oracle.cpp) where that is cheap.  Reference semantics:
 kmer_set.cpp:23-41 (set intersection), kmer-sketching.cpp:185-200 (ANI).
@@ -68,48 +70,54 @@ def _merge_counts(sk):
                      for i in range(n)], dtype=np.int64)
 
 
-@pytest.mark.parametrize("side_stream", [False, True])
-def test_join_layout_all_vs_all_on_rccl(env, side_stream):
+@pytest.mark.parametrize("side_stream,w", [(False, W), (True, W), (False, 45)])
+def test_join_layout_all_vs_all_on_rccl(env, side_stream, w):
     """sks_dist.all_vs_all_join through the collective branch on RCCL: the
-    all_reduce MAX of (largest sketch, element total), the padded layout gathers
-    (int64 data, uint8 ids, int32 bucket starts, int64 block starts), queued on
-    the collective stream while the rank's own tiles are counted, the packed
-    tile gather to rank 0 (dist.gather) and the matrix assembly — 130 genomes
-    (3 blocks, a ragged last one, an empty sketch).  With side_stream the
-    context's kernels run on a non-default HIP stream: join_layout_fns orders it
-    against torch's stream both ways."""
+    metadata gather, rank 0's bounds broadcast, the per-source sketch / size
+    broadcasts (each joined as it lands), the packed tile gather to rank 0
+    (dist.gather), the matrix assembly and the per-tile device ANI — 130 genomes
+    (3 blocks, a ragged last one, an empty sketch), u64 and (w = 45) 128-bit
+    k-mers.  With side_stream the context's kernels run on a non-default HIP
+    stream: GpuJoinOps orders it against torch's stream both ways."""
     torch, dist, ctx = env
     import sks_dist
     n, s = 130, 600
     genomes = _family(n, 30_000, 9)
     genomes[40] = b""
     d, seg = _upload(torch, genomes)
-    mask = sksffi.mask_generate(W, K, 0)
-    ss = ctx.sketch_build(d.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, s)
+    k = K if w == W else 30
+    mask = sksffi.mask_generate(w, k, 0)
+    ss = ctx.sketch_build(d.data_ptr(), seg[-1], seg, w, mask, sksffi.SKS_BOTTOM_S, s)
     sizes = ss.sizes().copy()
-    sk = [ss.sketch(i)[:, 0].copy() for i in range(n)]
+    sk = [ss.sketch(i) for i in range(n)]
     for g in (0, 64, 129):
-        want, _ = O.sketch(O.cut_runs(genomes[g]), W, mask, "bottom", s)
+        want, _ = O.sketch(O.cut_runs(genomes[g]), w, mask, "bottom", s)
         assert np.array_equal(ss.sketch(g), want)
-    want = _merge_counts(sk)
+    want = np.array([[O.intersect(sk[i], sk[j]) for j in range(n)] for i in range(n)], dtype=np.int64)
     assert want[0, 9] > 0 and want[40].sum() == 0
     stream = torch.cuda.Stream() if side_stream else None
     cctx = sksffi.Context(0, stream.cuda_stream) if side_stream else ctx
-    build, count, bounds = sks_dist.join_layout_fns(cctx, ss, sizes, device="cuda")
-    out = torch.full((n, n), -5, dtype=torch.int32, device="cuda")
-    mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), int(sizes.astype(np.int64).sum()),
-                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out,
-                                   bounds=bounds)
+    ops = sks_dist.GpuJoinOps(cctx, ss.elem_words)
+    res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
+                                   device="cuda", dst=0, ani_ones=k)
     torch.cuda.synchronize()
-    assert np.array_equal(mat.cpu().numpy().astype(np.int64), want), side_stream
+    assert np.array_equal(res.matrix.cpu().numpy().astype(np.int64), want), side_stream
+    # per-tile ANI (both orientations) against the host formula on the oracle counts
+    ani = res.ani.cpu().numpy()
+    for t, (I, J) in enumerate(res.tiles):
+        for r, c in ((0, 0), (5, 9), (63, 1)):
+            i, j = I * 64 + r, J * 64 + c
+            if i < n and j < n:
+                for a, b, got in ((i, j, ani[t, 0, r, c]), (j, i, ani[t, 1, c, r])):
+                    want_ani = sksffi.binomial_estimator(sksffi.containment(int(want[a, b]), int(sizes[a])), k)
+                    assert abs(got - want_ani) <= 1e-9, (a, b)
     if side_stream:
         cctx.close()
 
 
-def test_padded_sketch_all_vs_all_and_rows_on_rccl(env):
+def test_padded_sketch_all_vs_all_on_rccl(env):
     """sks_dist.all_vs_all (padded int64 sketches + int32 sizes gathered, symmetric
-    tiles, count all_reduce) and all_vs_all_rows at w = 45 ((lo, hi) pairs, row
-    blocks gathered as flat int32), both equal to the oracle's merge counts."""
+    tiles, count all_reduce), equal to the oracle's merge counts."""
     torch, dist, ctx = env
     import sks_dist
     n, s = 70, 400
@@ -129,26 +137,6 @@ def test_padded_sketch_all_vs_all_and_rows_on_rccl(env):
 
     got = sks_dist.all_vs_all(padded, psz, n, 1, 0, count_sym).cpu().numpy()
     assert np.array_equal(got.astype(np.int64), _merge_counts([ss.sketch(i)[:, 0] for i in range(n)]))
-
-    w, k, c = 45, 30, 15
-    m = O.mask(w, k, 2)
-    ssw = ctx.sketch_build(d.data_ptr(), seg[-1], seg, w, m, sksffi.SKS_FRAC_MOD, c)
-    skw = [O.sketch(O.cut_runs(g), w, m, "frac", c)[0] for g in genomes]
-    stride = max(len(x) for x in skw) + 1
-    pw = torch.full((n, 2 * stride), -1, dtype=torch.int64, device="cuda")
-    pwsz = torch.zeros(n, dtype=torch.int32, device="cuda")
-    ssw.export(pw.data_ptr(), stride, pwsz.data_ptr())
-    st2 = torch.arange(n, dtype=torch.int64, device="cuda") * stride
-
-    def count_rows(src, sizes, nn, r0, r1, out):
-        ctx.intersect_all(src.data_ptr(), st2.data_ptr(), sizes.data_ptr(), 2, nn, r0, r1,
-                          out.data_ptr())
-        torch.cuda.synchronize()
-
-    got = sks_dist.all_vs_all_rows(pw, pwsz, n, 1, 0, count_rows).cpu().numpy()
-    want = np.array([[O.intersect(skw[i], skw[j]) for j in range(n)] for i in range(n)])
-    assert want[0, 5] > 0
-    assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("w,k", [(W, K), (45, 30)])

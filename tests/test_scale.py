@@ -86,12 +86,11 @@ def test_config4_all_vs_all_1000x5mb(env):
         want, nw = O.sketch(O.cut_runs(raw), bench.W, mask, "bottom", s)
         assert np.array_equal(ss.sketch(g), want), g
         assert int(ss.windows()[g]) == nw
-    # the bench's pair path, world 1
-    build, count, bounds = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda")
-    out = torch.full((n, n), -1, dtype=torch.int32, device="cuda")
-    mat = sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), int(sizes.astype(np.int64).sum()),
-                                   sksffi.join_layout_log_b, build, count, device="cuda", out=out,
-                                   bounds=bounds)
+    # the bench's pair path, world 1: counts and device ANI
+    ones = bin(mask).count("1") // 2
+    res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), sks_dist.GpuJoinOps(ctx),
+                                   sksffi.join_layout_log_b, device="cuda", ani_ones=ones)
+    mat = res.matrix
     torch.cuda.synchronize()
     got = mat.cpu().numpy().astype(np.int64)
     want = _host_counts(_exported(ss, n))
@@ -100,6 +99,13 @@ def test_config4_all_vs_all_1000x5mb(env):
     assert np.array_equal(got, want)
     # the family structure is real: related pairs share k-mers, unrelated ones do not
     assert got[0, 1] > 0 and got[0, 50] > 0 and got[0, 999] < 50
+    # device ANI of all 10^6 ordered pairs against the host's sks_ani_from_counts
+    # (kmer-sketching.cpp:195-200, ani_estimation.cpp:24-42): within 1e-9
+    size_first = np.repeat(np.diag(got).astype(np.int32), n)
+    _, host_ani = sksffi.ani_from_counts(got.reshape(-1), size_first, ones)
+    dev_ani = res.ani.cpu().numpy().reshape(-1)
+    assert np.abs(dev_ani - host_ani).max() <= 1e-9
+    assert (dev_ani == host_ani).mean() > 0.99  # the device pow is within 1 ulp; nearly all bit-equal
 
 
 def test_config5_seed_sweep_8x200x5mb(env):

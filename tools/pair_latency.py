@@ -31,18 +31,14 @@ def main():
     buf[torch.tensor(seg[1:], device="cuda") - 1] = ord("\n")
     mask = sksffi.mask_generate(31, 21, 0)
     ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, 31, mask, sksffi.SKS_BOTTOM_S, bench.C4_S)
-    sizes = ss.sizes().copy()
-    mat = torch.empty((n, n), dtype=torch.int32, device="cuda")
-    cache = {}
+    ops = sks_dist.GpuJoinOps(ctx)
     issue, wall, first = [], [], []
     for it in range(steps + 2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        build, count, bounds = sks_dist.join_layout_fns(ctx, ss, sizes, device="cuda", cache=cache)
+        src = sks_dist.sketches_of(ss)
         t_f = time.perf_counter()
-        sks_dist.all_vs_all_join(n, 1, 0, int(sizes.max()), int(sizes.astype(np.int64).sum()),
-                                 sksffi.join_layout_log_b, build, count, device="cuda", out=mat, dst=0,
-                                 bounds=bounds)
+        sks_dist.all_vs_all_join(n, 1, 0, src, ops, sksffi.join_layout_log_b, device="cuda", dst=None)
         t1 = time.perf_counter()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
@@ -50,7 +46,7 @@ def main():
             first.append(t_f - t0)
             issue.append(t1 - t0)
             wall.append(t2 - t0)
-    print(f"fns {np.median(first) * 1e3:.3f} ms  issue {np.median(issue) * 1e3:.3f} ms  "
+    print(f"views {np.median(first) * 1e3:.3f} ms  issue {np.median(issue) * 1e3:.3f} ms  "
           f"wall {np.median(wall) * 1e3:.3f} ms  k_join {ctx.last_intersect_ms():.3f} ms", flush=True)
 
 
