@@ -53,6 +53,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 W, K, MASK_SEED = 31, 21, 0
 C3_CONTIGS, C3_CONTIG_LEN, C3_NRUN, C3_NRUN_LEN, C3_FRAC = 24, 125_000_000, 4, 10_000, 1000
 C4_GENOMES, C4_LEN, C4_ANCESTORS, C4_S = 1000, 5_000_000, 10, 10000
+C4W_W, C4W_K = 45, 30  # config 4 at a 128-bit (k+10, k) shape of the reference sweep
 C5_GENOMES, C5_SEEDS = 200, 8  # first 200 genomes of config 4, mask seeds 0..7
 
 
@@ -702,12 +703,15 @@ def cpu_baseline_c4_sketch(ctx, buf, seg, mask):
             "host": host_info(T)}
 
 
-def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
+def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
     """Config 4 all-vs-all.  Timed per step: the sketch phase (every rank's
     genomes), then the pair phase = counts for every ordered pair + containment
     and ANI on the device + the ANI copied into pinned host memory (the whole
     "comparison" of kmer-sketching.cpp:185-203).  A second pass times the counts
-    alone (layout + join, no ANI) for the fixed-cost figure."""
+    alone (layout + join, no ANI) for the fixed-cost figure.  w > 32 (the
+    reference sweep's (k+10, k) shapes, kmer-sketching.cpp:228-239) runs the
+    same flow on 128-bit k-mers: 16-byte values in the sketches, the layout
+    and the join (elem_words 2)."""
     import sks_dist
     _, g0, g1 = sks_dist.block_shard(C4_GENOMES, world, rank)
     n_local = g1 - g0
@@ -721,12 +725,12 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         buf[seg[i] + C4_LEN] = ord("\n")
     torch.cuda.synchronize()
     ones = bin(mask).count("1") // 2
-    ops = sks_dist.GpuJoinOps(ctx)
+    ops = sks_dist.GpuJoinOps(ctx, ew=2 if w > 32 else 1)
     host_ani = None  # pinned, sized on the first step
 
     def pair_step(ss, with_ani=True):
         nonlocal host_ani
-        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss), ops,
+        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss, ew=ops.ew), ops,
                                        sksffi.join_layout_log_b, device="cuda", dst=None,
                                        ani_ones=ones if with_ani else None)
         if with_ani:
@@ -738,6 +742,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
 
     t_sketch = t_pairs = t_counts = 0.0
     timed = 0
+    k_all = []
     res = ss = None
     sizes = np.zeros(0, np.uint32)
     for it in range(warmup + steps):
@@ -746,7 +751,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         t0 = time.perf_counter()
         ss = None
         if n_local:
-            ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, W, mask, sksffi.SKS_BOTTOM_S, C4_S)
+            ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, w, mask, sksffi.SKS_BOTTOM_S, C4_S)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         res = pair_step(ss)
@@ -757,7 +762,8 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
             t_sketch += ts
             t_pairs += tp
             timed += 1
-    k_ms = ctx.last_intersect_ms()  # the rank's last join launch (all tiles at N = 1)
+            k_all.append(ctx.last_intersect_ms())  # the rank's last join launch (all tiles at N = 1)
+    k_ms = float(np.mean(k_all)) if k_all else None
     sizes = ss.sizes().copy() if ss is not None else sizes
     # counts alone (the fixed-cost figure: pair phase minus the join kernel)
     for it in range(1 + steps):
@@ -794,7 +800,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         tot = float(a[:, 0].sum()) + float(a[tl[:, 0] != tl[:, 1], 1].sum())
         ani_mean = sum_over_ranks(tot, world) / (C4_GENOMES * C4_GENOMES)
     cpu = cpu_sk = None
-    if cpu_pairs and rank == 0 and world == 1:
+    if cpu_pairs and rank == 0 and world == 1 and w == W:
         cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
         cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask)
     ani_bytes = (C4_GENOMES * C4_GENOMES * 8) if world == 1 else int(res.ani.numel()) * 8
@@ -804,6 +810,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
         "ms_pair_phase": t_pairs * 1e3, "ms_sketch_phase": t_sketch * 1e3,
         "ms_counts_phase": t_counts * 1e3,
         "pair_kernel_ms_rank0": k_ms,
+        "pair_kernel_timing": "hipEvents around the k_join launch on the context stream, mean over the timed steps",
         "fixed_cost_ms": (t_counts * 1e3 - k_ms) if k_ms else None,
         "ani_readback_bytes_rank0": ani_bytes,
         "ani_max_abs_err_vs_host": ani_err,
@@ -816,10 +823,12 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False):
             "pairs_this_rank": C4_GENOMES * C4_GENOMES / world,
             "achieved_GBps": (8 * 2 * C4_S + 4) * C4_GENOMES * C4_GENOMES / world / (k_ms * 1e-3) / 1e9
             if k_ms else None},
-        "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - W + 1) / t_sketch,
+        "roofline": pairs_lds_roofline(k_ms) if world == 1 and w == W else None,
+        "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - w + 1) / t_sketch,
         "ani_mean_all_pairs": ani_mean,
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
-                   "genome_len": C4_LEN, "s": C4_S, "w": W, "k": K,
+                   "genome_len": C4_LEN, "s": C4_S, "w": w, "k": ones,
+                   "kmer_bits": 128 if w > 32 else 64,
                    "pair_sharding": "block-aligned genomes per rank; tile plan: the rank's own "
                                     "blocks' 64x64 join tiles, then half of every cross-rank block "
                                     "pair as the peer's sketches land",
@@ -970,6 +979,80 @@ def run_seed_sweep(ctx, world, rank, steps, warmup, lanes_n=2, cpu=False):
     }
 
 
+# LDS: the fastest random-address rate of profiles/r01/lds_atomics_microbench.txt
+# (ds_add_u32 random, 9.73 lane-ops/clk/CU at 2.4 GHz = 0.152 wave-instructions
+# per clock per CU); ds_cmpst_rtn_b32 (the join's insert) runs 5.66, ds_read_b64
+# 9.39.  k_join's mix is reads, compare-swaps and XOR atomics, so this peak is
+# an upper bound of what its LDS instructions could reach.
+LDS_PEAK_WAVE_INST_PER_CLK_CU = 9.73 / 64
+CUS, PEAK_CLK_GHZ, SIMDS = 256, 2.4, 1024
+
+
+def latest_profile_json(name):
+    """profiles/rNN/<name> of the newest round that has one."""
+    import glob
+    import re
+    found = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r*", name)):
+        m = re.search(r"[/\\]r(\d+)[/\\]" + re.escape(name) + "$", f)
+        if m:
+            found.append((int(m.group(1)), f))
+    return max(found)[1] if found else ""
+
+
+def scan_valu_roofline(kernel_ms):
+    """The scan's VALU issue bound (the bound it is on): counted
+    VALU wave-instructions per launch (PMC, profiles/rNN/scan_valu.json) over
+    the live kernel time, against 1024 SIMDs issuing the hot block's mix at the
+    measured per-instruction rates (tools/valu_mix.py).  Null when the profile
+    was measured on other scan sources."""
+    import srchash
+    path = latest_profile_json("scan_valu.json")
+    if not path:
+        return {"note": "no profiles/rNN/scan_valu.json"}
+    t = json.load(open(path))
+    src = os.path.relpath(path, ROOT)
+    if t.get("scan_source_hash") != srchash.scan_hash() or not t.get("sq_insts_valu_per_launch"):
+        return {"note": f"stale: {src} measured on scan sources {t.get('scan_source_hash')}, "
+                        f"these are {srchash.scan_hash()}", "source": src}
+    insts = t["sq_insts_valu_per_launch"]
+    achieved = insts / (kernel_ms * 1e-3)
+    peak = SIMDS / (t["mean_ns_per_valu_per_simd"] * 1e-9)
+    return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "VALU wave-instructions/s",
+            "frac": achieved / peak, "valu_per_window": t["valu_per_window"],
+            "hot_block_valu": t["hot_block_valu"], "mean_cycles_per_valu": t["mean_cycles_per_valu"],
+            "source": src,
+            "note": "SQ_INSTS_VALU per launch (PMC) / live kernel time, against 1024 SIMDs at the hot "
+                    "block's cycle-weighted mix (profiles/r01/isa_rates_microbench.txt)"}
+
+
+def pairs_lds_roofline(kernel_ms):
+    """k_join's LDS bound: LDS wave-instructions per all-pairs call (PMC,
+    profiles/rNN/pair_lds.json) over the live kernel time, against 256 CUs x
+    2.4 GHz x the microbench's fastest random LDS rate.  Null when the profile
+    was measured on other join sources."""
+    import srchash
+    path = latest_profile_json("pair_lds.json")
+    if not path or not kernel_ms:
+        return {"note": "no profiles/rNN/pair_lds.json"}
+    t = json.load(open(path))
+    src = os.path.relpath(path, ROOT)
+    if t.get("join_source_hash") != srchash.join_hash() or not t.get("sq_insts_lds_per_call"):
+        return {"note": f"stale: {src} measured on join sources {t.get('join_source_hash')}, "
+                        f"these are {srchash.join_hash()}", "source": src}
+    insts = t["sq_insts_lds_per_call"]
+    achieved = insts / (kernel_ms * 1e-3)
+    peak = CUS * PEAK_CLK_GHZ * 1e9 * LDS_PEAK_WAVE_INST_PER_CLK_CU
+    conf = t.get("sq_lds_bank_conflict_per_call")
+    act = t.get("sq_lds_idx_active_per_call")
+    return {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "LDS wave-instructions/s",
+            "frac": achieved / peak, "lds_insts_per_call": insts,
+            "bank_conflict_frac_of_lds_active": (conf / act) if conf and act else None,
+            "source": src,
+            "peak_note": "256 CUs x 2.4 GHz x 0.152 wave-instructions/clk/CU (ds_add_u32 random, "
+                         "profiles/r01/lds_atomics_microbench.txt; ds_cmpst_rtn_b32 0.088)"}
+
+
 def latest_traffic_json():
     """profiles/rNN/traffic.json of the newest round that has one: written by
     tools/profile_round.sh from rocprofv3 PMC passes over this same bench command
@@ -1010,6 +1093,7 @@ def main():
     ap.add_argument("--cpu-crosscheck-mb", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pairs", action="store_true")
+    ap.add_argument("--no-pairs-wide", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-c3-sharded", action="store_true")
@@ -1086,6 +1170,11 @@ def main():
         pairs = run_pairs(ctx, world, rank, mask, steps=max(1, min(args.steps, 10)),
                           warmup=1, cpu_pairs=not args.no_cpu_baseline)
 
+    pairs_wide = None
+    if not args.no_pairs and not args.no_pairs_wide:
+        pairs_wide = run_pairs(ctx, world, rank, sksffi.mask_generate(C4W_W, C4W_K, MASK_SEED),
+                               steps=max(1, min(args.steps, 10)), warmup=1, w=C4W_W)
+
     c3s = None
     if not args.no_c3_sharded:
         c3s = run_c3_sharded(ctx, world, rank, mask, buf, steps=3, warmup=1)
@@ -1125,12 +1214,14 @@ def main():
                          "kernel_ms_median": float(np.median(scan_ms)),
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "traffic_source": traffic_src, "traffic_note": traffic_note,
+                         "valu": scan_valu_roofline(scan_avg_ms),
                          "timing": "hipEvents around each scan launch of the serial pass "
                                    "(the --steps builds after --warmup)"},
             "cpu_baseline": cpu,
             "cpu_crosscheck": cpu_x,
             "config2": c2,
             "pairs": pairs,
+            "pairs_wide": pairs_wide,
             "seed_sweep": sweep,
             "end_to_end": e2e,
             "c3_one_genome_sharded": c3s,

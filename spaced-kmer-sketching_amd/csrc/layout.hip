@@ -56,7 +56,6 @@ using jc::kv_store;
 constexpr int kTile = 64;
 constexpr int kPT = 256;                 // threads of the layout kernels
 constexpr uint32_t kGCap = 2048;         // elements of one dedup batch (a group)
-constexpr int kPer = kGCap / kPT;        // elements per thread
 constexpr int kTabLog = 12;              // dedup table: 4096 slots (load <= 1/2)
 constexpr uint32_t kTab = 1u << kTabLog;
 constexpr uint32_t kIdxBits = 11;        // slot word: tag21 << 11 | element index
@@ -95,25 +94,22 @@ __device__ __forceinline__ KV key_at(const uint64_t* s_key, uint32_t i) {
 }
 
 // Inserts element i (value v) into the dedup table; returns the index of the
-// element that represents v (i itself when v was new: *claimed = its slot).
-// The table is cut into one region of kTab >> rb slots per hash bucket of the
-// group (rb = the bucket bits) and a value probes only its bucket's region, so
-// reading the table in slot order lists the distinct values bucket by bucket.
-// More distinct values than a region holds (never at the group sizes the
-// bucket count is chosen for) set *full: the caller redoes the group on the
-// slow path.  The probe loop has ONE exit edge and evaluates its stop test
-// without short-circuit (the element a slot word names is read whether or not
-// the tag matches; a free word names element 2047, read and ignored): the
-// two-exit form of this loop (free slot / same value, the entry assigned at
-// each exit) was miscompiled by ROCm 7.2 for gfx950 in round 3 (DESIGN.md §5;
-// reproducer in tools/microbench/chain_exits.hip).
+// element that represents v (i itself when v was new).  The table is cut into
+// regions, one per hash bucket of the pass (base = the bucket's region, rmask =
+// its size - 1), and a value probes only its bucket's region, so reading the
+// table in slot order lists the distinct values bucket by bucket.  More
+// distinct values than a region holds set *full (the caller redoes the group
+// with one bucket per pass and the whole table).  The probe loop has ONE exit
+// edge and evaluates its stop test without short-circuit (the element a slot
+// word names is read whether or not the tag matches; a free word names element
+// 2047, read and ignored): the two-exit form of this loop (free slot / same
+// value, the entry assigned at each exit) was miscompiled by ROCm 7.2 for
+// gfx950 in round 3 (reproducer in tools/microbench/chain_exits.hip).
 template <int EW>
 __device__ __forceinline__ uint32_t dd_insert(uint32_t* s_tab, const uint64_t* s_key, const KV& v, uint32_t i,
-                                              uint32_t rb, uint32_t* claimed, bool* full) {
+                                              uint32_t base, uint32_t rmask, bool* full) {
   const uint32_t tag = dd_tag<EW>(v);
   const uint32_t word = (tag << kIdxBits) | i;
-  const uint32_t rlog = kTabLog - rb, rmask = (1u << rlog) - 1;
-  const uint32_t base = rb ? (uint32_t)(kv_mix<EW>(v) >> (64 - rb)) << rlog : 0u;
   uint32_t h = dd_slot<EW>(v) & rmask, steps = 0;
   uint32_t x = atomicCAS(&s_tab[base + h], kTFree, word);
   for (;;) {
@@ -123,7 +119,6 @@ __device__ __forceinline__ uint32_t dd_insert(uint32_t* s_tab, const uint64_t* s
     ++steps;
     x = atomicCAS(&s_tab[base + h], kTFree, word);
   }
-  *claimed = base + h;
   if (steps > rmask) *full = true;
   return x == kTFree ? i : (x & kIdxMask);
 }
@@ -219,12 +214,9 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
                                                 const uint64_t* __restrict__ starts,
                                                 const uint32_t* __restrict__ sizes, uint32_t count,
                                                 uint32_t G, const uint64_t* __restrict__ bounds,
-                                                uint32_t* __restrict__ pos, uint32_t* __restrict__ zero_words,
-                                                uint32_t n_zero) {
+                                                uint32_t* __restrict__ pos) {
   __shared__ uint64_t s_smp[kPosSamples * EW];
   const uint32_t i = blockIdx.x;
-  // the placement's tickets and look-back words start at zero (grid-strided)
-  for (uint32_t z = i * kPT + threadIdx.x; z < n_zero; z += gridDim.x * kPT) zero_words[z] = 0;
   const uint32_t sz = sizes[i];
   const uint64_t st = starts[i];
   uint32_t stride = kPosStride;
@@ -256,30 +248,6 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
 
 __device__ unsigned long long g_layout_check;  // SKS check build: dedup invariant violations
 
-// One workgroup per (block, value group).  A region's groups write one
-// contiguous run of entries, so each workgroup needs the distinct counts of
-// the region's earlier groups: it takes a ticket (its order in the region,
-// which is also the group it handles — HIP promises no dispatch order, and a
-// workgroup only ever waits for workgroups that took earlier tickets, so all
-// of them are running), deduplicates its group, publishes the group's count
-// and looks back over its predecessors' published counts (decoupled
-// look-back; an 8-byte {flag, value} word per group, agent-scope atomics on
-// both sides).  Phases of the normal path (a group of <= gcap elements):
-//   P1  its elements (read into registers) go to s_key, masks cleared
-//   P2  every element is inserted into the dedup table; the representative of
-//       its value (the element that claimed a slot) collects the holders' bits
-//       in s_msk; representatives are counted per (bucket, lane & 15)
-//   P3  wave 0 scans the counts (cursors); the group's count is published and
-//       the region prefix looked up
-//   P4  bucket starts -> boff; representatives take a cursor and write
-//       {value, mask} at region start + prefix + cursor
-// A group above gcap elements (skewed values) takes the slow path: the prefix
-// first, then hash slices of the group, each gathered from the sketches,
-// deduplicated and written in slice order (a slice that still holds more than
-// gcap elements is split in two); exact for any input, reading the group once
-// per slice.
-constexpr uint64_t kStAgg = 1ull << 62, kStInc = 1ull << 63;
-
 #ifdef SKS_LAYOUT_STAMPS  // diagnostic build: cycles per k_gl_place phase (thread 0 of each workgroup)
 __device__ unsigned long long g_layout_stamps[10];
 #define LSTAMP(i)                                              \
@@ -294,310 +262,581 @@ __device__ unsigned long long g_layout_stamps[10];
 #define LSTAMP(i) do {} while (0)
 #endif
 
-__device__ __forceinline__ void status_publish(unsigned long long* st, uint64_t v) {
-  __hip_atomic_store(st, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef SKS_PLACE_DIAG
+#define SKS_PLACE_DIAG 0
+#endif
+constexpr int kPB = 256;                     // threads of the placement kernel
+constexpr int kRegPer = kGCap / kPB;         // group elements per thread held in registers (8)
+constexpr int kSlowPer = kGCap / kPB;        // slice path: slice elements per thread
+constexpr uint32_t kSpt = kTab / kPB;        // table slots per thread in the emit scan (16)
+constexpr uint32_t kMaxRG = 1u << jc::kRGLog;
+constexpr int kPassU = 4;                    // bucket passes: 64-element chunks loaded per round
+static_assert(kSpt % 4 == 0, "emit reads the slots as uint4");
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l);
+  return ((uint64_t)hi << 32) | lo;
 }
 
-// sum of the distinct counts of groups [0, j) of the region (thread 0 only)
-__device__ __forceinline__ uint32_t region_prefix(unsigned long long* st, uint32_t j) {
-  uint32_t prefix = 0;
-  for (int p = (int)j - 1; p >= 0; --p) {
-    unsigned long long v;
-    while (((v = __hip_atomic_load(st + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0)
-      __builtin_amdgcn_s_sleep(1);
-    prefix += (uint32_t)v;
-    if (v & kStInc) break;
+// A value group's raw elements, sketch by sketch: lane s of a wave holds
+// sketch s's count gc, the inclusive prefix gend (sketch s holds elements
+// [gend - gc, gend) of the group) and src (element i of sketch s is
+// data[src + i]); gn = the group's element count.
+struct GroupMap {
+  uint32_t gc, gend, gn;
+  uint64_t src;
+};
+__device__ __forceinline__ GroupMap group_map(const uint32_t* p0, const uint32_t* p1, bool sv, uint64_t stt,
+                                              int lane) {
+  GroupMap m;
+  const uint32_t glo = sv ? p0[lane] : 0;
+  const uint32_t ghi = sv ? max(p1[lane], glo) : 0;
+  m.gc = ghi - glo;
+  m.gend = wave_scan(m.gc);
+  m.gn = (uint32_t)__builtin_amdgcn_readlane((int)m.gend, 63);
+  m.src = stt + glo - (m.gend - m.gc);
+  return m;
+}
+
+// Where element b + lane of the group lives (b wave-uniform, b < gn): the lane
+// walks, wave-uniformly, the few sketches whose ranges meet [b, b + 64)
+// (readlanes, no LDS).  *own = its sketch slot; returns the element's index in
+// `data` (meaningless for b + lane >= gn).
+__device__ __forceinline__ uint64_t elem_at(const GroupMap& m, uint32_t b, int lane, uint32_t* own) {
+  const uint32_t i = b + (uint32_t)lane, lim = min(b + 64, m.gn);
+  uint32_t s = (uint32_t)__popcll(__ballot(m.gend <= b));  // first sketch ending after b
+  uint32_t o = 0;
+  uint64_t at = 0;
+  for (; s < 64; ++s) {
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)m.gend, (int)s);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)m.gc, (int)s);
+    if (e - c >= lim) break;
+    const uint64_t a = readlane64(m.src, s);
+    const bool mine = (i >= e - c) & (i < e);
+    o = mine ? s : o;
+    at = mine ? a : at;
   }
-  return prefix;
+  *own = o;
+  return at + i;
 }
 
+// The owner map of a value group of at most kGCap elements (for the loads of
+// group_load): s_own[i] = the sketch slot of element i, s_src[s] = sketch s's
+// source offset (element i of sketch s is data[s_src[s] + i]).  Wave w writes
+// the ranges of sketches w, w + 4, ..., a lane per element.  Returns gn (above
+// kGCap nothing is written: such a group takes the bucket passes).
+__device__ __forceinline__ uint32_t group_map_write(const uint32_t* p0, const uint32_t* p1, bool sv, uint64_t stt,
+                                                    int lane, int wave, uint8_t* s_own, uint64_t* s_src) {
+  const GroupMap m = group_map(p0, p1, sv, stt, lane);
+  if (m.gn <= kGCap) {
+    if (wave == 0) s_src[lane] = m.src;
+    for (uint32_t s = (uint32_t)wave; s < 64; s += kPB / 64) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)m.gc, (int)s);
+      const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)m.gend, (int)s) - c;
+      for (uint32_t e = (uint32_t)lane; e < c; e += 64) s_own[e0 + e] = (uint8_t)s;
+    }
+  }
+  return m.gn;
+}
+
+// Loads the group's elements i = tid + k * kPB < gn into registers through
+// its owner map (written by group_map_write, a barrier passed since).
+template <int EW>
+__device__ __forceinline__ void group_load(const uint64_t* __restrict__ data, const uint8_t* s_own,
+                                           const uint64_t* s_src, uint32_t gn, int tid, KV (&v)[kRegPer],
+                                           uint32_t (&sl)[kRegPer]) {
+#pragma unroll
+  for (int k = 0; k < kRegPer; ++k) {
+    const uint32_t i = tid + k * kPB;
+    v[k] = KV{0, 0};
+    sl[k] = 0;
+    if (gn <= kGCap && i < gn) {
+      const uint32_t s = s_own[i];
+      sl[k] = s;
+#if SKS_PLACE_DIAG == 3  // diagnostics: no global loads (values synthesised from the index)
+      v[k] = KV{(s_src[s] + i) * 0x9E3779B97F4A7C15ull, 0};
+#else
+      v[k] = kv_load<EW>(data, s_src[s] + i);
+#endif
+    }
+  }
+}
+
+// Emits one dedup pass: the table in slot order lists the pass's distinct
+// values bucket by bucket (region q of 4096 >> pl slots = bucket b0 + q).
+// Thread t reads slots [kSpt t, kSpt t + kSpt) (and frees them), a block scan
+// of the occupied counts gives every entry its place at the cursor; the
+// entries {value, mask} are written and the masks cleared for the next pass.
+// Two barriers.
+template <int EW>
+__device__ __forceinline__ void emit_pass(uint32_t* s_tab, const uint64_t* s_key, unsigned long long* s_msk,
+                                          uint32_t* s_wsum, uint32_t* boff_b0, uint32_t nb, uint32_t pl,
+                                          uint64_t base, uint64_t* __restrict__ out_vals,
+                                          unsigned long long* __restrict__ out_masks, uint32_t& cur, uint32_t& maxb,
+                                          int tid, int lane, int wave) {
+  uint32_t wv[kSpt];
+#pragma unroll
+  for (int q = 0; q < (int)kSpt / 4; ++q) {
+    uint4* p = reinterpret_cast<uint4*>(s_tab) + tid * (kSpt / 4) + q;
+    const uint4 x = *p;
+    *p = make_uint4(kTFree, kTFree, kTFree, kTFree);
+    wv[4 * q] = x.x;
+    wv[4 * q + 1] = x.y;
+    wv[4 * q + 2] = x.z;
+    wv[4 * q + 3] = x.w;
+  }
+  uint32_t occ = 0;
+#pragma unroll
+  for (int q = 0; q < (int)kSpt; ++q) occ += wv[q] != kTFree;
+  const uint32_t wincl = wave_scan(occ);
+  if (lane == 63) s_wsum[wave] = wincl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kPB / 64; ++w) {
+    const uint32_t x = s_wsum[w];
+    before += w < wave ? x : 0;
+    total += x;
+  }
+  const uint32_t excl = before + wincl - occ;
+  const uint32_t tpb = (uint32_t)kPB >> pl;  // threads per bucket region
+  const uint32_t q = (uint32_t)tid / tpb;
+  if ((uint32_t)tid % tpb == 0 && q < nb) boff_b0[q] = cur + excl;
+  // the pass's entries in slot order: element indices listed in the (freed)
+  // table, then written with coalesced stores and the table freed again
+  uint32_t d = excl;
+#pragma unroll
+  for (int k = 0; k < (int)kSpt; ++k)
+    if (wv[k] != kTFree) s_tab[d++] = wv[k] & kIdxMask;
+  __syncthreads();
+  for (uint32_t e = tid; e < total; e += kPB) {
+    const uint32_t i = s_tab[e];
+    s_tab[e] = kTFree;
+    const uint64_t o = base + cur + e;
+#if SKS_PLACE_DIAG != 4  // (diagnostics 4: no global stores)
+    kv_store<EW>(out_vals, o, key_at<EW>(s_key, i));
+    out_masks[o] = s_msk[i];
+#endif
+    s_msk[i] = 0;
+  }
+  // the largest bucket (entries): the occupied counts of its region's threads
+  uint32_t bo = occ;
+  if (tpb <= 64) {
+    for (uint32_t o2 = 1; o2 < tpb; o2 <<= 1) bo += __shfl_xor(bo, o2, 64);
+  } else {
+    bo = 0;
+    for (uint32_t w = q * (tpb / 64); w < (q + 1) * (tpb / 64); ++w) bo += s_wsum[w];
+  }
+  maxb = max(maxb, bo);
+  cur += total;
+}
+
+// One workgroup per (block, region): the region's value groups one after the
+// other, the next group's elements loading into registers while the current
+// one is placed, the region's entry cursor carried in registers (no cross-
+// workgroup prefix).  Per group of gn <= gcap raw elements (the normal path):
+//   P1  the elements go to s_key / s_own (LDS index = element index), and the
+//       next group's loads are issued into the same registers
+//   P2  every element is inserted into the dedup table (a region of 4096 / 8
+//       slots per bucket of the group); the representative of a value (the
+//       element that claimed its slot) collects the holders' sketch bits
+//   P3  the table is scanned in slot order (bucket by bucket) and freed,
+//   P4  the distinct entries {value, mask} are written at the region cursor.
+// Bucket passes: a group above gcap elements (a dense stretch of values held
+// by a whole family), or with more distinct values in one bucket than the
+// bucket's table region holds, is counted per bucket and placed in passes of
+// consecutive buckets holding <= gcap elements (re-read from the sketches with
+// coalesced loads, compacted into s_key; a pass whose table region overflows
+// is redone one bucket per pass, with the whole table).  A bucket above gcap
+// elements (adversarial values only) takes the slice path: hash slices of the
+// group gathered from the sketches, each deduplicated and written in slice
+// order (a slice still above gcap is split in two).  Exact for any input.
 template <int EW, bool CHECK>
-__global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ data,
+__global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ data,
                                                   const uint64_t* __restrict__ starts, uint32_t count,
                                                   uint32_t log_b, const uint32_t* __restrict__ pos,
                                                   const uint64_t* __restrict__ bstart,
                                                   uint64_t* __restrict__ out_vals,
                                                   unsigned long long* __restrict__ out_masks,
                                                   uint32_t* __restrict__ out_boff, uint32_t* __restrict__ stat,
-                                                  uint32_t gcap, uint32_t* __restrict__ tickets,
-                                                  unsigned long long* __restrict__ status) {
+                                                  uint32_t gcap) {
   __shared__ uint64_t s_key[kGCap * EW];
   __shared__ unsigned long long s_msk[kGCap];
   __shared__ uint32_t s_tab[kTab];
-  __shared__ uint8_t s_own[kGCap];   // element i of the group -> its sketch's slot
-  __shared__ uint64_t s_src[kTile];  // element index in `data` of slot s's element i: s_src[s] + i
-  __shared__ uint32_t s_wsum[kPT / 64];
-  __shared__ uint32_t s_j, s_pre, s_gd, s_qn, s_qd, s_full;
-  __shared__ uint32_t s_stk[2 * 72];  // slow path: (slice, level) work stack
+  __shared__ uint32_t s_pos[(kMaxRG + 1) * kTile];  // [j * 64 + s]: sketch s's start of the region's group j
+  __shared__ uint8_t s_own[kGCap];                  // LDS element -> its sketch slot
+  __shared__ uint32_t s_wsum[kPB / 64];
+  __shared__ uint32_t s_bcnt[1u << jc::kGLog];
+  __shared__ uint32_t s_full, s_pcnt, s_gd, s_qn, s_qd;
+  // s_src[64] (group_load's source offsets) and the slice path's work stack
+  // share one array: the slice path runs after the group's loads have read it
+  __shared__ uint64_t s_aux[72];
+  uint64_t* s_src = s_aux;
+  uint32_t* s_stk = reinterpret_cast<uint32_t*>(s_aux);  // (slice, level) pairs
 
   const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
   const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b);
   const uint32_t RG = (1u << jc::lay_rb_log(log_b)) >> gb_log;
-  const uint32_t blk = blockIdx.x / G, r = (blockIdx.x % G) / RG;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t blk = blockIdx.x / NR, r = blockIdx.x % NR;
+  // the wave index in an SGPR: the per-wave loop bounds stay scalar
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SKS_LAYOUT_STAMPS
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
-  if (tid == 0) s_j = RG == 1 ? 0u : atomicAdd(&tickets[blk * NR + r], 1u);
-  for (uint32_t i = tid; i < kTab / 4; i += kPT)
-    reinterpret_cast<uint4*>(s_tab)[i] = make_uint4(kTFree, kTFree, kTFree, kTFree);
-  for (uint32_t i = tid; i < kGCap / 2; i += kPT) reinterpret_cast<uint4*>(s_msk)[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  const uint32_t j = s_j, g = r * RG + j;
-  unsigned long long* st = status + (uint64_t)(blk * NR + r) * RG;
   const uint32_t s_end = min((uint32_t)kTile, count - kTile * blk);
   uint32_t* boff = out_boff + (uint64_t)blk * (B + NR);
   const uint64_t base = bstart[blk];
   const bool sv = (uint32_t)lane < s_end;
-  const uint32_t* prow = pos + (uint64_t)(kTile * blk + (sv ? lane : 0)) * (G + 1);
   const uint64_t stt = sv ? starts[kTile * blk + lane] : 0;
-  // lane s: its sketch's range [glo, ghi) in the group; the region's raw offset
-  const uint32_t glo = sv ? prow[g] : 0;
-  const uint32_t ghi = sv ? max(prow[g + 1], glo) : 0;
-  const uint32_t roff = __shfl(wave_scan(sv ? prow[r * RG] : 0), 63);
-  const uint32_t gc = ghi - glo, gincl = wave_scan(gc), gpre = gincl - gc;
-  const uint32_t gn = __shfl(gincl, 63);
+  for (uint32_t q = tid; q < (RG + 1) * kTile; q += kPB) {
+    const uint32_t j = q / kTile, s = q % kTile;
+    s_pos[q] = s < s_end ? pos[(uint64_t)(kTile * blk + s) * (G + 1) + r * RG + j] : 0;
+  }
+  for (uint32_t q = tid; q < kTab / 4; q += kPB)
+    reinterpret_cast<uint4*>(s_tab)[q] = make_uint4(kTFree, kTFree, kTFree, kTFree);
+  for (uint32_t q = tid; q < kGCap / 2; q += kPB) reinterpret_cast<uint4*>(s_msk)[q] = make_uint4(0, 0, 0, 0);
+  if (tid == 0) s_full = 0;
+  __syncthreads();
+  // the region's entries start at its raw offset in the block
+  uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(sv ? s_pos[lane] : 0u), 63);
   uint32_t maxb = 0;
+  KV v[kRegPer];
+  uint32_t sl[kRegPer];
+  uint32_t gn = group_map_write(s_pos, s_pos + kTile, sv, stt, lane, wave, s_own, s_src);
+  __syncthreads();
+  group_load<EW>(data, s_own, s_src, gn, tid, v, sl);
   LSTAMP(0);
 
-  bool normal = gn <= gcap;
-  if (normal) {
-    // ---- normal path -------------------------------------------------------------------------
-    for (uint32_t s = wave; s < s_end; s += kPT / 64) {  // owner map: element i -> slot
-      const uint32_t ps = __shfl(gpre, s), cs = __shfl(gc, s);
-      for (uint32_t e = lane; e < cs; e += 64) s_own[ps + e] = (uint8_t)s;
-    }
-    if (wave == 0) s_src[lane] = stt + glo - gpre;
-    if (tid == 0) s_full = 0;
-    __syncthreads();
-    LSTAMP(1);
-    KV v[kPer];
-    uint32_t sl[kPer];
+  for (uint32_t j = 0; j < RG; ++j) {
+    const uint32_t g = r * RG + j;
+    const uint32_t gn_j = gn;
+    // the next group's owner map, then its loads into v / nsl (in flight while
+    // this group is placed: v is in LDS by then, sl still names this group's owners)
+    uint32_t nsl[kRegPer];
+    bool fetched = false;
+    auto map_next = [&]() {
+      gn = j + 1 < RG ? group_map_write(s_pos + (j + 1) * kTile, s_pos + (j + 2) * kTile, sv, stt, lane, wave, s_own,
+                                        s_src)
+                      : 0u;
+    };
+    auto load_next = [&]() {
+      group_load<EW>(data, s_own, s_src, gn, tid, v, nsl);
+      fetched = true;
+    };
+    bool done = false;
+    if (gn_j == 0) {  // an empty group: its buckets start (and end) at the cursor
+      if ((uint32_t)tid < GB) boff[g * GB + tid] = cur;
+      done = true;
+    } else if (gn_j <= gcap) {
+      // ---- normal path ------------------------------------------------------------------------
+      __syncthreads();  // the previous pass has read s_key / s_msk / s_tab, the loads s_own / s_src
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = tid + k * kPT;
-      sl[k] = 0;
-      v[k] = KV{0, 0};
-      if (i < gn) {
-        const uint32_t s = s_own[i];
-        sl[k] = s;
-        v[k] = kv_load<EW>(data, s_src[s] + i);
-      }
-    }
-    // P1
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = tid + k * kPT;
-      if (i < gn) {
-        if constexpr (EW == 1) s_key[i] = v[k].lo;
-        else { s_key[2 * i] = v[k].lo; s_key[2 * i + 1] = v[k].hi; }
-      }
-    }
-    __syncthreads();
-    LSTAMP(2);
-    // P2: dedup; the representative's mask collects the holders' bits
-    bool full = false;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t i = tid + k * kPT;
-      if (i < gn) {
-        uint32_t h;
-        const uint32_t ri = dd_insert<EW>(s_tab, s_key, v[k], i, gb_log, &h, &full);
-        if (CHECK && !kv_eq<EW>(key_at<EW>(s_key, ri), v[k])) atomicAdd(&g_layout_check, 1ull);
-        atomicOr(&s_msk[ri], 1ull << sl[k]);
-      }
-    }
-    if (full) s_full = 1;
-    __syncthreads();
-    LSTAMP(3);
-    normal = s_full == 0;
-    if (normal) {
-      // P3: the table in slot order lists the distinct values bucket by bucket;
-      // thread t owns slots [16 t, 16 t + 16): occupied counts, block scan
-      constexpr uint32_t kSpt = kTab / kPT;
-      uint32_t wv[kSpt];
-#pragma unroll
-      for (int q = 0; q < (int)kSpt / 4; ++q) {
-        const uint4 x = reinterpret_cast<const uint4*>(s_tab)[tid * (kSpt / 4) + q];
-        wv[4 * q] = x.x;
-        wv[4 * q + 1] = x.y;
-        wv[4 * q + 2] = x.z;
-        wv[4 * q + 3] = x.w;
-      }
-      uint32_t occ = 0;
-#pragma unroll
-      for (int q = 0; q < (int)kSpt; ++q) occ += wv[q] != kTFree;
-      const uint32_t wincl = wave_scan(occ);
-      if (lane == 63) s_wsum[wave] = wincl;
-      __syncthreads();
-      uint32_t before = 0, total = 0;
-#pragma unroll
-      for (int w = 0; w < kPT / 64; ++w) {
-        const uint32_t x = s_wsum[w];
-        before += w < wave ? x : 0;
-        total += x;
-      }
-      const uint32_t excl = before + wincl - occ;  // entries before this thread's slots
-      if (tid == 0) {
-        if (j == 0) {
-          if (RG > 1) status_publish(st, kStInc | total);
-          s_pre = 0;
-        } else {
-          status_publish(st + j, kStAgg | total);
-          const uint32_t pre = region_prefix(st, j);
-          status_publish(st + j, kStInc | (uint64_t)(pre + total));
-          s_pre = pre;
+      for (int k = 0; k < kRegPer; ++k) {  // P1
+        const uint32_t i = tid + k * kPB;
+        if (i < gn_j) {
+          if constexpr (EW == 1) s_key[i] = v[k].lo;
+          else { s_key[2 * i] = v[k].lo; s_key[2 * i + 1] = v[k].hi; }
         }
       }
-      // bucket b's slots are threads [b * tpb, (b + 1) * tpb): its start and size
-      const uint32_t tpb = kPT >> gb_log;
-      const uint32_t b = tid / tpb;
+      if ((uint32_t)tid < GB) s_bcnt[tid] = 0;  // (read by every thread before the barrier above)
+      map_next();
       __syncthreads();
-      LSTAMP(4);
-      const uint32_t start = roff + s_pre;
-      if (tid % tpb == 0) boff[g * GB + b] = start + excl;
-      if (tid == 0 && j + 1 == RG) boff[B + r] = start + total;
-      // P4: write this thread's entries in slot order
-      uint32_t d = excl;
+      load_next();
+      LSTAMP(1);
+      // P2 (the values read back from LDS), every element's first probe issued
+      // together: keys, first compare-swaps, the named elements' keys; then the
+      // (rare) rest of each chain, one exit edge (see dd_insert).  A slot word
+      // is the claiming element's index; the element that claims a slot is its
+      // value's representative and takes the next place of its bucket
+      // (s_bcnt: entries are contiguous per bucket, in any order within it).
+      bool full = false;
+      const uint32_t rlog = kTabLog - gb_log, rmask = (1u << rlog) - 1;
+      uint32_t h[kRegPer], w[kRegPer], rep[kRegPer];
 #pragma unroll
-      for (int q = 0; q < (int)kSpt; ++q) {
-        if (wv[q] == kTFree) continue;
-        const uint32_t i = wv[q] & kIdxMask;
-        const uint64_t o = base + start + d;
-        ++d;
-        kv_store<EW>(out_vals, o, key_at<EW>(s_key, i));
-        out_masks[o] = s_msk[i];
-      }
-      // largest bucket: per bucket, the sum of its threads' occupied counts
-      uint32_t bo = occ;
-      for (uint32_t o2 = 1; o2 < tpb && o2 < 64; o2 <<= 1) bo += __shfl_xor(bo, o2, 64);
-      if (tpb > 64) {  // a bucket spans waves (gb_log < 2): add the other waves' sums
-        if (lane == 0) s_wsum[wave] = bo;
-        __syncthreads();
-        bo = 0;
-        for (uint32_t w = (tid / tpb) * (tpb / 64); w < (tid / tpb + 1) * (tpb / 64); ++w) bo += s_wsum[w];
-      }
-      maxb = max(maxb, bo);
-      LSTAMP(5);
-    }
-  }
-  if (!normal) {
-    // ---- slow path: the prefix first, then hash slices of the group ------------------------
-    for (uint32_t q = tid; q < kTab / 4; q += kPT)  // (after a full table on the normal path)
-      reinterpret_cast<uint4*>(s_tab)[q] = make_uint4(kTFree, kTFree, kTFree, kTFree);
-    if (tid == 0) s_pre = region_prefix(st, j);
-    __syncthreads();
-    const uint32_t start = roff + s_pre;
-    uint32_t cur = start;
-    uint32_t lvl0 = max(gb_log, 1u);
-    while (lvl0 < 32 && ((uint64_t)gn >> (lvl0 - 1)) > gcap / 2) ++lvl0;
-    uint32_t bk_cur = ~0u, bk_start = cur;
-    for (uint32_t q0 = 0; q0 < (1u << lvl0); ++q0) {
-      // depth-first over the slice and, when it is too large, its halves
-      // (smallest slice on top, so slices come out in hash order)
-      if (tid == 0) {
-        s_stk[0] = q0;
-        s_stk[1] = lvl0;
-        s_qd = 1;
-      }
-      __syncthreads();
-      for (;;) {
-        const uint32_t depth = s_qd;
-        if (depth == 0) break;
-        const uint32_t q = s_stk[2 * (depth - 1)], lvl = s_stk[2 * (depth - 1) + 1];
-        __syncthreads();
-        if (tid == 0) {
-          s_qd = depth - 1;
-          s_qn = 0;
-          s_gd = 0;
+      for (int k = 0; k < kRegPer; ++k) {
+        const uint32_t i = tid + k * kPB;
+        w[k] = kTFree;
+        h[k] = 0;
+        if (i < gn_j) {
+          const KV x = key_at<EW>(s_key, i);
+          h[k] = (kv_group_bucket<EW>(x, gb_log) << rlog) | (dd_slot<EW>(x) & rmask);
+          w[k] = atomicCAS(&s_tab[h[k]], kTFree, i);
         }
-        for (uint32_t i = tid; i < kTab / 4; i += kPT)
-          reinterpret_cast<uint4*>(s_tab)[i] = make_uint4(kTFree, kTFree, kTFree, kTFree);
-        __syncthreads();
-        for (uint32_t s = wave; s < s_end; s += kPT / 64) {
-          const uint32_t a = __shfl(glo, s), b = __shfl(ghi, s);
-          const uint64_t sts = __shfl(stt, s);
-          for (uint32_t e = a + lane; e < b; e += 64) {
-            const KV x = kv_load<EW>(data, sts + e);
-            if ((kv_mix<EW>(x) >> (64 - lvl)) == (uint64_t)q) {
-              const uint32_t idx = atomicAdd(&s_qn, 1u);
-              if (idx < gcap) {
-                if constexpr (EW == 1) s_key[idx] = x.lo;
-                else { s_key[2 * idx] = x.lo; s_key[2 * idx + 1] = x.hi; }
-                s_own[idx] = (uint8_t)s;
-              }
-            }
+      }
+#pragma unroll
+      for (int k = 0; k < kRegPer; ++k) {
+        const uint32_t i = tid + k * kPB;
+        rep[k] = kTFree;
+        if (i < gn_j) {
+          const KV x = key_at<EW>(s_key, i);
+          const uint32_t rbase = h[k] & ~rmask;
+          uint32_t hh = h[k] & rmask, xw = w[k], steps = 0;
+          KV u = key_at<EW>(s_key, xw & kIdxMask);
+          for (;;) {
+            if ((xw == kTFree) | kv_eq<EW>(u, x) | (steps > rmask)) break;
+            hh = (hh + 1) & rmask;
+            ++steps;
+            xw = atomicCAS(&s_tab[rbase + hh], kTFree, i);
+            u = key_at<EW>(s_key, xw & kIdxMask);
+          }
+          const bool f = steps > rmask;  // (an overflowed region names a foreign entry: the group is redone)
+          full |= f;
+          const uint32_t ri = xw == kTFree ? i : xw;
+          if (CHECK && !f && !kv_eq<EW>(key_at<EW>(s_key, ri), x)) atomicAdd(&g_layout_check, 1ull);
+          atomicOr(&s_msk[ri], 1ull << sl[k]);
+          if (xw == kTFree) {  // the representative: its slot (freed at emit) and its place in the bucket
+            const uint32_t bk = h[k] >> rlog;
+            rep[k] = (bk << 12) | atomicAdd(&s_bcnt[bk], 1u);
+            h[k] = rbase + hh;
           }
         }
-        __syncthreads();
-        const uint32_t nq = s_qn;
-        if (nq > gcap) {
-          // split the slice: one value has at most 64 holders, so halves of
-          // distinct values shrink; a 64-bit mix is a bijection for u64 values
-          if (lvl < 64) {
-            if (tid == 0) {
-              const uint32_t d = s_qd;
-              s_stk[2 * d] = 2 * q + 1;
-              s_stk[2 * d + 1] = lvl + 1;
-              s_stk[2 * d + 2] = 2 * q;
-              s_stk[2 * d + 3] = lvl + 1;
-              s_qd = d + 2;
-            }
-          } else if (tid == 0) {
-            atomicAdd(stat + 1, 1u);  // > gcap 128-bit values with one 64-bit mix: layout invalid
-          }
-          __syncthreads();
-          continue;
-        }
-        const uint32_t bq = (uint32_t)((uint64_t)q >> (lvl - gb_log));  // the slice's bucket
-        if (bq != bk_cur) {  // first slice of a bucket
-          if (bk_cur != ~0u) maxb = max(maxb, cur - bk_start);
-          bk_cur = bq;
-          bk_start = cur;
-          if (tid == 0) boff[g * GB + bq] = cur;
-        }
-        for (uint32_t i = tid; i < nq; i += kPT) s_msk[i] = 0;
-        __syncthreads();
-        bool rp[kPer];
+      }
+      if (full) s_full = 1;
+      __syncthreads();
+      LSTAMP(2);
+      if (s_full == 0) {
+        // P3: bucket starts from the counts; P4: every representative writes its
+        // entry {value, mask} and frees its slot and mask
+        uint32_t pre[1u << jc::kGLog], tot = 0;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-          const uint32_t i = tid + k * kPT;
-          rp[k] = false;
-          if (i < nq) {
-            const KV x = key_at<EW>(s_key, i);
-            uint32_t h;
-            bool full_unused = false;  // one region of kTab slots for <= gcap <= kTab / 2 elements
-            const uint32_t ri = dd_insert<EW>(s_tab, s_key, x, i, 0u, &h, &full_unused);
-            if (CHECK && !kv_eq<EW>(key_at<EW>(s_key, ri), x)) atomicAdd(&g_layout_check, 1ull);
-            atomicOr(&s_msk[ri], 1ull << s_own[i]);
-            rp[k] = ri == i;
-          }
+        for (uint32_t b = 0; b < (1u << jc::kGLog); ++b) {
+          const uint32_t c = b < GB ? s_bcnt[b] : 0u;
+          pre[b] = tot;
+          tot += c;
+          maxb = max(maxb, c);
         }
-        __syncthreads();
+        if ((uint32_t)tid < GB) boff[g * GB + tid] = cur + pre[tid];
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-          if (!rp[k]) continue;
-          const uint32_t i = tid + k * kPT;
-          const uint32_t d = atomicAdd(&s_gd, 1u);
-          const uint64_t o = base + cur + d;
+        for (int k = 0; k < kRegPer; ++k) {
+          if (rep[k] == kTFree) continue;
+          const uint32_t i = tid + k * kPB;
+          const uint64_t o = base + cur + pre[rep[k] >> 12] + (rep[k] & 4095u);
+#if SKS_PLACE_DIAG != 4  // (diagnostics 4: no global stores)
           kv_store<EW>(out_vals, o, key_at<EW>(s_key, i));
           out_masks[o] = s_msk[i];
-        }
-        __syncthreads();
-        cur += s_gd;
-      }
-      __syncthreads();  // every thread has read the empty stack before the next slice is pushed
-    }
-    if (bk_cur != ~0u) maxb = max(maxb, cur - bk_start);
-    LSTAMP(7);
-#ifdef SKS_LAYOUT_STAMPS
-    if (tid == 0) atomicAdd(&g_layout_stamps[8], 1ull);
 #endif
-    if (tid == 0) {
-      status_publish(st + j, kStInc | (uint64_t)(cur - roff));
-      if (j + 1 == RG) boff[B + r] = cur;
+          s_msk[i] = 0;
+          s_tab[h[k]] = kTFree;
+        }
+        cur += tot;
+        done = true;
+      } else {  // a bucket region overflowed: clean up, place the group in bucket passes
+        for (uint32_t q = tid; q < kTab / 4; q += kPB)
+          reinterpret_cast<uint4*>(s_tab)[q] = make_uint4(kTFree, kTFree, kTFree, kTFree);
+        for (uint32_t q = tid; q < kGCap / 2; q += kPB) reinterpret_cast<uint4*>(s_msk)[q] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        if (tid == 0) s_full = 0;
+      }
+      LSTAMP(3);
     }
+    if (!fetched) {
+      __syncthreads();  // the owner map and s_src are free
+      map_next();
+      __syncthreads();
+      load_next();
+    }
+    if (!done) {
+      // ---- bucket passes ------------------------------------------------------------------------
+      const GroupMap m = group_map(s_pos + j * kTile, s_pos + (j + 1) * kTile, sv, stt, lane);
+      // visits every element of the group (coalesced, kPassU chunks per round): f(value, slot)
+      auto for_each = [&](auto&& f) {
+        for (uint32_t c0 = (uint32_t)wave * 64; c0 < m.gn; c0 += kPB * kPassU) {
+          KV x[kPassU];
+          uint32_t o[kPassU];
+#pragma unroll
+          for (int u = 0; u < kPassU; ++u) {
+            const uint32_t b = c0 + u * kPB;
+            o[u] = 0;
+            x[u] = KV{0, 0};
+            if (b < m.gn) {
+              const uint64_t at = elem_at(m, b, lane, &o[u]);
+              if (b + (uint32_t)lane < m.gn) x[u] = kv_load<EW>(data, at);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kPassU; ++u)
+            if (c0 + u * kPB + (uint32_t)lane < m.gn) f(x[u], o[u]);
+        }
+      };
+      __syncthreads();
+      if ((uint32_t)tid < GB) s_bcnt[tid] = 0;
+      __syncthreads();
+      for_each([&](const KV& x, uint32_t) { atomicAdd(&s_bcnt[kv_group_bucket<EW>(x, gb_log)], 1u); });
+      __syncthreads();
+      bool slices = false;
+      for (uint32_t b = 0; b < GB; ++b) slices |= s_bcnt[b] > gcap;
+      // passes [b0, b1) of consecutive buckets with <= gcap elements; one_bucket
+      // after a pass whose table region overflowed
+      uint32_t b0 = 0;
+      bool one_bucket = false;
+      while (!slices && b0 < GB) {
+        uint32_t b1 = b0 + 1, n = s_bcnt[b0];
+        if (!one_bucket)
+          while (b1 < GB && n + s_bcnt[b1] <= gcap) n += s_bcnt[b1++];
+        if (n == 0) {  // empty buckets start (and end) at the cursor
+          if ((uint32_t)tid < b1 - b0) boff[g * GB + b0 + tid] = cur;
+          b0 = b1;
+          continue;
+        }
+        uint32_t pl = 0;
+        while ((1u << pl) < b1 - b0) ++pl;
+        __syncthreads();  // the previous pass has read s_key / s_msk / s_own / s_pcnt
+        if (tid == 0) s_pcnt = 0;
+        __syncthreads();
+        for_each([&](const KV& x, uint32_t o) {
+          if (kv_group_bucket<EW>(x, gb_log) - b0 < b1 - b0) {
+            const uint32_t idx = atomicAdd(&s_pcnt, 1u);
+            if constexpr (EW == 1) s_key[idx] = x.lo;
+            else { s_key[2 * idx] = x.lo; s_key[2 * idx + 1] = x.hi; }
+            s_own[idx] = (uint8_t)o;
+          }
+        });
+        __syncthreads();
+        const uint32_t np = s_pcnt, rlog = kTabLog - pl;
+        bool full = false;
+        for (uint32_t i = tid; i < np; i += kPB) {
+          const KV x = key_at<EW>(s_key, i);
+          bool f = false;
+          const uint32_t ri = dd_insert<EW>(s_tab, s_key, x, i, (kv_group_bucket<EW>(x, gb_log) - b0) << rlog,
+                                            (1u << rlog) - 1, &f);
+          full |= f;
+          if (CHECK && !f && !kv_eq<EW>(key_at<EW>(s_key, ri), x)) atomicAdd(&g_layout_check, 1ull);
+          atomicOr(&s_msk[ri], 1ull << s_own[i]);
+        }
+        if (full) s_full = 1;
+        __syncthreads();
+        if (s_full) {  // redo these buckets one per pass
+          for (uint32_t q = tid; q < kTab / 4; q += kPB)
+            reinterpret_cast<uint4*>(s_tab)[q] = make_uint4(kTFree, kTFree, kTFree, kTFree);
+          for (uint32_t q = tid; q < kGCap / 2; q += kPB) reinterpret_cast<uint4*>(s_msk)[q] = make_uint4(0, 0, 0, 0);
+          __syncthreads();
+          if (tid == 0) s_full = 0;
+          one_bucket = true;
+          continue;
+        }
+        emit_pass<EW>(s_tab, s_key, s_msk, s_wsum, boff + g * GB + b0, b1 - b0, pl, base, out_vals, out_masks, cur,
+                      maxb, tid, lane, wave);
+        b0 = b1;
+      }
+      if (slices) {
+        // ---- slice path: hash slices of the group, gathered from the sketches -----------------
+        const uint32_t glo = sv ? s_pos[j * kTile + lane] : 0;
+        const uint32_t ghi = sv ? max(s_pos[(j + 1) * kTile + lane], glo) : 0;
+        uint32_t lvl0 = max(gb_log, 1u);
+        while (lvl0 < 32 && ((uint64_t)gn_j >> (lvl0 - 1)) > gcap / 2) ++lvl0;
+        uint32_t bk_cur = ~0u, bk_start = cur;
+        for (uint32_t q0 = 0; q0 < (1u << lvl0); ++q0) {
+          // depth-first over the slice and, when it is too large, its halves
+          // (smallest slice on top, so slices come out in hash order)
+          __syncthreads();
+          if (tid == 0) {
+            s_stk[0] = q0;
+            s_stk[1] = lvl0;
+            s_qd = 1;
+          }
+          __syncthreads();
+          for (;;) {
+            const uint32_t depth = s_qd;
+            if (depth == 0) break;
+            const uint32_t q = s_stk[2 * (depth - 1)], lvl = s_stk[2 * (depth - 1) + 1];
+            __syncthreads();
+            if (tid == 0) {
+              s_qd = depth - 1;
+              s_qn = 0;
+              s_gd = 0;
+            }
+            for (uint32_t i = tid; i < kTab / 4; i += kPB)
+              reinterpret_cast<uint4*>(s_tab)[i] = make_uint4(kTFree, kTFree, kTFree, kTFree);
+            __syncthreads();
+            for (uint32_t s = wave; s < s_end; s += kPB / 64) {
+              const uint32_t a = __shfl(glo, s), b = __shfl(ghi, s);
+              const uint64_t sts = __shfl(stt, s);
+              for (uint32_t e = a + lane; e < b; e += 64) {
+                const KV x = kv_load<EW>(data, sts + e);
+                if ((kv_mix<EW>(x) >> (64 - lvl)) == (uint64_t)q) {
+                  const uint32_t idx = atomicAdd(&s_qn, 1u);
+                  if (idx < gcap) {
+                    if constexpr (EW == 1) s_key[idx] = x.lo;
+                    else { s_key[2 * idx] = x.lo; s_key[2 * idx + 1] = x.hi; }
+                    s_own[idx] = (uint8_t)s;
+                  }
+                }
+              }
+            }
+            __syncthreads();
+            const uint32_t nq = s_qn;
+            if (nq > gcap) {
+              // split the slice: one value has at most 64 holders, so halves of
+              // distinct values shrink; a 64-bit mix is a bijection for u64 values
+              if (lvl < 64) {
+                if (tid == 0) {
+                  const uint32_t d = s_qd;
+                  s_stk[2 * d] = 2 * q + 1;
+                  s_stk[2 * d + 1] = lvl + 1;
+                  s_stk[2 * d + 2] = 2 * q;
+                  s_stk[2 * d + 3] = lvl + 1;
+                  s_qd = d + 2;
+                }
+              } else if (tid == 0) {
+                atomicAdd(stat + 1, 1u);  // > gcap 128-bit values with one 64-bit mix: layout invalid
+              }
+              __syncthreads();
+              continue;
+            }
+            const uint32_t bq = (uint32_t)((uint64_t)q >> (lvl - gb_log));  // the slice's bucket
+            if (bq != bk_cur) {  // first slice of a bucket
+              if (bk_cur != ~0u) maxb = max(maxb, cur - bk_start);
+              bk_cur = bq;
+              bk_start = cur;
+              if (tid == 0) boff[g * GB + bq] = cur;
+            }
+            for (uint32_t i = tid; i < nq; i += kPB) s_msk[i] = 0;
+            __syncthreads();
+            bool rp[kSlowPer];
+#pragma unroll
+            for (int k = 0; k < kSlowPer; ++k) {
+              const uint32_t i = tid + k * kPB;
+              rp[k] = false;
+              if (i < nq) {
+                const KV x = key_at<EW>(s_key, i);
+                bool full_unused = false;  // one region of kTab slots for <= gcap <= kTab / 2 elements
+                const uint32_t ri = dd_insert<EW>(s_tab, s_key, x, i, 0u, kTab - 1, &full_unused);
+                if (CHECK && !kv_eq<EW>(key_at<EW>(s_key, ri), x)) atomicAdd(&g_layout_check, 1ull);
+                atomicOr(&s_msk[ri], 1ull << s_own[i]);
+                rp[k] = ri == i;
+              }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kSlowPer; ++k) {
+              if (!rp[k]) continue;
+              const uint32_t i = tid + k * kPB;
+              const uint32_t d = atomicAdd(&s_gd, 1u);
+              const uint64_t o = base + cur + d;
+              kv_store<EW>(out_vals, o, key_at<EW>(s_key, i));
+              out_masks[o] = s_msk[i];
+            }
+            __syncthreads();
+            cur += s_gd;
+          }
+        }
+        if (bk_cur != ~0u) maxb = max(maxb, cur - bk_start);
+        // leave the table free and the masks clear for the next group
+        __syncthreads();
+        for (uint32_t q = tid; q < kTab / 4; q += kPB)
+          reinterpret_cast<uint4*>(s_tab)[q] = make_uint4(kTFree, kTFree, kTFree, kTFree);
+        for (uint32_t q = tid; q < kGCap / 2; q += kPB) reinterpret_cast<uint4*>(s_msk)[q] = make_uint4(0, 0, 0, 0);
+#ifdef SKS_LAYOUT_STAMPS
+        if (tid == 0) atomicAdd(&g_layout_stamps[8], 1ull);
+#endif
+      }
+      LSTAMP(4);
+    }
+#pragma unroll
+    for (int k = 0; k < kRegPer; ++k) sl[k] = nsl[k];
   }
+  if (tid == 0) boff[B + r] = cur;
   // the largest block-bucket: one word for every workgroup; the stat only
   // grows, so a workgroup whose maximum is not above the value it reads skips
   // the atomic (one word takes ~88 atomics per microsecond)
@@ -608,6 +847,7 @@ __global__ __launch_bounds__(kPT) void k_gl_place(const uint64_t* __restrict__ d
       atomicMax(stat, maxb);
   }
 }
+
 
 }  // namespace
 
@@ -628,12 +868,10 @@ hipError_t join_layout_bounds(const uint64_t* data, const uint64_t* starts, cons
   return hipGetLastError();
 }
 
-// temp = bounds | pos[count][G + 1] | tickets[n_blk * NR] (even) | look-back words[n_blk * G]
+// temp = bounds | pos[count][G + 1]
 size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, int ew) {
-  const uint64_t G = jc::lay_groups(log_b), n_blk = (count + kTile - 1) / kTile;
-  const uint64_t n_tick = n_blk * jc::lay_regions(log_b);
-  return ((G + 1) * 8 * ew + 255) / 256 * 256 + (uint64_t)count * (G + 1) * 4 + ((n_tick + 1) & ~1ull) * 4 +
-         n_blk * G * 8 + 16;
+  const uint64_t G = jc::lay_groups(log_b);
+  return ((G + 1) * 8 * ew + 255) / 256 * 256 + (uint64_t)count * (G + 1) * 4 + 16;
 }
 
 // SKS_LAYOUT_GROUP_CAP (diagnostics, clamped to [64, kGCap]): the largest
@@ -662,40 +900,32 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   const uint32_t n_blk = (count + kTile - 1) / kTile;
   uint64_t* bounds_tmp = static_cast<uint64_t*>(temp);
   uint32_t* pos = reinterpret_cast<uint32_t*>(static_cast<char*>(temp) + ((G + 1) * 8 * ew + 255) / 256 * 256);
-  // placement tickets [n_blk * NR] u32, then look-back words [n_blk * G] u64
-  const uint64_t n_tick = (uint64_t)n_blk * jc::lay_regions(log_b);
-  uint32_t* tickets = pos + (((uint64_t)count * (G + 1) + 1) & ~(uint64_t)1);  // 8-byte aligned
-  unsigned long long* status =
-      reinterpret_cast<unsigned long long*>(tickets + ((n_tick + 1) & ~(uint64_t)1));
-  const uint32_t n_zero = (uint32_t)(((n_tick + 1) & ~(uint64_t)1) + 2ull * n_blk * G);
   // bounds (unless given) and block starts in one launch, the groups' positions
-  // in every sketch (and the zeroed look-back state), then the placement
+  // in every sketch, then the placement: a workgroup per (block, region)
   const uint32_t nb_bounds = d_bounds ? 0 : (G + 1 + kPT / 64 - 1) / (kPT / 64);
   const uint64_t* bounds = d_bounds ? d_bounds : bounds_tmp;
-  const dim3 grid_place(n_blk * G);
+  const dim3 grid_place(n_blk * jc::lay_regions(log_b));
   auto* masks = reinterpret_cast<unsigned long long*>(out_masks);
   if (ew == 1) {
     hipLaunchKernelGGL(k_gl_prep<1>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
                        bounds_tmp, nb_bounds, out_bstart);
-    hipLaunchKernelGGL(k_gl_pos<1>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos,
-                       tickets, n_zero);
+    hipLaunchKernelGGL(k_gl_pos<1>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
     if (check)
-      hipLaunchKernelGGL((k_gl_place<1, true>), grid_place, dim3(kPT), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), tickets, status);
+      hipLaunchKernelGGL((k_gl_place<1, true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
     else
-      hipLaunchKernelGGL((k_gl_place<1, false>), grid_place, dim3(kPT), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), tickets, status);
+      hipLaunchKernelGGL((k_gl_place<1, false>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
   } else {
     hipLaunchKernelGGL(k_gl_prep<2>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
                        bounds_tmp, nb_bounds, out_bstart);
-    hipLaunchKernelGGL(k_gl_pos<2>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos,
-                       tickets, n_zero);
+    hipLaunchKernelGGL(k_gl_pos<2>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
     if (check)
-      hipLaunchKernelGGL((k_gl_place<2, true>), grid_place, dim3(kPT), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), tickets, status);
+      hipLaunchKernelGGL((k_gl_place<2, true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
     else
-      hipLaunchKernelGGL((k_gl_place<2, false>), grid_place, dim3(kPT), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), tickets, status);
+      hipLaunchKernelGGL((k_gl_place<2, false>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
   }
 #ifdef SKS_LAYOUT_STAMPS
   {
@@ -705,9 +935,9 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
     const unsigned long long z[10] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_layout_stamps), z, sizeof z);
     const double wgs = (double)grid_place.x;
-    fprintf(stderr, "[k_gl_place stamps] cycles per workgroup: ticket+meta %.0f own %.0f load+P1 %.0f P2 %.0f "
-            "P3+lookback %.0f P4 %.0f | slow groups %llu, cycles each %.0f (%.0f workgroups)\n", h[0] / wgs,
-            h[1] / wgs, h[2] / wgs, h[3] / wgs, h[4] / wgs, h[5] / wgs, h[8], h[8] ? h[7] / (double)h[8] : 0.0, wgs);
+    fprintf(stderr, "[k_gl_place stamps] cycles per workgroup: setup+first load %.0f P1+next map+loads %.0f P2 %.0f "
+            "P3+P4 %.0f bucket passes / slow %.0f | slow groups %llu (%.0f workgroups)\n", h[0] / wgs,
+            h[1] / wgs, h[2] / wgs, h[3] / wgs, h[4] / wgs, h[8], wgs);
   }
 #endif
   return hipGetLastError();

@@ -35,8 +35,17 @@ def source_hash(rels=None):
     return h.hexdigest()[:16]
 
 
+# the sources of the all-pairs join (k_join and its layout build):
+# profiles/rNN/pair_lds.json records this hash
+JOIN_FILES = ["csrc/join.hip", "csrc/join_common.hpp", "csrc/layout.hip", "csrc/sks_internal.hpp"]
+
+
 def scan_hash():
     return source_hash(SCAN_FILES)
+
+
+def join_hash():
+    return source_hash(JOIN_FILES)
 
 
 if __name__ == "__main__":

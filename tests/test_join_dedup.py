@@ -155,3 +155,40 @@ def test_layout_slow_path_slice_splits(torch_cuda, ctx, monkeypatch, shape):
         assert ctx.join_check_violations() == 0
     finally:
         ctx.set_join_check(False)
+
+
+@pytest.mark.parametrize("shape", ["one_bucket", "gcap256"])
+def test_layout_bucket_passes(torch_cuda, ctx, monkeypatch, shape):
+    """Inputs that leave the layout build's normal path but not its register
+    and bucket-pass paths.  one_bucket (default group cap): every value hashes
+    into the same bucket of its value group (the top bits of
+    v * 0x9E3779B97F4A7C15, layout.hip kv_mix), so that bucket's table region
+    (512 of the 4096 slots) overflows and the group is redone in bucket passes.
+    gcap256: group cap 256 with groups of ~750 elements in 3 families, so
+    groups are placed in passes of consecutive buckets holding <= 256 elements,
+    re-read from the sketches.  With the check kernels on, no invariant is
+    violated and the counts equal numpy's."""
+    torch = torch_cuda
+    rng = np.random.default_rng({"one_bucket": 11, "gcap256": 12}[shape])
+    n = 140
+    if shape == "one_bucket":
+        pool = rng.integers(0, 2**64 - 1, size=4_000_000, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            pool = pool[(pool * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(61) == 0]
+        pool = np.unique(pool)[:200_000]
+        sk = [np.unique(pool[rng.integers(0, pool.size, size=1500)]) for _ in range(n)]
+    else:
+        monkeypatch.setenv("SKS_LAYOUT_GROUP_CAP", "256")
+        base = [np.unique(rng.integers(0, 2**62, size=3000, dtype=np.uint64)) for _ in range(3)]
+        sk = [np.unique(np.concatenate([base[i % 3][rng.random(base[i % 3].size) < 0.9],
+                                        rng.integers(0, 2**62, size=100, dtype=np.uint64)])) for i in range(n)]
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)]
+                     for i in range(n)])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    ctx.set_join_check(True)
+    try:
+        for got in _all_ways(torch, ctx, d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n):
+            assert np.array_equal(got, want)
+        assert ctx.join_check_violations() == 0
+    finally:
+        ctx.set_join_check(False)

@@ -48,6 +48,27 @@ def _pmc_per_dispatch(path, counter):
     return [vals[k] for k in sorted(vals)]
 
 
+def _pmc_kernel(d, kernel, counter):
+    """Per-dispatch values (summed over the counter's dimensions) of `counter`
+    for dispatches of `kernel` in the PMC passes under d."""
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+                k = (f, int(r["Dispatch_Id"]))
+                vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def _pmc_kernel_ms(d, kernel):
+    ms = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"]:
+                ms[(f, int(r["Dispatch_Id"]))] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+    return statistics.median(ms.values()) if ms else None
+
+
 def main(src, dst, warmup, steps):
     os.makedirs(dst, exist_ok=True)
     stats = _one(os.path.join(src, "trace"), "*kernel_stats.csv")
@@ -95,6 +116,42 @@ def main(src, dst, warmup, steps):
             with redirect_stdout(buf):
                 pmc_by_kernel.main(os.path.join(src, sub), kernels)
             open(os.path.join(dst, name), "w").write(buf.getvalue())
+    # scan VALU issue (roofline.valu): counted VALU per launch, the hot block's mix
+    sq = os.path.join(src, "sq")
+    if os.path.isdir(sq):
+        insts = _pmc_kernel(sq, SCAN, "SQ_INSTS_VALU")
+        import valu_mix
+        buf = io.StringIO()
+        with redirect_stdout(buf):
+            valu_mix.main(None)
+        mix = json.loads(buf.getvalue())
+        windows = None
+        try:
+            line = [l for l in open(os.path.join(src, "bench_traced.json")) if l.startswith("{")][-1]
+            windows = json.loads(line)["config"]["windows_per_genome"]
+        except (OSError, IndexError, KeyError, ValueError):
+            pass
+        valu = {"kernel": SCAN, "sq_insts_valu_per_launch": statistics.median(insts) if insts else None,
+                "windows_per_launch": windows,
+                "valu_per_window": (64 * statistics.median(insts) / windows) if insts and windows else None,
+                "hot_block_valu": mix["hot_block_valu"], "hot_block_cycles": mix["hot_block_cycles"],
+                "mean_cycles_per_valu": mix["mean_cycles_per_valu"],
+                "mean_ns_per_valu_per_simd": mix["mean_cycles_per_valu"] / 2.4,
+                "rates": mix["cycles_unit"], "scan_source_hash": srchash.scan_hash()}
+        with open(os.path.join(dst, "scan_valu.json"), "w") as f:
+            json.dump(valu, f, indent=1)
+    # k_join LDS instructions per all-pairs call (pairs.roofline in bench.py)
+    pr = os.path.join(src, "pairs")
+    if os.path.isdir(pr):
+        lds = {"kernel": "k_join<1, false> (config 4, 1000 x bottom-s 10000, tools/bench_pairs.py family)",
+               "join_source_hash": srchash.join_hash()}
+        for c in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
+                  "SQ_WAVE_CYCLES", "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE"):
+            v = _pmc_kernel(pr, "k_join", c)
+            lds[c.lower() + "_per_call"] = statistics.median(v) if v else None
+        lds["profiled_ms"] = _pmc_kernel_ms(pr, "k_join")
+        with open(os.path.join(dst, "pair_lds.json"), "w") as f:
+            json.dump(lds, f, indent=1)
     print(json.dumps({"launches": {k: launches[k] for k in ("median_ms", "mean_ms", "bench_line_hipevent_kernel_ms")},
                       "traffic": traffic["scan_hbm_bytes_per_launch"]}, indent=1))
 
