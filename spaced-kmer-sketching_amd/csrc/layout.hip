@@ -266,7 +266,9 @@ __device__ unsigned long long g_layout_stamps[10];
 #define SKS_PLACE_DIAG 0
 #endif
 constexpr int kPB = 256;                     // threads of the placement kernel
-constexpr int kRegPer = kGCap / kPB;         // group elements per thread held in registers (8)
+constexpr int kTPS = kPB / 64;               // threads per sketch in the register path (4)
+constexpr int kRegPer = 12;                  // elements of its sketch per thread held in registers
+constexpr uint32_t kSkCap = kTPS * kRegPer;  // a group with a sketch holding more (48) takes the bucket passes
 constexpr int kSlowPer = kGCap / kPB;        // slice path: slice elements per thread
 constexpr uint32_t kSpt = kTab / kPB;        // table slots per thread in the emit scan (16)
 constexpr uint32_t kMaxRG = 1u << jc::kRGLog;
@@ -321,43 +323,43 @@ __device__ __forceinline__ uint64_t elem_at(const GroupMap& m, uint32_t b, int l
   return at + i;
 }
 
-// The owner map of a value group of at most kGCap elements (for the loads of
-// group_load): s_own[i] = the sketch slot of element i, s_src[s] = sketch s's
-// source offset (element i of sketch s is data[s_src[s] + i]).  Wave w writes
-// the ranges of sketches w, w + 4, ..., a lane per element.  Returns gn (above
-// kGCap nothing is written: such a group takes the bucket passes).
-__device__ __forceinline__ uint32_t group_map_write(const uint32_t* p0, const uint32_t* p1, bool sv, uint64_t stt,
-                                                    int lane, int wave, uint8_t* s_own, uint64_t* s_src) {
-  const GroupMap m = group_map(p0, p1, sv, stt, lane);
-  if (m.gn <= kGCap) {
-    if (wave == 0) s_src[lane] = m.src;
-    for (uint32_t s = (uint32_t)wave; s < 64; s += kPB / 64) {
-      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)m.gc, (int)s);
-      const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)m.gend, (int)s) - c;
-      for (uint32_t e = (uint32_t)lane; e < c; e += 64) s_own[e0 + e] = (uint8_t)s;
-    }
-  }
-  return m.gn;
+// Thread t's view of a value group in the register path: it serves sketch
+// s = t / 4 (the block's 64 sketches, 4 threads each) and loads elements
+// e = t % 4 + 4 k of the sketch's part of the group (e < gc) from
+// data[src + e]; the element's LDS index is gpre + e (the group's elements,
+// sketch by sketch).  fat: some sketch holds more than kSkCap elements of the
+// group (the group takes the bucket passes).
+struct GroupView {
+  uint32_t gn, gpre, gc;
+  uint64_t src;
+  bool fat;
+};
+__device__ __forceinline__ GroupView group_view(const uint32_t* p0, const uint32_t* p1, bool sv, uint64_t stt,
+                                                int lane, uint32_t s) {
+  const GroupMap m = group_map(p0, p1, sv, stt, lane);  // lane = sketch
+  GroupView g;
+  g.gn = m.gn;
+  g.gc = (uint32_t)__shfl((int)m.gc, (int)s, 64);
+  g.gpre = (uint32_t)__shfl((int)m.gend, (int)s, 64) - g.gc;
+  const uint64_t at = m.src + (m.gend - m.gc);  // sketch lane's first element of the group
+  g.src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(at >> 32), (int)s, 64) << 32) |
+          (uint32_t)__shfl((int)(uint32_t)at, (int)s, 64);
+  g.fat = __ballot(m.gc > kSkCap) != 0;
+  return g;
 }
 
-// Loads the group's elements i = tid + k * kPB < gn into registers through
-// its owner map (written by group_map_write, a barrier passed since).
 template <int EW>
-__device__ __forceinline__ void group_load(const uint64_t* __restrict__ data, const uint8_t* s_own,
-                                           const uint64_t* s_src, uint32_t gn, int tid, KV (&v)[kRegPer],
-                                           uint32_t (&sl)[kRegPer]) {
+__device__ __forceinline__ void group_load(const uint64_t* __restrict__ data, const GroupView& g, uint32_t sub,
+                                           KV (&v)[kRegPer]) {
 #pragma unroll
   for (int k = 0; k < kRegPer; ++k) {
-    const uint32_t i = tid + k * kPB;
+    const uint32_t e = sub + kTPS * k;
     v[k] = KV{0, 0};
-    sl[k] = 0;
-    if (gn <= kGCap && i < gn) {
-      const uint32_t s = s_own[i];
-      sl[k] = s;
+    if (!g.fat && g.gn <= kGCap && e < g.gc) {
 #if SKS_PLACE_DIAG == 3  // diagnostics: no global loads (values synthesised from the index)
-      v[k] = KV{(s_src[s] + i) * 0x9E3779B97F4A7C15ull, 0};
+      v[k] = KV{(g.src + e) * 0x9E3779B97F4A7C15ull, 0};
 #else
-      v[k] = kv_load<EW>(data, s_src[s] + i);
+      v[k] = kv_load<EW>(data, g.src + e);
 #endif
     }
   }
@@ -469,11 +471,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
   __shared__ uint32_t s_wsum[kPB / 64];
   __shared__ uint32_t s_bcnt[1u << jc::kGLog];
   __shared__ uint32_t s_full, s_pcnt, s_gd, s_qn, s_qd;
-  // s_src[64] (group_load's source offsets) and the slice path's work stack
-  // share one array: the slice path runs after the group's loads have read it
-  __shared__ uint64_t s_aux[72];
-  uint64_t* s_src = s_aux;
-  uint32_t* s_stk = reinterpret_cast<uint32_t*>(s_aux);  // (slice, level) pairs
+  __shared__ uint32_t s_stk[2 * 72];  // slice path: (slice, level) work stack
 
   const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
   const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b);
@@ -502,47 +500,43 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
   uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(sv ? s_pos[lane] : 0u), 63);
   uint32_t maxb = 0;
   KV v[kRegPer];
-  uint32_t sl[kRegPer];
-  uint32_t gn = group_map_write(s_pos, s_pos + kTile, sv, stt, lane, wave, s_own, s_src);
-  __syncthreads();
-  group_load<EW>(data, s_own, s_src, gn, tid, v, sl);
+  const uint32_t my_s = (uint32_t)tid / kTPS, sub = (uint32_t)tid % kTPS;  // this thread's sketch
+  GroupView gv = group_view(s_pos, s_pos + kTile, sv, stt, lane, my_s);
+  group_load<EW>(data, gv, sub, v);
   LSTAMP(0);
 
   for (uint32_t j = 0; j < RG; ++j) {
     const uint32_t g = r * RG + j;
-    const uint32_t gn_j = gn;
-    // the next group's owner map, then its loads into v / nsl (in flight while
-    // this group is placed: v is in LDS by then, sl still names this group's owners)
-    uint32_t nsl[kRegPer];
+    const GroupView gj = gv;
+    const uint32_t gn_j = gj.gn;
+    // the next group's elements load into v (in flight while this group is
+    // placed; this group's values are in LDS by then)
     bool fetched = false;
-    auto map_next = [&]() {
-      gn = j + 1 < RG ? group_map_write(s_pos + (j + 1) * kTile, s_pos + (j + 2) * kTile, sv, stt, lane, wave, s_own,
-                                        s_src)
-                      : 0u;
-    };
     auto load_next = [&]() {
-      group_load<EW>(data, s_own, s_src, gn, tid, v, nsl);
+      if (j + 1 < RG) {
+        gv = group_view(s_pos + (j + 1) * kTile, s_pos + (j + 2) * kTile, sv, stt, lane, my_s);
+        group_load<EW>(data, gv, sub, v);
+      }
       fetched = true;
     };
     bool done = false;
     if (gn_j == 0) {  // an empty group: its buckets start (and end) at the cursor
       if ((uint32_t)tid < GB) boff[g * GB + tid] = cur;
       done = true;
-    } else if (gn_j <= gcap) {
+    } else if (gn_j <= gcap && !gj.fat) {
       // ---- normal path ------------------------------------------------------------------------
-      __syncthreads();  // the previous pass has read s_key / s_msk / s_tab, the loads s_own / s_src
+      __syncthreads();  // the previous pass has read s_key / s_msk / s_tab / s_bcnt
 #pragma unroll
       for (int k = 0; k < kRegPer; ++k) {  // P1
-        const uint32_t i = tid + k * kPB;
-        if (i < gn_j) {
+        const uint32_t e = sub + kTPS * k, i = gj.gpre + e;
+        if (e < gj.gc) {
           if constexpr (EW == 1) s_key[i] = v[k].lo;
           else { s_key[2 * i] = v[k].lo; s_key[2 * i + 1] = v[k].hi; }
         }
       }
-      if ((uint32_t)tid < GB) s_bcnt[tid] = 0;  // (read by every thread before the barrier above)
-      map_next();
-      __syncthreads();
+      if ((uint32_t)tid < GB) s_bcnt[tid] = 0;
       load_next();
+      __syncthreads();
       LSTAMP(1);
       // P2 (the values read back from LDS), every element's first probe issued
       // together: keys, first compare-swaps, the named elements' keys; then the
@@ -555,20 +549,21 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
       uint32_t h[kRegPer], w[kRegPer], rep[kRegPer];
 #pragma unroll
       for (int k = 0; k < kRegPer; ++k) {
-        const uint32_t i = tid + k * kPB;
+        const uint32_t e = sub + kTPS * k, i = gj.gpre + e;
         w[k] = kTFree;
         h[k] = 0;
-        if (i < gn_j) {
+        if (e < gj.gc) {
           const KV x = key_at<EW>(s_key, i);
-          h[k] = (kv_group_bucket<EW>(x, gb_log) << rlog) | (dd_slot<EW>(x) & rmask);
+          // bucket (top gb_log bits of the mix) and slot in its region (the next rlog bits)
+          h[k] = (uint32_t)(kv_mix<EW>(x) >> (64 - kTabLog));
           w[k] = atomicCAS(&s_tab[h[k]], kTFree, i);
         }
       }
 #pragma unroll
       for (int k = 0; k < kRegPer; ++k) {
-        const uint32_t i = tid + k * kPB;
+        const uint32_t e = sub + kTPS * k, i = gj.gpre + e;
         rep[k] = kTFree;
-        if (i < gn_j) {
+        if (e < gj.gc) {
           const KV x = key_at<EW>(s_key, i);
           const uint32_t rbase = h[k] & ~rmask;
           uint32_t hh = h[k] & rmask, xw = w[k], steps = 0;
@@ -584,7 +579,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
           full |= f;
           const uint32_t ri = xw == kTFree ? i : xw;
           if (CHECK && !f && !kv_eq<EW>(key_at<EW>(s_key, ri), x)) atomicAdd(&g_layout_check, 1ull);
-          atomicOr(&s_msk[ri], 1ull << sl[k]);
+          atomicOr(&s_msk[ri], 1ull << my_s);
           if (xw == kTFree) {  // the representative: its slot (freed at emit) and its place in the bucket
             const uint32_t bk = h[k] >> rlog;
             rep[k] = (bk << 12) | atomicAdd(&s_bcnt[bk], 1u);
@@ -610,7 +605,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
 #pragma unroll
         for (int k = 0; k < kRegPer; ++k) {
           if (rep[k] == kTFree) continue;
-          const uint32_t i = tid + k * kPB;
+          const uint32_t i = gj.gpre + sub + kTPS * k;
           const uint64_t o = base + cur + pre[rep[k] >> 12] + (rep[k] & 4095u);
 #if SKS_PLACE_DIAG != 4  // (diagnostics 4: no global stores)
           kv_store<EW>(out_vals, o, key_at<EW>(s_key, i));
@@ -630,12 +625,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
       }
       LSTAMP(3);
     }
-    if (!fetched) {
-      __syncthreads();  // the owner map and s_src are free
-      map_next();
-      __syncthreads();
-      load_next();
-    }
+    if (!fetched) load_next();
     if (!done) {
       // ---- bucket passes ------------------------------------------------------------------------
       const GroupMap m = group_map(s_pos + j * kTile, s_pos + (j + 1) * kTile, sv, stt, lane);
@@ -833,8 +823,6 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
       }
       LSTAMP(4);
     }
-#pragma unroll
-    for (int k = 0; k < kRegPer; ++k) sl[k] = nsl[k];
   }
   if (tid == 0) boff[B + r] = cur;
   // the largest block-bucket: one word for every workgroup; the stat only
@@ -848,6 +836,414 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
   }
 }
 
+
+// ---- u64 values (w <= 32): the dedup table holds the values themselves ---------------------
+// k_gl_place1 is k_gl_place for u64 values with the values, not element
+// indices, in a 2048-slot table of 64-bit words (one compare-swap per probe and
+// no key array: 35 KB of LDS, four workgroups per CU).  The table's empty word is
+// 0, so the value 0 (a poly-A k-mer) is kept apart as s_zero: its mix is 0, so
+// it is the first value of bucket 0 (and of the first slice of bucket 0).
+constexpr uint32_t kVLog = 11, kVT = 1u << kVLog;  // value slots
+constexpr uint32_t kVSpt = kVT / kPB;              // slots per thread in a scan emit (8)
+static_assert(kGCap <= kVT, "a normal-path group fits the value table");
+#ifndef SKS_LAYOUT_HALF_AT
+#define SKS_LAYOUT_HALF_AT 1024
+#endif
+constexpr uint32_t kHalfAt = SKS_LAYOUT_HALF_AT;   // predicted distinct values above which a group takes two halves
+static_assert(kVSpt % 2 == 0, "scan emit reads slot pairs");
+
+// Inserts v != 0 into the table region [rbase, rbase + rmask] starting at
+// slot h0: one loop exit (see dd_insert).  Returns the slot holding v, or ~0u
+// when the region is full; *claimed: this call stored v (v was new).
+__device__ __forceinline__ uint32_t vt_insert(unsigned long long* s_vt, unsigned long long v, uint32_t rbase,
+                                              uint32_t h0, uint32_t rmask, unsigned long long x, bool* claimed) {
+  uint32_t hh = h0, steps = 0;
+  for (;;) {
+    if ((x == 0ull) | (x == v) | (steps > rmask)) break;
+    hh = (hh + 1) & rmask;
+    ++steps;
+    x = atomicCAS(&s_vt[rbase + hh], 0ull, v);
+  }
+  *claimed = x == 0ull;
+  return steps > rmask ? ~0u : rbase + hh;
+}
+
+// A pass of the value table: the values whose mix starts with a prefix of
+// `lvl` bits in [q0, q0 + span).  span > 1 only at the bucket level (lvl =
+// gb_log, span a power of two); the whole table is the pass's one region.
+struct VPass {
+  uint32_t lvl, span;
+  uint64_t q0;
+};
+__device__ __forceinline__ bool vp_in(const VPass& p, uint64_t mix) {
+  const uint64_t top = p.lvl ? mix >> (64 - p.lvl) : 0ull;
+  return top - p.q0 < p.span;
+}
+template <bool CHECK>
+__global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k_gl_place1(const uint64_t* __restrict__ data,
+                                                   const uint64_t* __restrict__ starts, uint32_t count,
+                                                   uint32_t log_b, const uint32_t* __restrict__ pos,
+                                                   const uint64_t* __restrict__ bstart,
+                                                   uint64_t* __restrict__ out_vals,
+                                                   unsigned long long* __restrict__ out_masks,
+                                                   uint32_t* __restrict__ out_boff, uint32_t* __restrict__ stat,
+                                                   uint32_t gcap) {
+  __shared__ unsigned long long s_vt[kVT];  // values (0: empty)
+  __shared__ unsigned long long s_vm[kVT];  // their sketch masks
+  __shared__ uint32_t s_pos[(kMaxRG + 1) * kTile];
+  __shared__ uint32_t s_bcnt[1u << jc::kGLog];
+  __shared__ unsigned long long s_zero;       // holders of the value 0
+  __shared__ uint32_t s_full, s_sd;
+  __shared__ unsigned long long s_sq[72];     // pass stack: q0
+  __shared__ uint32_t s_sl[72];               // pass stack: lvl << 8 | log2(span)
+  __shared__ uint32_t s_w8[(1u << jc::kGLog) * (kPB / 64)];  // pass emit: per-bucket wave totals
+
+  const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
+  const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b);
+  const uint32_t RG = (1u << jc::lay_rb_log(log_b)) >> gb_log;
+  const uint32_t blk = blockIdx.x / NR, r = blockIdx.x % NR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef SKS_LAYOUT_STAMPS
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
+  const uint32_t s_end = min((uint32_t)kTile, count - kTile * blk);
+  uint32_t* boff = out_boff + (uint64_t)blk * (B + NR);
+  const uint64_t base = bstart[blk];
+  const bool sv = (uint32_t)lane < s_end;
+  const uint64_t stt = sv ? starts[kTile * blk + lane] : 0;
+  for (uint32_t q = tid; q < (RG + 1) * kTile; q += kPB) {
+    const uint32_t j = q / kTile, s = q % kTile;
+    s_pos[q] = s < s_end ? pos[(uint64_t)(kTile * blk + s) * (G + 1) + r * RG + j] : 0;
+  }
+  for (uint32_t q = tid; q < kVT / 2; q += kPB) {
+    reinterpret_cast<uint4*>(s_vt)[q] = make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4*>(s_vm)[q] = make_uint4(0, 0, 0, 0);
+  }
+  if ((uint32_t)tid < (1u << jc::kGLog)) s_bcnt[tid] = 0;
+  if (tid == 0) {
+    s_full = 0;
+    s_zero = 0;
+  }
+  __syncthreads();
+  uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(sv ? s_pos[lane] : 0u), 63);
+  uint32_t maxb = 0;
+  KV v[kRegPer];
+  const uint32_t my_s = (uint32_t)tid / kTPS, sub = (uint32_t)tid % kTPS;
+  const unsigned long long my_bit = 1ull << my_s;
+  GroupView gv = group_view(s_pos, s_pos + kTile, sv, stt, lane, my_s);
+  group_load<1>(data, gv, sub, v);
+  uint32_t dshare = 1u << 16;  // distinct / raw of the region's last placed group (16.16)
+
+  // emit of a pass (thread t reads slots [8 t, 8 t + 8)): the pass's table holds
+  // the values of buckets [q0, q0 + span) (a slice of one bucket when span = 1)
+  // in one region; each thread counts its values per bucket, a wave scan per
+  // bucket and the waves' totals place them bucket by bucket (any order within
+  // a bucket), the value 0 first when the pass holds prefix 0
+  auto emit_pass1 = [&](const VPass& p, uint32_t g, uint32_t first) {
+    constexpr uint32_t NB = 1u << jc::kGLog;
+    unsigned long long wv[kVSpt];
+#pragma unroll
+    for (int q = 0; q < (int)kVSpt / 2; ++q) {
+      const ulonglong2 x = reinterpret_cast<const ulonglong2*>(s_vt)[tid * (kVSpt / 2) + q];
+      wv[2 * q] = x.x;
+      wv[2 * q + 1] = x.y;
+    }
+    uint32_t bq[kVSpt], cnt[NB];
+#pragma unroll
+    for (uint32_t b = 0; b < NB; ++b) cnt[b] = 0;
+#pragma unroll
+    for (int k = 0; k < (int)kVSpt; ++k) {
+      const uint64_t mx = kv_mix<1>(KV{wv[k], 0});
+      bq[k] = p.span > 1 ? (uint32_t)((mx >> (64 - gb_log)) - p.q0) : 0u;
+#pragma unroll
+      for (uint32_t b = 0; b < NB; ++b) cnt[b] += (wv[k] != 0ull && bq[k] == b) ? 1u : 0u;
+    }
+    uint32_t off[NB];
+#pragma unroll
+    for (uint32_t b = 0; b < NB; ++b) {
+      const uint32_t incl = wave_scan(cnt[b]);
+      off[b] = incl - cnt[b];
+      if (lane == 63) s_w8[b * (kPB / 64) + wave] = incl;
+    }
+    __syncthreads();
+    const uint32_t zero = (p.q0 == 0 && s_zero) ? 1u : 0u;
+    uint32_t start = zero, total = zero;
+#pragma unroll
+    for (uint32_t b = 0; b < NB; ++b) {
+      uint32_t tb = 0, before = 0;
+#pragma unroll
+      for (int w = 0; w < kPB / 64; ++w) {
+        const uint32_t x = s_w8[b * (kPB / 64) + w];
+        tb += x;
+        before += w < wave ? x : 0u;
+      }
+      off[b] += start + before;
+      if (p.span > 1 && (uint32_t)tid == b && b < p.span)
+        boff[g * GB + (uint32_t)p.q0 + b] = cur + (b == 0 ? 0u : start);
+      maxb = max(maxb, tb + (b == 0 ? zero : 0u));
+      start += tb;
+      total += tb;
+    }
+    if (p.span == 1 && first && tid == 0) boff[g * GB + (uint32_t)(p.q0 >> (p.lvl - gb_log))] = cur;
+#pragma unroll
+    for (int k = 0; k < (int)kVSpt; ++k) {
+      if (wv[k] == 0ull) continue;
+      uint32_t d = 0;
+#pragma unroll
+      for (uint32_t b = 0; b < NB; ++b)
+        if (bq[k] == b) d = off[b]++;
+      const uint32_t slot = tid * kVSpt + k;
+      const uint64_t o = base + cur + d;
+      out_vals[o] = wv[k];
+      out_masks[o] = s_vm[slot];
+      s_vt[slot] = 0ull;
+      s_vm[slot] = 0ull;
+    }
+    if (tid == 0 && zero) {
+      out_vals[base + cur] = 0ull;
+      out_masks[base + cur] = s_zero;
+    }
+    cur += total;
+    __syncthreads();  // every thread has read s_zero / s_w8
+    if (tid == 0 && zero) s_zero = 0;
+  };
+
+  for (uint32_t j = 0; j < RG; ++j) {
+    const uint32_t g = r * RG + j;
+    const GroupView gj = gv;
+    const uint32_t gn_j = gj.gn;
+    bool done = false, fetched = false;
+    if (gn_j == 0) {  // an empty group: its buckets start (and end) at the cursor
+      if ((uint32_t)tid < GB) boff[g * GB + tid] = cur;
+      done = true;
+    } else if (gn_j <= gcap && !gj.fat) {
+      // ---- normal path: the group's buckets from registers, in one or two passes ---------------
+      // every element's first compare-swap issued together, then the (rare) rest of
+      // the chains; a representative (the element that stored its value) takes the
+      // next place of its bucket (entries contiguous per bucket, any order within).
+      // The whole table is one region (placement goes by the bucket counters, not by
+      // slot order); a group predicted to hold more than kHalfAt distinct values
+      // (raw count x the region's running distinct share) is placed in two halves
+      // of its buckets, keeping the table at most about half full (linear probing
+      // at a load near 1 walks long chains: unrelated genomes' largest groups).
+      const uint32_t nh = (GB > 1 && (uint64_t)gn_j * dshare > ((uint64_t)kHalfAt << 16)) ? 2u : 1u;
+      const uint32_t bn = GB / nh;
+      uint32_t dsum = 0;
+      for (uint32_t hf = 0; hf < nh; ++hf) {
+        const uint32_t blo = hf * bn;
+        __syncthreads();  // the previous emit has freed its slots and reset s_bcnt / s_zero
+        uint32_t h[kRegPer], bk[kRegPer];
+        unsigned long long x0[kRegPer];
+#pragma unroll
+        for (int k = 0; k < kRegPer; ++k) {
+          const uint32_t e = sub + kTPS * k;
+          const uint64_t m = kv_mix<1>(v[k]);
+          x0[k] = ~0ull;
+          bk[k] = gb_log ? (uint32_t)(m >> (64 - gb_log)) : 0u;
+          h[k] = (uint32_t)((gb_log ? m << gb_log : m) >> (64 - kVLog));  // (the bits after the bucket)
+          if (e < gj.gc && v[k].lo != 0ull && bk[k] - blo < bn) x0[k] = atomicCAS(&s_vt[h[k]], 0ull, v[k].lo);
+        }
+        bool full = false;
+        uint32_t rep[kRegPer];
+#pragma unroll
+        for (int k = 0; k < kRegPer; ++k) {
+          const uint32_t e = sub + kTPS * k;
+          rep[k] = kTFree;
+          if (e < gj.gc) {
+            if (v[k].lo == 0ull) {  // (bucket 0: the first half)
+              if (hf == 0) atomicOr(&s_zero, my_bit);
+              continue;
+            }
+            if (bk[k] - blo >= bn) continue;
+            bool claimed;
+            const uint32_t slot = vt_insert(s_vt, v[k].lo, 0u, h[k], kVT - 1, x0[k], &claimed);
+            if (slot == ~0u) {  // (unreachable: at most gcap <= kVT values)
+              full = true;
+              continue;
+            }
+            if (CHECK && s_vt[slot] != v[k].lo) atomicAdd(&g_layout_check, 1ull);
+            atomicOr(&s_vm[slot], my_bit);
+            if (claimed) {
+              rep[k] = (bk[k] << 12) | atomicAdd(&s_bcnt[bk[k]], 1u);
+              h[k] = slot;
+            }
+          }
+        }
+        if (full) atomicAdd(stat + 1, 1u);  // the layout is invalid (the caller retries)
+        LSTAMP(2);
+        if (hf + 1 == nh) {  // the next group's loads (in flight during the emit)
+          if (j + 1 < RG) {
+            gv = group_view(s_pos + (j + 1) * kTile, s_pos + (j + 2) * kTile, sv, stt, lane, my_s);
+            group_load<1>(data, gv, sub, v);
+          }
+          fetched = true;
+        }
+        __syncthreads();
+        const uint32_t zero = (hf == 0 && s_zero) ? 1u : 0u;  // the value 0: first in bucket 0
+        uint32_t pre[1u << jc::kGLog], tot = zero;
+#pragma unroll
+        for (uint32_t b = 0; b < (1u << jc::kGLog); ++b) {
+          const uint32_t c = b - blo < bn ? s_bcnt[b] : 0u;
+          pre[b] = tot;
+          tot += c;
+          maxb = max(maxb, c + (b == 0 ? zero : 0u));
+        }
+        if ((uint32_t)tid < bn) boff[g * GB + blo + tid] = cur + (tid == 0 ? 0u : pre[blo + tid]);
+#pragma unroll
+        for (int k = 0; k < kRegPer; ++k) {
+          if (rep[k] == kTFree) continue;
+          const uint64_t o = base + cur + pre[rep[k] >> 12] + (rep[k] & 4095u);
+#if SKS_PLACE_DIAG != 4
+          out_vals[o] = s_vt[h[k]];
+          out_masks[o] = s_vm[h[k]];
+#endif
+          s_vt[h[k]] = 0ull;
+          s_vm[h[k]] = 0ull;
+        }
+        if (tid == 0 && zero) {
+          out_vals[base + cur] = 0ull;
+          out_masks[base + cur] = s_zero;
+        }
+        cur += tot;
+        dsum += tot;
+        LSTAMP(3);
+        __syncthreads();  // counts and s_zero read; the table is free again
+        if ((uint32_t)tid < GB) s_bcnt[tid] = 0;
+        if (tid == 0) s_zero = 0;
+      }
+      dshare = (uint32_t)(((uint64_t)dsum << 16) / gn_j);
+      done = true;
+    }
+    if (!fetched && j + 1 < RG) {
+      gv = group_view(s_pos + (j + 1) * kTile, s_pos + (j + 2) * kTile, sv, stt, lane, my_s);
+      group_load<1>(data, gv, sub, v);
+    }
+    if (!done) {
+      // ---- passes: prefixes of the values' mixes, re-read from the sketches --------------------
+      // (a group above gcap raw elements, or with a sketch above kSkCap elements):
+      // the buckets in parts of about 1536 elements; a pass whose table overflows
+      // (more than 2048 distinct values) is split (buckets into halves, then a
+      // bucket into hash slices), depth first, so entries come out in bucket and
+      // slice order
+      const GroupMap m = group_map(s_pos + j * kTile, s_pos + (j + 1) * kTile, sv, stt, lane);
+#ifdef SKS_LAYOUT_STAMPS
+      if (tid == 0) {
+        atomicAdd(&g_layout_stamps[8], 1ull);
+        atomicAdd(&g_layout_stamps[gj.fat ? 5 : gn_j > gcap ? 6 : 7], 1ull);
+      }
+#endif
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t parts = 1;  // predicted distinct values (raw x the running distinct share) per part <= 1536
+        while (parts < GB && (uint64_t)gn_j * dshare > (1536ull << 16) * parts) parts <<= 1;
+        const uint32_t sp_log = gb_log - (31 - __builtin_clz(parts));  // log2(GB / parts)
+        for (uint32_t q = 0; q < parts; ++q) {  // rightmost first: the leftmost is on top
+          s_sq[q] = (uint64_t)(parts - 1 - q) << sp_log;
+          s_sl[q] = (gb_log << 8) | sp_log;
+        }
+        s_sd = parts;
+      }
+      __syncthreads();
+      uint32_t bk_start = cur;
+      const uint32_t cur0 = cur;
+      for (;;) {
+        const uint32_t depth = s_sd;
+        if (depth == 0) break;
+        VPass p;
+        p.q0 = s_sq[depth - 1];
+        p.lvl = s_sl[depth - 1] >> 8;
+        const uint32_t sl2 = s_sl[depth - 1] & 255u;
+        p.span = 1u << sl2;
+        __syncthreads();
+        if (tid == 0) s_sd = depth - 1;
+        bool full = false;
+        for (uint32_t c0 = (uint32_t)wave * 64; c0 < m.gn; c0 += kPB * kPassU) {
+          KV x[kPassU];
+          uint32_t o[kPassU];
+#pragma unroll
+          for (int u = 0; u < kPassU; ++u) {
+            const uint32_t b = c0 + u * kPB;
+            o[u] = 0;
+            x[u] = KV{0, 0};
+            if (b < m.gn) {
+              const uint64_t at = elem_at(m, b, lane, &o[u]);
+              if (b + (uint32_t)lane < m.gn) x[u] = kv_load<1>(data, at);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kPassU; ++u) {
+            if (c0 + u * kPB + (uint32_t)lane >= m.gn) continue;
+            const uint64_t mx = kv_mix<1>(x[u]);
+            if (!vp_in(p, mx)) continue;
+            if (x[u].lo == 0ull) {
+              atomicOr(&s_zero, 1ull << o[u]);
+              continue;
+            }
+            const uint32_t h0 = (uint32_t)((p.lvl ? mx << p.lvl : mx) >> (64 - kVLog));
+            bool claimed;
+            const uint32_t slot = vt_insert(s_vt, x[u].lo, 0u, h0, kVT - 1, atomicCAS(&s_vt[h0], 0ull, x[u].lo),
+                                            &claimed);
+            if (slot == ~0u) {
+              full = true;
+              continue;
+            }
+            if (CHECK && s_vt[slot] != x[u].lo) atomicAdd(&g_layout_check, 1ull);
+            atomicOr(&s_vm[slot], 1ull << o[u]);
+          }
+        }
+        if (full) s_full = 1;
+        __syncthreads();
+        if (s_full) {  // split the pass: halves of its buckets, or two hash slices of its bucket
+          for (uint32_t q = tid; q < kVT / 2; q += kPB) {
+            reinterpret_cast<uint4*>(s_vt)[q] = make_uint4(0, 0, 0, 0);
+            reinterpret_cast<uint4*>(s_vm)[q] = make_uint4(0, 0, 0, 0);
+          }
+          __syncthreads();
+          if (tid == 0) {
+#ifdef SKS_LAYOUT_STAMPS
+            atomicAdd(&g_layout_stamps[9], 1ull);
+#endif
+            s_full = 0;
+            s_zero = 0;
+            const uint32_t d = s_sd;
+            if (p.span > 1) {
+              const uint32_t h2 = sl2 - 1;
+              s_sq[d] = p.q0 + (p.span >> 1);
+              s_sl[d] = (p.lvl << 8) | h2;
+              s_sq[d + 1] = p.q0;
+              s_sl[d + 1] = (p.lvl << 8) | h2;
+            } else {
+              s_sq[d] = 2 * p.q0 + 1;
+              s_sl[d] = (p.lvl + 1) << 8;
+              s_sq[d + 1] = 2 * p.q0;
+              s_sl[d + 1] = (p.lvl + 1) << 8;
+            }
+            s_sd = d + 2;
+          }
+          __syncthreads();
+          continue;
+        }
+        // the first slice of a bucket starts the bucket
+        uint32_t first = 0;
+        if (p.span == 1) {
+          const uint32_t sh = p.lvl - gb_log;
+          first = (p.q0 & ((1ull << sh) - 1)) == 0 ? 1u : 0u;
+          if (first) bk_start = cur;
+        }
+        emit_pass1(p, g, first);
+        if (p.span == 1) maxb = max(maxb, cur - bk_start);
+      }
+      dshare = (uint32_t)(((uint64_t)(cur - cur0) << 16) / gn_j);
+    }
+  }
+  if (tid == 0) boff[B + r] = cur;
+  if (wave == 0) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxb = max(maxb, (uint32_t)__shfl_xor(maxb, o, 64));
+    if (lane == 0 && maxb && maxb > __hip_atomic_load(stat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(stat, maxb);
+  }
+}
 
 }  // namespace
 
@@ -911,10 +1307,10 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
                        bounds_tmp, nb_bounds, out_bstart);
     hipLaunchKernelGGL(k_gl_pos<1>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
     if (check)
-      hipLaunchKernelGGL((k_gl_place<1, true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
+      hipLaunchKernelGGL((k_gl_place1<true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
                          out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
     else
-      hipLaunchKernelGGL((k_gl_place<1, false>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
+      hipLaunchKernelGGL((k_gl_place1<false>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
                          out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
   } else {
     hipLaunchKernelGGL(k_gl_prep<2>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
@@ -936,8 +1332,9 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_layout_stamps), z, sizeof z);
     const double wgs = (double)grid_place.x;
     fprintf(stderr, "[k_gl_place stamps] cycles per workgroup: setup+first load %.0f P1+next map+loads %.0f P2 %.0f "
-            "P3+P4 %.0f bucket passes / slow %.0f | slow groups %llu (%.0f workgroups)\n", h[0] / wgs,
-            h[1] / wgs, h[2] / wgs, h[3] / wgs, h[4] / wgs, h[8], wgs);
+            "P3+P4 %.0f bucket passes / slow %.0f | groups in passes %llu (fat %llu, above cap %llu, full %llu), "
+            "pass splits %llu (%.0f workgroups)\n",
+            h[0] / wgs, h[1] / wgs, h[2] / wgs, h[3] / wgs, h[4] / wgs, h[8], h[5], h[6], h[7], h[9], wgs);
   }
 #endif
   return hipGetLastError();

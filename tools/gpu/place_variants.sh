@@ -13,7 +13,7 @@ import csv, glob, re, sys
 f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
     m = re.search(r"(k_\w+)", r["Name"])
-    if m and m.group(1) in ("k_gl_place", "k_join", "k_gl_pos"):
+    if m and m.group(1).startswith(("k_gl_place", "k_join", "k_gl_pos", "k_gl_prep")):
         print(sys.argv[2], sys.argv[3], m.group(1), round(float(r["AverageNs"]) / 1e3, 1), "us")
 PY
     rm -rf $O/t_${tag}_$m

@@ -41,17 +41,24 @@ def main():
     torch.cuda.synchronize()
     bounds = b.cpu().numpy().view(np.uint64)
     sk = [ss.sketch(i)[:, 0] for i in range(n)]
-    raw, dist = [], []
+    raw, dist, fat = [], [], []
     for b0 in range(0, n, 64):
         blk = sk[b0:b0 + 64]
         gi = [np.searchsorted(bounds[1:G], s, side="right") for s in blk]
         allv = np.concatenate(blk)
         allg = np.concatenate(gi)
+        per = np.stack([np.bincount(x, minlength=G) for x in gi])  # [sketch, group]
         for g in range(G):
             v = allv[allg == g]
             raw.append(len(v))
             dist.append(len(np.unique(v)))
-    raw, dist = np.array(raw), np.array(dist)
+            fat.append(int(per[:, g].max()))
+    raw, dist, fat = np.array(raw), np.array(dist), np.array(fat)
+    top = np.argsort(raw)[-8:]
+    print("largest groups (block, group, raw, distinct, largest per-sketch count):",
+          [(int(t // G), int(t % G), int(raw[t]), int(dist[t]), int(fat[t])) for t in top])
+    print("groups with a sketch above 48:", int((fat > 48).sum()), "first few:",
+          [(int(t // G), int(t % G), int(raw[t]), int(fat[t])) for t in np.nonzero(fat > 48)[0][:8]])
     print(f"{mode} n={n} log_b={log_b} G={G}: raw per group mean {raw.mean():.0f} max {raw.max()} "
           f"p99 {np.percentile(raw, 99):.0f} (> 2048: {(raw > 2048).sum()} of {len(raw)}); distinct mean "
           f"{dist.mean():.0f} max {dist.max()}; dedup {raw.sum() / dist.sum():.2f}x", flush=True)
