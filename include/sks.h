@@ -340,6 +340,12 @@ int sks_sketch_set_export_csr(const sks_sketch_set* set, uint64_t* d_data, uint3
  * containments.  Queued on the context stream. */
 int sks_ani_matrix(sks_ctx* ctx, const int32_t* d_counts, uint32_t n, int kmer_num_ones, double* d_cont,
                    double* d_ani);
+/* Rows [row_begin, row_end) of sks_ani_matrix (same addressing: d_ani[i * n + j]),
+ * so a caller can convert and copy out the rows an all-pairs call has finished
+ * (rows of tile rows [0, I) are final once those tile rows are counted) while
+ * later tiles are still being counted. */
+int sks_ani_rows(sks_ctx* ctx, const int32_t* d_counts, uint32_t n, uint32_t row_begin, uint32_t row_end,
+                 int kmer_num_ones, double* d_cont, double* d_ani);
 /* Packed tiles (d_packed [n_tiles][64][64] of tiles d_tiles[2t] = I,
  * d_tiles[2t + 1] = J, as sks_intersect_layout_tiles writes them):
  * d_ani[t][0][r][c] = ANI of (64 I + r, 64 J + c), d_ani[t][1][c][r] = ANI of

@@ -28,11 +28,13 @@ __device__ __forceinline__ double ani_of(int32_t inter, int32_t size_first, doub
   return c <= 0.0 ? 0.0 : pow(c, inv_k);
 }
 
-// ani[i * n + j] for the dense n x n count matrix; |S_i| = counts[i][i]
-__global__ __launch_bounds__(kAB) void k_ani_matrix(const int32_t* __restrict__ counts, uint32_t n, double inv_k,
+// ani[i * n + j] for rows [row_begin, row_end) of the dense n x n count
+// matrix; |S_i| = counts[i][i]
+__global__ __launch_bounds__(kAB) void k_ani_matrix(const int32_t* __restrict__ counts, uint32_t n,
+                                                    uint32_t row_begin, uint32_t row_end, double inv_k,
                                                     double* __restrict__ cont, double* __restrict__ ani) {
-  const uint64_t idx = (uint64_t)blockIdx.x * kAB + threadIdx.x;
-  if (idx >= (uint64_t)n * n) return;
+  const uint64_t idx = (uint64_t)row_begin * n + (uint64_t)blockIdx.x * kAB + threadIdx.x;
+  if (idx >= (uint64_t)row_end * n) return;
   const uint32_t i = (uint32_t)(idx / n);
   double c;
   const double a = ani_of(counts[idx], counts[(uint64_t)i * n + i], inv_k, &c);
@@ -60,13 +62,13 @@ __global__ __launch_bounds__(kAB) void k_ani_tiles(const int32_t* __restrict__ p
 
 }  // namespace
 
-hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, int kmer_num_ones, double* cont, double* ani,
-                             hipStream_t s) {
-  const uint64_t cells = (uint64_t)n * n;
-  if (!cells) return hipSuccess;
+hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, uint32_t row_begin, uint32_t row_end,
+                             int kmer_num_ones, double* cont, double* ani, hipStream_t s) {
+  if (row_end > n || row_begin >= row_end) return hipSuccess;
+  const uint64_t cells = (uint64_t)(row_end - row_begin) * n;
   const double inv_k = ((double)1.0) / ((double)kmer_num_ones);
-  hipLaunchKernelGGL(k_ani_matrix, dim3((unsigned)((cells + kAB - 1) / kAB)), dim3(kAB), 0, s, counts, n, inv_k,
-                     cont, ani);
+  hipLaunchKernelGGL(k_ani_matrix, dim3((unsigned)((cells + kAB - 1) / kAB)), dim3(kAB), 0, s, counts, n, row_begin,
+                     row_end, inv_k, cont, ani);
   return hipGetLastError();
 }
 

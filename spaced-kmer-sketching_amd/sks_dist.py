@@ -345,7 +345,27 @@ class JoinResult:
         self.tiles = self.counts = self.ani = self.matrix = None
 
 
-def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None):
+def _row_parts(nb, parts=6):
+    """Tile-row ranges [I0, I1) of an nb x nb upper triangle with about
+    T / parts tiles each (the early tile rows hold the most tiles)."""
+    T = nb * (nb + 1) // 2
+    target = max(1, -(-T // parts))
+    out, i0, acc = [], 0, 0
+    for i in range(nb):
+        acc += nb - i
+        if acc >= target or i == nb - 1:
+            out.append((i0, i + 1))
+            i0, acc = i + 1, 0
+    return out
+
+
+def _tiles_before(I, nb):
+    """Upper-triangle tiles (row-major) before tile row I."""
+    return I * nb - I * (I - 1) // 2
+
+
+def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None,
+                    ani_host=None):
     """All-vs-all intersection counts (kmer_set.cpp:143-184 over the
     generate_all_pairs_from_vector list, generators.hpp:44-58), and ANI when
     ani_ones (the k of binomial_estimator) is given.
@@ -373,11 +393,33 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     if solo:
         lay = ops.build(mine, log_b, None, "own")
         out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+        res.counts = res.matrix = out
+        if ani_ones is not None and ani_host is not None and n_genomes and hasattr(ops, "count_range"):
+            # rows of tile rows [0, I) are final once those tile rows are counted
+            # (the row-major upper triangle; the mirror halves come from earlier
+            # rows): each part's ANI rows are computed and copied into ani_host on a
+            # copy stream while the next part's tiles are counted
+            n, nb = n_genomes, (n_genomes + TILE - 1) // TILE
+            res.ani = torch.empty((n, n), dtype=torch.float64, device=device)
+            copy = _copy_stream(device)
+            flat_d, flat_h = res.ani.view(-1), ani_host.view(-1)
+            for I0, I1 in _row_parts(nb):
+                ops.count_range(n, log_b, lay, _tiles_before(I0, nb), _tiles_before(I1, nb), out)
+                r0, r1 = I0 * TILE, min(n, I1 * TILE)
+                ops.ani_rows(out, n, r0, r1, ani_ones, res.ani)
+                ev = torch.cuda.Event()
+                ev.record()
+                copy.wait_event(ev)
+                with torch.cuda.stream(copy):
+                    flat_h[r0 * n:r1 * n].copy_(flat_d[r0 * n:r1 * n], non_blocking=True)
+            torch.cuda.current_stream().wait_stream(copy)
+            return res
         if n_genomes:
             ops.count(n_genomes, log_b, lay, 0, lay, 0, None, out)
-        res.counts = res.matrix = out
         if ani_ones is not None:
             res.ani = ops.ani_matrix(out, n_genomes, ani_ones)
+            if ani_host is not None:
+                ani_host.view(-1).copy_(res.ani.view(-1), non_blocking=True)
         return res
     # rank 0's group bounds, shared by every layout (blocks of different ranks
     # are joined bucket by bucket)
@@ -423,6 +465,20 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
     res.matrix = place_tiles(out, tiles, got, n_genomes)
     return res
+
+
+_COPY_STREAMS = {}
+
+
+def _copy_stream(device):
+    """A high-priority side stream per device for device-to-host copies (HIP maps
+    streams onto four hardware queues; a normal-priority copy stream can land on
+    the compute stream's queue and wait behind its kernels: DESIGN.md §6)."""
+    key = str(device)
+    if key not in _COPY_STREAMS:
+        lo, hi = torch.cuda.Stream.priority_range()
+        _COPY_STREAMS[key] = torch.cuda.Stream(device=device, priority=hi)
+    return _COPY_STREAMS[key]
 
 
 def _max_over(x, world, device):
@@ -534,6 +590,19 @@ class GpuJoinOps:
             self.ctx.intersect_layout_pair_tiles(n, log_b, [t.data_ptr() for t in rows], r_blk0,
                                                  [t.data_ptr() for t in cols], c_blk0, tl.data_ptr(), 0,
                                                  tl.shape[0], out.dim() == 3, out.data_ptr(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+
+    def count_range(self, n, log_b, lay, tile_begin, tile_end, out):
+        """Upper-triangle tiles [tile_begin, tile_end) of one layout, counts added
+        to the dense n x n matrix out (both halves)."""
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in lay), 0, 0, tile_begin, tile_end,
+                                        False, out.data_ptr(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+
+    def ani_rows(self, counts, n, r0, r1, k, ani):
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.ani_rows(counts.data_ptr(), n, r0, r1, k, ani.data_ptr())
         _torch_waits_for_ctx(self.ctx)
 
     def ani_matrix(self, counts, n, k):

@@ -62,7 +62,7 @@ EXPORTED = [
     "sks_intersect_layout_tiles",
     "sks_join_layout_bounds", "sks_join_layout_groups", "sks_join_layout_boff_words",
     "sks_ctx_set_join_check", "sks_ctx_join_check_violations", "sks_intersect_layout_pair_tiles",
-    "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_tiles",
+    "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_rows", "sks_ani_tiles",
 ]
 
 _lib = None
@@ -137,6 +137,7 @@ def lib():
                                                   C.c_uint64, C.c_int, vp]
     L.sks_sketch_set_export_csr.argtypes = [vp, vp, vp]
     L.sks_ani_matrix.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, vp]
+    L.sks_ani_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, vp, vp]
     L.sks_ani_tiles.argtypes = [vp, vp, vp, C.c_uint64, C.c_uint32, vp, C.c_int, vp]
     L.sks_ctx_set_join_check.argtypes = [vp, C.c_int]
     L.sks_ctx_join_check_violations.argtypes = [vp, u64p]
@@ -385,6 +386,11 @@ class Context:
         """sks_ani_matrix (device pointers): ANI of every ordered pair of the n x n counts."""
         check(lib().sks_ani_matrix(self.h, C.c_void_p(counts), n, kmer_num_ones,
                                    C.c_void_p(cont) if cont else None, C.c_void_p(ani)))
+
+    def ani_rows(self, counts, n, row_begin, row_end, kmer_num_ones, ani, cont=None):
+        """sks_ani_rows (device pointers): rows [row_begin, row_end) of ani_matrix."""
+        check(lib().sks_ani_rows(self.h, C.c_void_p(counts), n, row_begin, row_end, kmer_num_ones,
+                                 C.c_void_p(cont) if cont else None, C.c_void_p(ani)))
 
     def ani_tiles(self, packed, tiles, n_tiles, n, sizes, kmer_num_ones, ani):
         """sks_ani_tiles (device pointers): both orientations of every pair of packed tiles."""
