@@ -447,3 +447,22 @@ def test_tile_plan_partitions_upper_triangle(n, world):
             sks_dist.block_shard(n, world, r)[1] == sks_dist.block_shard(n, world, r)[0] * 64]
     if full:  # ranks holding whole block ranges get near-equal shares
         assert max(full) - min(full) <= world
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3, 5, 16, 17, 40])
+def test_row_parts_finish_rows(nb):
+    """The pipelined one-rank ANI (sks_dist.all_vs_all_join ani_host) converts
+    and copies the rows of tile rows [I0, I1) after counting upper-triangle
+    tiles [tiles_before(I0), tiles_before(I1)): the parts cover every tile
+    once, in order, and when a part ends every tile a finished row needs —
+    (I, J) for J >= I and the mirrored (J, I) for J < I — has been counted."""
+    parts = sks_dist._row_parts(nb)
+    assert parts[0][0] == 0 and parts[-1][1] == nb
+    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+    order = [(i, j) for i in range(nb) for j in range(i, nb)]  # intersect.hip sym_tile order
+    assert sks_dist._tiles_before(nb, nb) == len(order)
+    for I0, I1 in parts:
+        done = set(order[:sks_dist._tiles_before(I1, nb)])
+        for I in range(I0, I1):
+            for J in range(nb):
+                assert (min(I, J), max(I, J)) in done, (I0, I1, I, J)
