@@ -9,7 +9,7 @@ Headline (`value`): k-mers hashed/s, whole job, on config 3 of BASELINE.json
 N-runs per contig, spaced seed w=31/k=21 mask seed 0, FracMinHash 1/1000).
 A step = one complete sketch build of that genome (fused scan kernel + sort +
 unique, host syncs included) with the bytes already resident in HBM. The timed
-steps run with --inflight (default 2) builds in flight, one context and HIP
+steps run with --inflight (default 3) builds in flight, one context and HIP
 stream each, so one build's post-processing overlaps the next build's scan; a
 serial pass (`ms_per_step_serial`) and the scan kernel's own time are reported
 beside it.
@@ -25,7 +25,9 @@ sketches are broadcast by their owner over RCCL (torch.distributed "nccl") and
 each rank joins its blocks with a source's as they land (a fixed plan splits
 the upper-triangle 64x64 tiles); containment and ANI are computed on the
 device per tile and copied to the rank's host memory.  At N = 1 the counts go
-straight into the n x n matrix and the ANI matrix (8 MB) is read back.
+straight into the n x n matrix and the ANI matrix (8 MB) is copied to host
+memory.  `pairs_wide`:
+the same leg at w = 45 / k = 30 (128-bit k-mers).
 
 `cpu_baseline`: the reference-faithful CPU port (oracle/ref_port.cpp, see
 BASELINE.md) timed on this box's host cores on a bounded sample of the same
@@ -732,12 +734,15 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
         nonlocal host_ani
         if world == 1 and with_ani and host_ani is None:
             host_ani = torch.empty(C4_GENOMES * C4_GENOMES, dtype=torch.float64, pin_memory=True)
-        # one rank: the ANI rows are computed and copied to host memory part by
-        # part while later tile rows are counted (sks_dist all_vs_all_join)
+        # one rank: the dense ANI matrix is computed after the counts and copied to
+        # host memory in one piece (the tile-row pipelined form, ani_host with
+        # pipelined=True, measured slower: DESIGN.md §6)
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss, ew=ops.ew), ops,
                                        sksffi.join_layout_log_b, device="cuda", dst=None,
                                        ani_ones=ones if with_ani else None,
-                                       ani_host=host_ani if world == 1 and with_ani else None)
+                                       ani_host=host_ani if world == 1 and with_ani else None,
+                                       pipelined=os.environ.get("SKS_BENCH_PIPELINED_ANI") == "1",
+                                       max_size=int(ss.sizes().max()) if ss is not None and ss.n else None)
         if with_ani and world > 1:  # this rank's ANI tiles, both orientations
             flat = res.ani.reshape(-1)
             if host_ani is None or host_ani.numel() != flat.numel():

@@ -13,6 +13,7 @@
 
 #include <cstdint>
 
+#include "sks_ani.hpp"
 #include "sks_internal.hpp"
 
 namespace sks {
@@ -62,8 +63,13 @@ __global__ __launch_bounds__(kAB) void k_ani_tiles(const int32_t* __restrict__ p
 
 }  // namespace
 
-hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, uint32_t row_begin, uint32_t row_end,
-                             int kmer_num_ones, double* cont, double* ani, hipStream_t s) {
+hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, int kmer_num_ones, double* cont, double* ani,
+                             hipStream_t s) {
+  return launch_ani_rows(counts, n, 0, n, kmer_num_ones, cont, ani, s);
+}
+
+hipError_t launch_ani_rows(const int32_t* counts, uint32_t n, uint32_t row_begin, uint32_t row_end,
+                           int kmer_num_ones, double* cont, double* ani, hipStream_t s) {
   if (row_end > n || row_begin >= row_end) return hipSuccess;
   const uint64_t cells = (uint64_t)(row_end - row_begin) * n;
   const double inv_k = ((double)1.0) / ((double)kmer_num_ones);

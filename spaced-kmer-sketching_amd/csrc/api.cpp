@@ -16,6 +16,7 @@
 #include "sks.h"
 #include "sks_api_internal.hpp"
 #include "sks_hash.hpp"
+#include "sks_ani.hpp"
 #include "sks_internal.hpp"
 
 namespace sks {
@@ -1629,7 +1630,7 @@ int sks_ani_matrix(sks_ctx* c, const int32_t* d_counts, uint32_t n, int kmer_num
   if (kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_ani_matrix: kmer_num_ones must be positive");
   if (n && (!d_counts || !d_ani)) return sks::fail(SKS_E_ARG, "sks_ani_matrix: null argument");
   DeviceGuard g(c->device);
-  SKS_HIP(sks::launch_ani_matrix(d_counts, n, 0, n, kmer_num_ones, d_cont, d_ani, c->stream));
+  SKS_HIP(sks::launch_ani_matrix(d_counts, n, kmer_num_ones, d_cont, d_ani, c->stream));
   return SKS_OK;
 }
 
@@ -1640,7 +1641,7 @@ int sks_ani_rows(sks_ctx* c, const int32_t* d_counts, uint32_t n, uint32_t row_b
   if (row_begin > row_end || row_end > n) return sks::fail(SKS_E_ARG, "sks_ani_rows: bad row range");
   if (row_end > row_begin && (!d_counts || !d_ani)) return sks::fail(SKS_E_ARG, "sks_ani_rows: null argument");
   DeviceGuard g(c->device);
-  SKS_HIP(sks::launch_ani_matrix(d_counts, n, row_begin, row_end, kmer_num_ones, d_cont, d_ani, c->stream));
+  SKS_HIP(sks::launch_ani_rows(d_counts, n, row_begin, row_end, kmer_num_ones, d_cont, d_ani, c->stream));
   return SKS_OK;
 }
 

@@ -204,10 +204,9 @@ __global__ __launch_bounds__(kPT) void k_gl_prep(const uint64_t* __restrict__ da
 // pos[i][g] = first element of sketch i in value group g (lower bound of
 // bounds[g]; pos[i][0] = 0, pos[i][G] = size).  A workgroup per sketch stages
 // every kPosStride-th element in LDS with one coalesced pass, and a thread per
-// bound searches that sample and then loads the (at most 7) elements between
-// the two samples it falls between, together (a stride-8 sample touches every
-// 64-B line of a u64 sketch, so the launch is bound by reading the sketches
-// once).  A sketch above kPosSamples * stride
+// bound searches that sample and then the one cache line it points at (a
+// stride-8 sample touches every 64-B line of a u64 sketch, so the launch is
+// bound by reading the sketches once).  A sketch above kPosSamples * stride
 // elements samples with a larger stride.
 constexpr uint32_t kPosStride = 8, kPosSamples = 2048;
 template <int EW>
@@ -239,19 +238,9 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
       if (kv_lt<EW>(kv_load<EW>(s_smp, mid), x)) lo = mid + 1; else hi = mid;
     }
     uint32_t a = lo ? (lo - 1) * stride + 1 : 0, e = min(sz, lo * stride);
-    if (stride == kPosStride) {
-      // at most 7 elements between two samples: loaded together (one round trip),
-      // the lower bound is a plus those below x
-      uint32_t c = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < kPosStride - 1; ++q)
-        if (a + q < e) c += kv_lt<EW>(kv_load<EW>(data, st + a + q), x) ? 1u : 0u;
-      a += c;
-    } else {
-      while (a < e) {
-        const uint32_t mid = (a + e) >> 1;
-        if (kv_lt<EW>(kv_load<EW>(data, st + mid), x)) a = mid + 1; else e = mid;
-      }
+    while (a < e) {
+      const uint32_t mid = (a + e) >> 1;
+      if (kv_lt<EW>(kv_load<EW>(data, st + mid), x)) a = mid + 1; else e = mid;
     }
     out[g] = a;
   }

@@ -213,8 +213,8 @@ unsigned long long layout_check_take();
 
 // ---- containment / ANI (ani.hip) ------------------------------------------------------------
 // Dense: ani[i * n + j] from the n x n count matrix (|S_i| on its diagonal).
-hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, uint32_t row_begin, uint32_t row_end,
-                             int kmer_num_ones, double* cont, double* ani, hipStream_t s);
+hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, int kmer_num_ones, double* cont, double* ani,
+                             hipStream_t s);
 // Packed symmetric tiles (I, J) = tiles[2t], tiles[2t + 1]: out [t][2][64][64]
 // (both orientations of each pair); sizes[i] = |S_i|.
 hipError_t launch_ani_tiles(const int32_t* packed, const uint32_t* tiles, uint64_t n_tiles, uint32_t n,

@@ -154,12 +154,19 @@ def _torch_waits_for_ctx(ctx):
         torch.cuda.current_stream().wait_stream(s)
 
 
+_EXT_STREAMS = {}
+
+
 def _ctx_torch_stream(ctx):
     h = getattr(ctx, "stream", 0) or 0
     cur = torch.cuda.current_stream()
     if h == cur.cuda_stream:
         return None
-    return torch.cuda.default_stream() if h == 0 else torch.cuda.ExternalStream(h)
+    if h == 0:
+        return torch.cuda.default_stream()
+    if h not in _EXT_STREAMS:  # one wrapper per HIP stream (building one per call costs host time)
+        _EXT_STREAMS[h] = torch.cuda.ExternalStream(h)
+    return _EXT_STREAMS[h]
 
 
 def _gather_tiles(parts, world, dst):
@@ -365,7 +372,7 @@ def _tiles_before(I, nb):
 
 
 def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None,
-                    ani_host=None):
+                    ani_host=None, pipelined=False, max_size=None):
     """All-vs-all intersection counts (kmer_set.cpp:143-184 over the
     generate_all_pairs_from_vector list, generators.hpp:44-58), and ANI when
     ani_ones (the k of binomial_estimator) is given.
@@ -378,11 +385,17 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     (tiles None: every upper-triangle tile into the dense matrix out);
     ani_matrix(counts, n, k); ani_tiles(tiles, packed, sizes, n, k).
     dst: the rank that assembles the n x n count matrix (None: none, "all":
-    every rank).  Returns a JoinResult."""
+    every rank).  ani_host (one rank, no process group): a pinned host tensor of
+    n * n float64 that receives the ANI matrix (queued, not waited for);
+    pipelined: count in tile-row parts and copy each part's finished ANI rows
+    while later parts are counted (measured slower on config 4: DESIGN.md §6).
+    Returns a JoinResult."""
     res = JoinResult()
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
     solo = _solo(world)
-    mx = int(mine.sizes.max().item()) if mine.n else 0
+    # the largest local sketch (max_size: known to the caller's host, e.g. from
+    # SketchSet.sizes(); else one device reduction and a read-back)
+    mx = (int(max_size) if max_size is not None else int(mine.sizes.max().item())) if mine.n else 0
     if solo:
         ns, totals, mxs = [mine.n], [mine.total], [mx]
     else:
@@ -394,7 +407,7 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
         lay = ops.build(mine, log_b, None, "own")
         out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
         res.counts = res.matrix = out
-        if ani_ones is not None and ani_host is not None and n_genomes and hasattr(ops, "count_range"):
+        if pipelined and ani_ones is not None and ani_host is not None and n_genomes and hasattr(ops, "count_range"):
             # rows of tile rows [0, I) are final once those tile rows are counted
             # (the row-major upper triangle; the mirror halves come from earlier
             # rows): each part's ANI rows are computed and copied into ani_host on a

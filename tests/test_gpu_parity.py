@@ -1008,7 +1008,7 @@ def test_all_vs_all_join_ani_rows_to_host(torch_cuda, ctx):
     ops = sks_dist.GpuJoinOps(ctx)
     host = torch.empty(n * n, dtype=torch.float64, pin_memory=True)
     res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
-                                   device="cuda", dst=None, ani_ones=k, ani_host=host)
+                                   device="cuda", dst=None, ani_ones=k, ani_host=host, pipelined=True)
     torch.cuda.synchronize()
     got = res.matrix.cpu().numpy()
     for i in range(0, n, 37):
