@@ -728,11 +728,14 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
     torch.cuda.synchronize()
     ones = bin(mask).count("1") // 2
     ops = sks_dist.GpuJoinOps(ctx, ew=2 if w > 32 else 1)
+    # one rank without a process group: dense counts and ANI; with one (N > 1, or
+    # the world-1 RCCL rehearsal) the exchange path with per-tile ANI
+    solo = world == 1 and not collective()
     host_ani = None  # pinned, sized on the first step
 
     def pair_step(ss, with_ani=True):
         nonlocal host_ani
-        if world == 1 and with_ani and host_ani is None:
+        if solo and with_ani and host_ani is None:
             host_ani = torch.empty(C4_GENOMES * C4_GENOMES, dtype=torch.float64, pin_memory=True)
         # one rank: the dense ANI matrix is computed after the counts and copied to
         # host memory in one piece (the tile-row pipelined form, ani_host with
@@ -740,10 +743,10 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
         res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss, ew=ops.ew), ops,
                                        sksffi.join_layout_log_b, device="cuda", dst=None,
                                        ani_ones=ones if with_ani else None,
-                                       ani_host=host_ani if world == 1 and with_ani else None,
+                                       ani_host=host_ani if solo and with_ani else None,
                                        pipelined=os.environ.get("SKS_BENCH_PIPELINED_ANI") == "1",
                                        max_size=int(ss.sizes().max()) if ss is not None and ss.n else None)
-        if with_ani and world > 1:  # this rank's ANI tiles, both orientations
+        if with_ani and not solo:  # this rank's ANI tiles, both orientations
             flat = res.ani.reshape(-1)
             if host_ani is None or host_ani.numel() != flat.numel():
                 host_ani = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
@@ -792,7 +795,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
     t_counts /= max(steps, 1)
     ani_mean = None
     counts = None
-    if world == 1:
+    if solo:
         counts = res.matrix.cpu().numpy()
         assert (counts == counts.T).all() and counts[0, 1] > 0
         assert (np.diag(counts) == sizes).all()
@@ -812,10 +815,10 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
         tot = float(a[:, 0].sum()) + float(a[tl[:, 0] != tl[:, 1], 1].sum())
         ani_mean = sum_over_ranks(tot, world) / (C4_GENOMES * C4_GENOMES)
     cpu = cpu_sk = None
-    if cpu_pairs and rank == 0 and world == 1 and w == W:
+    if cpu_pairs and rank == 0 and solo and w == W:
         cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
         cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask)
-    ani_bytes = (C4_GENOMES * C4_GENOMES * 8) if world == 1 else int(res.ani.numel()) * 8
+    ani_bytes = (C4_GENOMES * C4_GENOMES * 8) if solo else int(res.ani.numel()) * 8
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s (count + containment + ANI, ANI in host memory)", "scaling": "strong",
@@ -836,7 +839,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
             "pairs_this_rank": C4_GENOMES * C4_GENOMES / world,
             "achieved_GBps": (8 * 2 * C4_S + 4) * C4_GENOMES * C4_GENOMES / world / (k_ms * 1e-3) / 1e9
             if k_ms else None},
-        "roofline": pairs_lds_roofline(k_ms) if world == 1 and w == W else None,
+        "roofline": pairs_lds_roofline(k_ms) if solo and w == W else None,
         "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - w + 1) / t_sketch,
         "ani_mean_all_pairs": ani_mean,
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
