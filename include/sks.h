@@ -23,7 +23,8 @@ extern "C" {
 #endif
 
 #define SKS_ABI_VERSION 2  /* 2: deduplicated join layout (masks, region ends), elem_words on
-                              the layout entry points, sks_ctx_set_join_check */
+                              the layout entry points, sks_ctx_set_join_check; later additions
+                              within 2 (new symbols only): sks_ani_rows */
 
 typedef enum sks_status {
   SKS_OK = 0,
