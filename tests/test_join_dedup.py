@@ -192,3 +192,35 @@ def test_layout_bucket_passes(torch_cuda, ctx, monkeypatch, shape):
         assert ctx.join_check_violations() == 0
     finally:
         ctx.set_join_check(False)
+
+
+def test_layout_pass_splits_u64(torch_cuda, ctx):
+    """u64 layout passes that overflow the 2048-slot value table and split
+    (bucket halves, then hash slices): the group bounds come from the even
+    sketches (the sampled ones, spread over the whole value range), while the
+    odd sketches put 3000 values each into one narrow range, so one value group
+    of each block holds ~96k distinct values.  Also the value 0 (the table's
+    empty word) in some sketches.  With the check kernels on, no invariant is
+    violated and the counts equal numpy's."""
+    torch = torch_cuda
+    rng = np.random.default_rng(21)
+    n = 128
+    sk = []
+    for i in range(n):
+        if i % 2 == 0:
+            a = rng.integers(1, 2**62, size=3000, dtype=np.uint64)
+        else:
+            a = (np.uint64(2**40) + rng.integers(0, 2**20, size=3000, dtype=np.uint64))
+        if i % 9 == 0:
+            a = np.concatenate([a, np.zeros(1, np.uint64)])
+        sk.append(np.unique(a))
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)]
+                     for i in range(n)])
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    ctx.set_join_check(True)
+    try:
+        for got in _all_ways(torch, ctx, d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n):
+            assert np.array_equal(got, want)
+        assert ctx.join_check_violations() == 0
+    finally:
+        ctx.set_join_check(False)
