@@ -125,6 +125,20 @@ def sum_over_ranks(x, world):
     return _reduce_scalar(x, dist.ReduceOp.SUM)
 
 
+def sum_vector_over_ranks(v, world):
+    if not collective():
+        return v
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.int64)).to(dev)
+    dist.all_reduce(t)
+    return t.cpu().numpy()
+
+
+# all-vs-all sketch exchange between ranks (sks_dist.all_vs_all_join): p2p | allgather | broadcast
+EXCHANGE = "p2p"
+
+
 # ---- config 3 ---------------------------------------------------------------------
 def c3_layout():
     """Byte layout of one genome: contigs separated by '\\n'; N-run offsets."""
@@ -728,30 +742,22 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
     torch.cuda.synchronize()
     ones = bin(mask).count("1") // 2
     ops = sks_dist.GpuJoinOps(ctx, ew=2 if w > 32 else 1)
-    # one rank without a process group: dense counts and ANI; with one (N > 1, or
-    # the world-1 RCCL rehearsal) the exchange path with per-tile ANI
+    # one rank without a process group counts every tile of one layout; with one
+    # (N > 1, or the world-1 RCCL rehearsal) the cyclic tile plan and the sketch
+    # exchange.  Either way the join writes every counted pair's ANI straight
+    # into this pinned host matrix (sks_intersect_layout_ani; each rank the cells
+    # of its own tiles), so no ANI kernel or device-to-host copy follows the join
     solo = world == 1 and not collective()
-    host_ani = None  # pinned, sized on the first step
+    host_ani = sksffi.HostBuffer(C4_GENOMES * C4_GENOMES * 8)
+    host_ani.array[:] = 0.0
 
     def pair_step(ss, with_ani=True):
-        nonlocal host_ani
-        if solo and with_ani and host_ani is None:
-            host_ani = torch.empty(C4_GENOMES * C4_GENOMES, dtype=torch.float64, pin_memory=True)
-        # one rank: the dense ANI matrix is computed after the counts and copied to
-        # host memory in one piece (the tile-row pipelined form, ani_host with
-        # pipelined=True, measured slower: DESIGN.md §6)
-        res = sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss, ew=ops.ew), ops,
-                                       sksffi.join_layout_log_b, device="cuda", dst=None,
-                                       ani_ones=ones if with_ani else None,
-                                       ani_host=host_ani if solo and with_ani else None,
-                                       pipelined=os.environ.get("SKS_BENCH_PIPELINED_ANI") == "1",
-                                       max_size=int(ss.sizes().max()) if ss is not None and ss.n else None)
-        if with_ani and not solo:  # this rank's ANI tiles, both orientations
-            flat = res.ani.reshape(-1)
-            if host_ani is None or host_ani.numel() != flat.numel():
-                host_ani = torch.empty(flat.numel(), dtype=torch.float64, pin_memory=True)
-            host_ani.copy_(flat, non_blocking=True)
-        return res
+        return sks_dist.all_vs_all_join(C4_GENOMES, world, rank, sks_dist.sketches_of(ss, ew=ops.ew), ops,
+                                        sksffi.join_layout_log_b, device="cuda", dst=None,
+                                        ani_ones=ones if with_ani else None,
+                                        ani_out=host_ani if with_ani else None,
+                                        max_size=int(ss.sizes().max()) if ss is not None and ss.n else None,
+                                        size_bound=C4_S, exchange=EXCHANGE)
 
     t_sketch = t_pairs = t_counts = 0.0
     timed = 0
@@ -793,32 +799,35 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
     t_sketch /= max(timed, 1)
     t_pairs /= max(timed, 1)
     t_counts /= max(steps, 1)
-    ani_mean = None
+    res.check_layouts()  # every join layout of the last timed step was valid
+    ani = host_ani.array.reshape(C4_GENOMES, C4_GENOMES)
     counts = None
+    # the rank's tiles' counts placed in the n x n matrix (zero elsewhere)
+    mat = sks_dist.place_tiles(torch.zeros((C4_GENOMES, C4_GENOMES), dtype=torch.int32, device="cuda"),
+                               res.tiles, res.counts, C4_GENOMES).cpu().numpy()
+    # the fused ANI against the host's (kmer-sketching.cpp:195-200 on the exact
+    # counts), on every cell this rank's tiles cover
+    covered = np.zeros((C4_GENOMES, C4_GENOMES), bool)
+    for I, J in np.asarray(res.tiles).reshape(-1, 2):
+        covered[I * 64:(I + 1) * 64, J * 64:(J + 1) * 64] = True
+        covered[J * 64:(J + 1) * 64, I * 64:(I + 1) * 64] = True
+    all_sizes = np.zeros(C4_GENOMES, np.int64)
+    all_sizes[g0:g1] = sizes
+    all_sizes = sum_vector_over_ranks(all_sizes, world)
+    rows_i = np.nonzero(covered)[0]
+    _, h_ani = sksffi.ani_from_counts(mat[covered], all_sizes[rows_i].astype(np.int32), ones)
+    ani_err = float(np.abs(ani[covered] - h_ani).max()) if covered.any() else 0.0
+    assert ani_err <= 1e-9, ani_err
+    ani_mean = sum_over_ranks(float(ani[covered].sum()), world) / (C4_GENOMES * C4_GENOMES)
     if solo:
-        counts = res.matrix.cpu().numpy()
+        counts = mat
         assert (counts == counts.T).all() and counts[0, 1] > 0
         assert (np.diag(counts) == sizes).all()
-        ani = host_ani.numpy().reshape(C4_GENOMES, C4_GENOMES)
-        # the device ANI against the host's (kmer-sketching.cpp:195-200 on the exact counts)
-        size_first = np.repeat(np.diag(counts).astype(np.int32), C4_GENOMES)
-        _, h_ani = sksffi.ani_from_counts(counts.reshape(-1), size_first, ones)
-        ani_err = float(np.abs(ani.reshape(-1) - h_ani).max())
-        assert ani_err <= 1e-9, ani_err
-        ani_mean = float(ani.mean())
-    else:
-        ani_err = None
-        # ANI sum over every ordered pair, from the tiles' two orientations (a
-        # diagonal tile's second block repeats its first)
-        a = res.ani.cpu().numpy()
-        tl = np.asarray(res.tiles).reshape(-1, 2)
-        tot = float(a[:, 0].sum()) + float(a[tl[:, 0] != tl[:, 1], 1].sum())
-        ani_mean = sum_over_ranks(tot, world) / (C4_GENOMES * C4_GENOMES)
     cpu = cpu_sk = None
     if cpu_pairs and rank == 0 and solo and w == W:
         cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
         cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask)
-    ani_bytes = (C4_GENOMES * C4_GENOMES * 8) if solo else int(res.ani.numel()) * 8
+    ani_bytes = int(covered.sum()) * 8
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
         "unit": "ordered pairs/s (count + containment + ANI, ANI in host memory)", "scaling": "strong",
@@ -845,12 +854,12 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
                    "genome_len": C4_LEN, "s": C4_S, "w": w, "k": ones,
                    "kmer_bits": 128 if w > 32 else 64,
-                   "pair_sharding": "block-aligned genomes per rank; tile plan: the rank's own "
-                                    "blocks' 64x64 join tiles, then half of every cross-rank block "
-                                    "pair as the peer's sketches land",
-                   "collective": ("all_gather of (genomes, elements, largest sketch) + broadcast of "
-                                  "rank 0's group bounds + one broadcast of sketches and sizes per "
-                                  f"source rank ({backend_label()})" if collective() else "none")},
+                   "pair_sharding": "block-aligned genomes per rank; cyclic tile plan: the rank's own "
+                                    "blocks' 64x64 join tiles, then every tile pairing its blocks with "
+                                    "ranks r+1 .. r+N/2 (the N/2 pairs split) as their sketches land",
+                   "ani": "written by the join (last workgroup of each tile) into pinned host memory",
+                   "collective": (f"broadcast of rank 0's group bounds + sketch exchange '{EXCHANGE}' of "
+                                  f"sketches padded to s ({backend_label()})" if collective() else "none")},
         "cpu_baseline": cpu,
         "cpu_baseline_sketch_phase": cpu_sk,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
@@ -1119,6 +1128,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=3,
                     help="config-3 builds in flight (one context + HIP stream each)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--exchange", default="p2p", choices=["p2p", "allgather", "broadcast"],
+                    help="config-4 sketch exchange between ranks (sks_dist.all_vs_all_join)")
     ap.add_argument("--dist-rehearsal", action="store_true",
                     help="start the process group at world 1 too (under torchrun), so the "
                          "collective paths run on the backend")
@@ -1126,6 +1137,8 @@ def main():
                     help="PMC HBM traffic of the scan launches this command times "
                          "(tools/profile_round.sh; default: the newest profiles/rNN)")
     args = ap.parse_args()
+    global EXCHANGE
+    EXCHANGE = args.exchange
 
     world, rank, local = dist_setup(args.gpus, args.dist_backend, args.dist_rehearsal)
     ctx = sksffi.Context(local)

@@ -24,7 +24,9 @@ extern "C" {
 
 #define SKS_ABI_VERSION 2  /* 2: deduplicated join layout (masks, region ends), elem_words on
                               the layout entry points, sks_ctx_set_join_check; later additions
-                              within 2 (new symbols only): sks_ani_rows */
+                              within 2 (new symbols only): sks_ani_rows, sks_intersect_layout_ani,
+                              sks_host_alloc, sks_host_free, sks_join_layout_stat_copy,
+                              sks_sketches_export */
 
 typedef enum sks_status {
   SKS_OK = 0,
@@ -298,6 +300,12 @@ int sks_join_layout_build(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* 
                           uint32_t log_b, const uint64_t* d_bounds, uint64_t* d_out_vals,
                           uint64_t* d_out_masks, uint32_t* d_out_boff, uint64_t* d_out_bstart,
                           uint32_t* max_block_bucket);
+/* Queues a copy of the last sks_join_layout_build's two status words on this
+ * context — [0] the largest block-bucket population, [1] non-zero when the
+ * layout is invalid (see max_block_bucket) — into d_dst (2 x u32, device), so
+ * a caller that skips the read-back can check the layout after the join
+ * without a stream round trip.  Call it right after the build. */
+int sks_join_layout_stat_copy(sks_ctx* ctx, uint32_t* d_dst);
 /* sks_intersect_sym over a join layout of n sketches: upper-triangle 64x64 tiles
  * [tile_begin, tile_end) into the n x n int32 matrix d_out (zeroed first). */
 int sks_intersect_sym_layout(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_words, const uint64_t* d_vals,
@@ -331,6 +339,38 @@ int sks_intersect_layout_pair_tiles(sks_ctx* ctx, uint32_t n, uint32_t log_b, in
                                     const uint64_t* d_cmasks, const uint32_t* d_cboff, const uint64_t* d_cbstart,
                                     uint32_t c_blk0, const uint32_t* d_tiles, uint64_t tile_begin,
                                     uint64_t tile_end, int packed, int32_t* d_out);
+/* sks_intersect_layout_pair_tiles fused with containment / ANI — the count
+ * loop, the containment / binomial_estimator loop and the host result vector of
+ * kmer-sketching.cpp:185-200 (ani_estimation.cpp:24-42) in one launch: counts
+ * are added to d_out as there (packed or both halves of the n x n matrix; the
+ * caller zeroes d_out), and as each tile's last workgroup finishes, it writes
+ *   ani[i * n + j] = binomial_estimator(containment(|S_i ∩ S_j|, d_sizes[i]), kmer_num_ones)
+ * for both orientations (i, j) and (j, i) of every pair of the tile (the
+ * diagonal tile's own pairs once).  d_sizes[i] = |S_i| (int32, n entries, by
+ * global genome index).  ani: n * n doubles in device memory, or pinned host
+ * memory (sks_host_alloc, or any hipHostMalloc'd buffer): the kernel then
+ * writes the host matrix itself, so the transfer runs while later tiles are
+ * counted.  Cells of tiles not in the list are left untouched.  d_tiles ==
+ * NULL: the upper-triangle tiles [tile_begin, tile_end) of ONE layout
+ * (rows == cols, r_blk0 = c_blk0 = 0). */
+int sks_intersect_layout_ani(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_words,
+                             const uint64_t* d_rvals, const uint64_t* d_rmasks, const uint32_t* d_rboff,
+                             const uint64_t* d_rbstart, uint32_t r_blk0, const uint64_t* d_cvals,
+                             const uint64_t* d_cmasks, const uint32_t* d_cboff, const uint64_t* d_cbstart,
+                             uint32_t c_blk0, const uint32_t* d_tiles, uint64_t tile_begin, uint64_t tile_end,
+                             int packed, int32_t* d_out, const int32_t* d_sizes, int kmer_num_ones, double* ani);
+/* sks_sketch_set_export for sketches given as device arrays (e.g. a received
+ * shard): d_dst[i * stride * elem_words ...] = sketch i padded with ~0 words,
+ * d_dst_sizes[i] = d_sizes[i]; queued on the context stream, no wait.  Every
+ * d_sizes[i] must be <= stride (the caller's bound; larger sketches are cut). */
+int sks_sketches_export(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
+                        int elem_words, uint32_t n, uint64_t* d_dst, uint64_t stride, uint32_t* d_dst_sizes);
+/* Pinned host memory the device reads and writes directly (coherent, mapped
+ * into every device's address space): the destination of a fused ANI matrix.
+ * No reference counterpart (the reference's result vectors are plain host
+ * vectors, kmer-sketching.cpp:193). */
+int sks_host_alloc(uint64_t bytes, void** out);
+int sks_host_free(void* p);
 /* The set's sketches back to back (sizes[i] * elem_words words each, in order)
  * and its sizes, copied into caller device buffers (a send buffer). */
 int sks_sketch_set_export_csr(const sks_sketch_set* set, uint64_t* d_data, uint32_t* d_sizes);

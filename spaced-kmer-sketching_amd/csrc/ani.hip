@@ -23,12 +23,6 @@ namespace {
 constexpr int kAB = 256;
 constexpr int kTile = 64;
 
-__device__ __forceinline__ double ani_of(int32_t inter, int32_t size_first, double inv_k, double* cont) {
-  const double c = inter == 0 ? 0.0 : (double)inter / (double)size_first;
-  if (cont) *cont = c;
-  return c <= 0.0 ? 0.0 : pow(c, inv_k);
-}
-
 // ani[i * n + j] for rows [row_begin, row_end) of the dense n x n count
 // matrix; |S_i| = counts[i][i]
 __global__ __launch_bounds__(kAB) void k_ani_matrix(const int32_t* __restrict__ counts, uint32_t n,

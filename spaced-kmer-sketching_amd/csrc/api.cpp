@@ -204,6 +204,8 @@ struct sks_ctx {
   sks::Scratch flag, pos;
   sks::Scratch meta;                // small per-segment device arrays
   sks::Scratch iwork;               // intersection bucket tables
+  sks::Scratch tdone;               // fused ANI: workgroups finished per join tile
+  const uint32_t* layout_stat = nullptr;  // the last join-layout build's 2 status words (in iwork)
   std::vector<uint64_t> meta_host;  // staging for `meta`
   sks_timings last{};
   int grid_override = 0;
@@ -560,7 +562,7 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
   c->stream = reinterpret_cast<hipStream_t>(stream);
   // every scratch buffer is used on the context's stream only
   for (sks::Scratch* sc : {&c->ingress, &c->tmp, &c->rec[0], &c->rec[1], &c->rec[2], &c->flag,
-                           &c->pos, &c->meta, &c->iwork})
+                           &c->pos, &c->meta, &c->iwork, &c->tdone})
     sc->owner = &c->stream;
   for (auto& b : c->buf) b.owner = &c->stream;
   if (hipEventCreate(&c->ev_begin) != hipSuccess || hipEventCreate(&c->ev_end) != hipSuccess ||
@@ -584,6 +586,7 @@ int sks_ctx_destroy(sks_ctx* c) {
   c->pos.release();
   c->meta.release();
   c->iwork.release();
+  c->tdone.release();
   c->ingress.release();
   trim_device_cache(c->device);
   (void)hipEventDestroy(c->ev_begin);
@@ -1539,6 +1542,7 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
   char* w = static_cast<char*>(c->iwork.ptr);
   uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
   SKS_HIP(hipMemsetAsync(stat, 0, 8, c->stream));
+  c->layout_stat = stat;
   if (n == 0) {
     SKS_HIP(hipMemsetAsync(d_out_bstart, 0, 8, c->stream));
   } else {
@@ -1550,6 +1554,14 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
     SKS_HIP(sks::pinned_d2h(h, stat, 8, c->stream));
     *max_block_bucket = h[1] ? UINT32_MAX : h[0];
   }
+  return SKS_OK;
+}
+
+int sks_join_layout_stat_copy(sks_ctx* c, uint32_t* d_dst) {
+  if (!c || !d_dst) return sks::fail(SKS_E_ARG, "sks_join_layout_stat_copy: null argument");
+  if (!c->layout_stat) return sks::fail(SKS_E_ARG, "sks_join_layout_stat_copy: no layout built on this context");
+  DeviceGuard g(c->device);
+  SKS_HIP(hipMemcpyAsync(d_dst, c->layout_stat, 8, hipMemcpyDeviceToDevice, c->stream));
   return SKS_OK;
 }
 
@@ -1624,6 +1636,69 @@ int sks_intersect_layout_pair_tiles(sks_ctx* c, uint32_t n, uint32_t log_b, int 
   return SKS_OK;
 }
 
+int sks_intersect_layout_ani(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_words, const uint64_t* d_rvals,
+                             const uint64_t* d_rmasks, const uint32_t* d_rboff, const uint64_t* d_rbstart,
+                             uint32_t r_blk0, const uint64_t* d_cvals, const uint64_t* d_cmasks,
+                             const uint32_t* d_cboff, const uint64_t* d_cbstart, uint32_t c_blk0,
+                             const uint32_t* d_tiles, uint64_t tile_begin, uint64_t tile_end, int packed,
+                             int32_t* d_out, const int32_t* d_sizes, int kmer_num_ones, double* ani) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: null ctx");
+  if (log_b > 14) return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: log_b > 14");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: kmer_num_ones must be positive");
+  if (tile_begin > tile_end) return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: bad tile range");
+  if (!d_tiles && tile_end > sks::intersect_sym_tiles(n))
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: tile range beyond the upper triangle");
+  if (!d_tiles && tile_end > tile_begin && (r_blk0 != 0 || c_blk0 != 0 || d_rvals != d_cvals))
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: a tile range needs one layout with blk0 = 0 "
+                                "(pass a tile list)");
+  if (tile_end > tile_begin &&
+      (!d_rboff || !d_rbstart || !d_cboff || !d_cbstart || !d_out || !d_sizes || !ani))
+    return sks::fail(SKS_E_ARG, "sks_intersect_layout_ani: null argument");
+  DeviceGuard g(c->device);
+  // the ANI matrix may be host memory: the kernel needs its device-side address
+  double* d_ani = ani;
+  if (tile_end > tile_begin) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, ani) == hipSuccess && at.type == hipMemoryTypeHost) {
+      void* dp = nullptr;
+      SKS_HIP(hipHostGetDevicePointer(&dp, ani, 0));
+      d_ani = static_cast<double*>(dp);
+    }
+    (void)hipGetLastError();  // an unregistered pointer leaves an error behind; use it as is
+  }
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  if (n && tile_end > tile_begin) {
+    const uint64_t nt = tile_end - tile_begin;
+    SKS_HIP(c->tdone.reserve(nt * sizeof(uint32_t)));
+    SKS_HIP(hipMemsetAsync(c->tdone.ptr, 0, nt * sizeof(uint32_t), c->stream));
+    const sks::JoinLayout R{d_rvals, d_rmasks, d_rboff, d_rbstart}, C{d_cvals, d_cmasks, d_cboff, d_cbstart};
+    const sks::JoinAni A{d_ani, d_sizes, kmer_num_ones, static_cast<uint32_t*>(c->tdone.ptr)};
+    SKS_HIP(sks::join_launch(R, 0u - r_blk0, C, 0u - c_blk0, n, log_b, elem_words, true, 0, n, tile_begin,
+                             tile_end, d_tiles, packed != 0, d_out, c->join_check, c->stream, &A));
+  }
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return sks::fail(SKS_E_ARG, "sks_host_alloc: null out");
+  *out = nullptr;
+  if (!bytes) return SKS_OK;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return sks::fail(SKS_E_NOMEM, "sks_host_alloc: hipHostMalloc of " + std::to_string(bytes) + " bytes failed");
+  }
+  *out = p;
+  return SKS_OK;
+}
+
+int sks_host_free(void* p) {
+  if (p) SKS_HIP(hipHostFree(p));
+  return SKS_OK;
+}
+
 int sks_ani_matrix(sks_ctx* c, const int32_t* d_counts, uint32_t n, int kmer_num_ones, double* d_cont,
                    double* d_ani) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_ani_matrix: null ctx");
@@ -1653,6 +1728,17 @@ int sks_ani_tiles(sks_ctx* c, const int32_t* d_packed, const uint32_t* d_tiles, 
     return sks::fail(SKS_E_ARG, "sks_ani_tiles: null argument");
   DeviceGuard g(c->device);
   SKS_HIP(sks::launch_ani_tiles(d_packed, d_tiles, n_tiles, n, d_sizes, kmer_num_ones, d_ani, c->stream));
+  return SKS_OK;
+}
+
+int sks_sketches_export(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
+                        int elem_words, uint32_t n, uint64_t* d_dst, uint64_t stride, uint32_t* d_dst_sizes) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_sketches_export: null ctx");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (n && (!d_starts || !d_sizes || !d_dst || !d_dst_sizes || !stride))
+    return sks::fail(SKS_E_ARG, "sks_sketches_export: null argument or zero stride");
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::launch_export(d_data, d_starts, d_sizes, n, elem_words, d_dst, stride, d_dst_sizes, c->stream));
   return SKS_OK;
 }
 

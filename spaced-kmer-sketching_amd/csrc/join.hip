@@ -29,6 +29,7 @@
 #include <cstdint>
 
 #include "join_common.hpp"
+#include "sks_ani.hpp"
 #include "sks_internal.hpp"
 
 namespace sks {
@@ -63,6 +64,7 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 // hit items with more rows than this are spread over the wave's lanes (rows_add)
 constexpr uint32_t kLight = 2;
 static_assert(kJCap == 1024, "entry index: 10 bits of the slot word");
+static_assert(kFSlots >= kTile * kTile, "the fused ANI stages a tile's counts in the slot table");
 
 // s_waitcnt immediate for gfx9 "vmcnt(0)" with expcnt / lgkmcnt left at their
 // maxima: vmcnt = imm[3:0] | imm[15:14] << 4, expcnt = imm[6:4], lgkmcnt = imm[11:8]
@@ -80,6 +82,11 @@ struct JoinArgs {
   uint64_t ld;
   uint32_t cap;  // column entries per chunk (<= kJCap): table load <= cap / kFSlots
   int packed;    // out = [tile - tile_begin][64][64]
+  // fused containment / ANI (JoinAni): null ani = counts only
+  double* ani;
+  const int32_t* sizes;
+  double inv_k;
+  uint32_t* tile_done;  // [tile - tile_begin]
 };
 
 template <int EW>
@@ -484,16 +491,56 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
       atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
     }
   }
+  if (!a.ani) return;
+  // ---- fused containment / ANI: the tile's last workgroup converts it --------------------------
+  // Every workgroup of the tile releases its count atomics (agent scope) before
+  // counting itself done; the one that completes the tile acquires and reads the
+  // tile's counts back with agent-scope loads (per-XCD L2s are not coherent), then
+  // writes both orientations of the tile's ANI: (r, c) with lanes over columns and
+  // (c, r) with lanes over rows, so every wave's stores are one contiguous 512-byte
+  // row segment of the n x n matrix (ani may be pinned host memory: PCIe writes).
+  __threadfence();
+  __syncthreads();
+  if (tid == 0)
+    s_top = __hip_atomic_fetch_add(a.tile_done + (t - a.tile_begin), 1u, __ATOMIC_ACQ_REL,
+                                   __HIP_MEMORY_SCOPE_AGENT) + 1 == a.n_groups;
+  __syncthreads();
+  if (!s_top) return;
+  __threadfence();
+  int32_t* s_cnt = reinterpret_cast<int32_t*>(s_slot);  // the table is free: 4096 counts
+  for (uint32_t q = tid; q < (uint32_t)(kTile * kTile); q += kJB) {
+    const uint32_t r = q / kTile, c = q % kTile, gr = row0 + r, gc = col0 + c;
+    int32_t x = 0;
+    if (gr < row_lim && gc < a.n) {
+      const int32_t* p = a.packed ? a.out + (t - a.tile_begin) * (kTile * kTile) + q : a.out + (uint64_t)gr * a.ld + gc;
+      x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_cnt[q] = x;
+  }
+  __syncthreads();
+  for (uint32_t r = tid >> 6; r < kTile; r += kJB / 64) {
+    const uint32_t gr = row0 + r, gc = col0 + lane;
+    if (gr < row_lim && gc < a.n)
+      a.ani[(uint64_t)gr * a.n + gc] = ani_of(s_cnt[r * kTile + lane], a.sizes[gr], a.inv_k, nullptr);
+  }
+  if (I != J) {
+    for (uint32_t c = tid >> 6; c < kTile; c += kJB / 64) {
+      const uint32_t gr = row0 + lane, gc = col0 + c;
+      if (gr < row_lim && gc < a.n)
+        a.ani[(uint64_t)gc * a.n + gr] = ani_of(s_cnt[lane * kTile + c], a.sizes[gc], a.inv_k, nullptr);
+    }
+  }
 }
 
 template <int EW, bool CHECK>
 hipError_t launch_join_slices(JoinArgs ja, uint64_t tile_begin, uint64_t tile_end, bool packed, int32_t* out,
-                              hipStream_t s) {
+                              uint32_t* tile_done, hipStream_t s) {
   const uint64_t tiles_per_launch = std::max<uint64_t>(1, kMaxGrid / ja.n_groups);
   for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
     const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
     ja.tile_begin = t0;
     if (packed) ja.out = out + (t0 - tile_begin) * (uint64_t)(kTile * kTile);
+    if (ja.ani) ja.tile_done = tile_done + (t0 - tile_begin);
     hipLaunchKernelGGL((k_join<EW, CHECK>), dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -529,8 +576,9 @@ unsigned long long join_check_take() {
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
                        uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
-                       int32_t* out, bool check, hipStream_t s) {
+                       int32_t* out, bool check, hipStream_t s, const JoinAni* ani) {
   if (log_b > jc::kMaxLogB || (ew != 1 && ew != 2)) return hipErrorInvalidValue;
+  if (ani && !sym && !d_tiles) return hipErrorInvalidValue;  // ANI of whole tiles only
   const uint32_t n_cb = (n + kTile - 1) / kTile;
   const uint32_t n_rb = sym ? n_cb : (row_end - row_begin + kTile - 1) / kTile;
   if (!d_tiles) {
@@ -560,6 +608,12 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.out = out;
   ja.ld = n;
   ja.cap = join_cap();
+  if (ani) {
+    ja.ani = ani->ani;
+    ja.sizes = ani->sizes;
+    ja.inv_k = ((double)1.0) / ((double)ani->kmer_num_ones);
+  }
+  uint32_t* tile_done = ani ? ani->tile_done : nullptr;
   // bucket groups per tile: ~128 buckets per workgroup (a workgroup's start-up —
   // clearing its table and count planes — and its count flush, up to 4096 global
   // atomics on a tile of related genomes, are then small beside its chunks), at
@@ -577,10 +631,10 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.buckets_per_group = (B + groups - 1) / groups;
   ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
   if (ew == 1)
-    return check ? launch_join_slices<1, true>(ja, tile_begin, tile_end, packed, out, s)
-                 : launch_join_slices<1, false>(ja, tile_begin, tile_end, packed, out, s);
-  return check ? launch_join_slices<2, true>(ja, tile_begin, tile_end, packed, out, s)
-               : launch_join_slices<2, false>(ja, tile_begin, tile_end, packed, out, s);
+    return check ? launch_join_slices<1, true>(ja, tile_begin, tile_end, packed, out, tile_done, s)
+                 : launch_join_slices<1, false>(ja, tile_begin, tile_end, packed, out, tile_done, s);
+  return check ? launch_join_slices<2, true>(ja, tile_begin, tile_end, packed, out, tile_done, s)
+               : launch_join_slices<2, false>(ja, tile_begin, tile_end, packed, out, tile_done, s);
 }
 
 }  // namespace sks

@@ -203,10 +203,21 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
 // `rows` and column block c_blk0 + J of `cols` (uint32 arithmetic: 0 - blk0
 // maps global block indices onto a layout whose block 0 is blk0).  packed:
 // out = [tile - tile_begin][64][64].  Counts are added to `out`.
+// Fused containment / ANI (sym / tile-list launches only): the last workgroup
+// of each tile reads the tile's finished counts back and writes
+// ani[i * n + j] = binomial_estimator(containment(count, sizes[i]), k) for both
+// orientations of the tile, so the conversion (and, when `ani` is pinned host
+// memory, its PCIe transfer) runs under the join instead of after it.
+struct JoinAni {
+  double* ani;            // n x n row-major: HBM, or host memory mapped for the device
+  const int32_t* sizes;   // [n] |S_i| by global genome index
+  int kmer_num_ones;      // k of binomial_estimator
+  uint32_t* tile_done;    // [tile_end - tile_begin] workgroups finished per tile, zeroed
+};
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
                        uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
-                       int32_t* out, bool check, hipStream_t s);
+                       int32_t* out, bool check, hipStream_t s, const JoinAni* ani = nullptr);
 // SKS check builds: invariant violations counted since the last call (and reset)
 unsigned long long join_check_take();
 unsigned long long layout_check_take();

@@ -136,9 +136,11 @@ def seed_sweep(n_seeds, world, rank, ani_for_seed, n_genomes, device="cpu"):
 # ---- stream ordering, packed tiles, one receiving rank ---------------------------------------
 # Each rank counts a fixed plan of upper-triangle 64x64 tiles (tile_plan): the
 # tiles of its own blocks first — from its own data, while the exchange is in
-# flight — then its half of every cross-rank block pair.  Counts stay packed
-# ([tile][64][64] int32, 16 KB per tile); when asked they go to ONE rank (dst),
-# where the n x n matrix is assembled: no collective carries n^2 words.
+# flight — then the tiles pairing its blocks with those of the peers the cyclic
+# plan gives it.  Counts stay packed ([tile][64][64] int32, 16 KB per tile);
+# when asked they go to ONE rank (dst), where the n x n matrix is assembled: no
+# collective carries n^2 words.  Containment and ANI are written by the join
+# itself (sks_intersect_layout_ani), straight into the caller's n x n matrix.
 
 def _ctx_waits_for_torch(ctx):
     """Order the context's HIP stream after work queued so far on torch's current
@@ -216,22 +218,29 @@ def place_tiles(mat, tiles, parts, n):
     return mat
 
 
-# ---- all-vs-all over join layouts, sketches exchanged per source rank ---------------------
+# ---- all-vs-all over join layouts -------------------------------------------------------------
 # The join kernel's input (sks_join_layout_build) is built per 64-sketch block.
 # Each rank owns whole blocks (block_shard), sketches them and builds the layout
 # of its own blocks; it counts its own blocks' tiles on that layout at once.
-# Every rank's sketches are then broadcast by their owner (all ranks issue the
-# broadcasts in rank order; with RCCL they run on the collective stream), and
-# as source q's sketches land, the receiver builds q's block layout and counts
-# its share of the (own, q) tiles (tile_plan), while the later sources are
-# still in flight.  Raw sketches travel (8 B per element, or 16 B for 128-bit
-# k-mers) rather than layouts: a deduplicated layout keeps its regions at raw
-# offsets (16 B per raw element with the mask), and rebuilding a peer's layout
-# (~90 us for all of config 4) costs less than moving twice the bytes.  All
+# The cross-rank tiles follow a cyclic plan (tile_plan_by_peer): rank r counts
+# every tile pairing its blocks with those of rank r + d (mod N) for
+# d = 1 .. N/2, the d = N/2 pairs (even N) split in halves between the two, so
+# a rank needs the sketches of N/2 peers, not N - 1, and builds N/2 peer
+# layouts (4 instead of 7 at N = 8).  Sketches travel padded to a common stride
+# (the caller's size bound, e.g. bottom-s s: no size exchange and no host
+# round trip), by one of three exchanges:
+#   "p2p"        batched send/recv, step d: send to r - d, receive from r + d
+#                (each rank receives only what its plan needs; the joins of
+#                step d start as soon as step d has landed),
+#   "allgather"  one all_gather_into_tensor of the per-rank padded blocks (the
+#                collective north_star names; every peer lands at once),
+#   "broadcast"  one broadcast per source rank, queued in rank order.
+# Raw sketches travel rather than layouts: a deduplicated layout keeps its
+# regions at raw offsets with 16 B per slot, so it is larger than the sketch,
+# and rebuilding a peer's layout costs less than moving twice the bytes.  All
 # layouts share rank 0's value-group bounds (broadcast first), so every pair of
-# blocks is bucketed alike.  Counts stay packed per tile; containment / ANI are
-# computed per tile on the rank that counted it (sks_ani_tiles); the count
-# tiles are assembled into the n x n matrix only where asked (dst).
+# blocks is bucketed alike.  Containment / ANI are written by the join into the
+# caller's n x n matrix as each tile completes (the rank's own tiles only).
 
 def block_shard(n_genomes, world, rank):
     """(blocks per rank, g0, g1): genome range of `rank`, whole 64-sketch blocks."""
@@ -245,9 +254,11 @@ def block_shard(n_genomes, world, rank):
 def tile_plan_by_peer(n_genomes, world, rank):
     """(local, remote): local int64 [T, 2] — the upper-triangle tiles (I, J)
     with both blocks in the rank's own block range; remote — a list over ranks
-    q of the tiles pairing the two ranks' blocks that `rank` counts (row-major
-    over the pair, the lower rank takes the first half; I is in the lower
-    rank's blocks, J in the higher's; empty for q == rank)."""
+    q of the tiles pairing the two ranks' blocks that `rank` counts (I in the
+    lower rank's blocks, J in the higher's).  Cyclic: rank r counts the pairs
+    with q = r + d (mod world) for d = 1 .. world // 2; at d = world / 2 (even
+    world) the two ranks reach each other, and the lower rank takes the first
+    half of the pair's tiles (row-major), the higher the rest."""
     nb = (n_genomes + TILE - 1) // TILE
     bpr = block_shard(n_genomes, world, rank)[0]
 
@@ -258,17 +269,19 @@ def tile_plan_by_peer(n_genomes, world, rank):
     I, J = np.meshgrid(mine, mine, indexing="ij")
     keep = I <= J
     local = np.stack([I[keep], J[keep]], axis=1).reshape(-1, 2) if mine.size else np.zeros((0, 2), np.int64)
-    remote = []
-    for q in range(world):
+    remote = [np.zeros((0, 2), np.int64) for _ in range(world)]
+    for d in range(1, world // 2 + 1):
+        q = (rank + d) % world
         a, b = min(rank, q), max(rank, q)
         ba, bb = blocks(a), blocks(b)
-        if q == rank or not ba.size or not bb.size:
-            remote.append(np.zeros((0, 2), np.int64))
+        if not ba.size or not bb.size:
             continue
         I, J = np.meshgrid(ba, bb, indexing="ij")
         pairs = np.stack([I.reshape(-1), J.reshape(-1)], axis=1)
-        h = (len(pairs) + 1) // 2
-        remote.append(pairs[:h] if rank == a else pairs[h:])
+        if 2 * d == world:
+            h = (len(pairs) + 1) // 2
+            pairs = pairs[:h] if rank == a else pairs[h:]
+        remote[q] = pairs
     local.flags.writeable = False  # cached: shared by every caller
     for r in remote:
         r.flags.writeable = False
@@ -277,16 +290,25 @@ def tile_plan_by_peer(n_genomes, world, rank):
 
 def tile_plan(n_genomes, world, rank):
     """(local, remote) int64 arrays [T, 2] of the upper-triangle tiles (I, J) that
-    `rank` counts: its own blocks' tiles, then its share of every cross-rank
-    block pair (tile_plan_by_peer, concatenated in rank order).  Every tile of
+    `rank` counts: its own blocks' tiles, then its share of the cross-rank
+    block pairs (tile_plan_by_peer, concatenated in rank order).  Every tile of
     the n x n upper triangle is in exactly one rank's plan."""
     local, remote = tile_plan_by_peer(n_genomes, world, rank)
     return local, np.concatenate(remote).reshape(-1, 2)
 
 
+def peer_needs(n_genomes, world, rank):
+    """Ranks whose sketches `rank` needs (its plan pairs its blocks with theirs),
+    in the cyclic order r + 1, r + 2, ...."""
+    _, remote = tile_plan_by_peer(n_genomes, world, rank)
+    return [(rank + d) % world for d in range(1, world) if len(remote[(rank + d) % world])]
+
+
 class Sketches:
     """A rank's sketch set as tensors: data int64 [total * ew] (sketches back to
-    back), sizes int32 [n], starts int64 [n] (element index of each sketch)."""
+    back, or at a fixed stride), sizes int32 [n], starts int64 [n] (element
+    index of each sketch); total = elements the data holds (an upper bound of
+    the sizes' sum)."""
 
     def __init__(self, data, sizes, ew=1, starts=None):
         self.data, self.sizes, self.ew = data, sizes, ew
@@ -299,199 +321,250 @@ class Sketches:
         self.total = int(data.numel()) // ew
 
 
-def _exchange_start(own, ns, totals, world, rank):
-    """Starts one broadcast per source rank (in rank order, on every rank) of
-    the source's sketches; returns wait(q) -> Sketches of rank q.  With RCCL the
-    broadcasts run on the collective stream and wait(q) only orders torch's
-    current stream after source q's (the host does not block); with gloo the
-    data goes through host memory, synchronously."""
+def _strided(data, sizes, ew, stride):
+    n = int(sizes.numel())
+    st = torch.arange(n, dtype=torch.int64, device=sizes.device) * stride
+    return Sketches(data[:n * stride * ew], sizes, ew, starts=st)
+
+
+def _exchange_start(own, n_genomes, world, rank, stride, ops, mode):
+    """Starts moving the sketches the cyclic plan needs, padded to `stride`
+    elements; returns wait(q) -> Sketches of rank q (q in peer_needs).  With
+    RCCL everything runs on the collective stream and wait(q) only orders
+    torch's current stream after q's data (the host does not block); with gloo
+    the data goes through host memory."""
     ew, dev = own.ew, own.data.device
     nccl = dist.get_backend() == "nccl"
-    bufs = []
-    for q in range(world):
-        if q == rank:
-            bufs.append((own.data, own.sizes))
+    bdev = dev if nccl else "cpu"
+    bpr = block_shard(n_genomes, world, rank)[0]
+    per = bpr * TILE  # genomes of a full rank
+    counts = [block_shard(n_genomes, world, q)[2] - block_shard(n_genomes, world, q)[1] for q in range(world)]
+    needs = peer_needs(n_genomes, world, rank)
+    # this rank's sketches at the common stride (a full rank's worth of rows for
+    # the all-gather; the rows past counts[rank] have size 0)
+    rows = per if mode == "allgather" else counts[rank]
+    send = torch.full((max(rows, 1) * stride * ew,), -1, dtype=torch.int64, device=dev)
+    send_sz = torch.zeros(max(rows, 1), dtype=torch.int32, device=dev)
+    if own.n:
+        ops.pad(own, stride, send, send_sz)
+    if not nccl:
+        send, send_sz = send.cpu(), send_sz.cpu()
+    got, works = {}, {}
+    if mode == "allgather":
+        full = torch.empty((world,) + tuple(send.shape), dtype=torch.int64, device=bdev)
+        full_sz = torch.empty((world, send_sz.numel()), dtype=torch.int32, device=bdev)
+        if nccl:
+            ws = [dist.all_gather_into_tensor(full, send, async_op=True),
+                  dist.all_gather_into_tensor(full_sz, send_sz, async_op=True)]
         else:
-            bufs.append((torch.empty(max(totals[q] * ew, 1), dtype=torch.int64, device=dev if nccl else "cpu"),
-                         torch.empty(max(ns[q], 1), dtype=torch.int32, device=dev if nccl else "cpu")))
-    works = []
-    for q in range(world):
-        d, sz = bufs[q]
-        nd, nz = totals[q] * ew, ns[q]
-        if not nccl and q == rank:
-            d, sz = d.cpu(), sz.cpu()
-        ws = []
-        for t, k in ((d, nd), (sz, nz)):
-            if k:  # every rank knows the sizes: all skip empty sources alike
-                ws.append(dist.broadcast(t[:k], src=q, async_op=nccl))
-        works.append(ws)
-        if not nccl:
-            bufs[q] = (d, sz)
+            dist.all_gather(list(full.unbind(0)), send)
+            dist.all_gather(list(full_sz.unbind(0)), send_sz)
+            ws = []
+        for q in needs:
+            got[q] = (full[q], full_sz[q, :counts[q]])
+            works[q] = ws
+    elif mode == "broadcast":
+        for q in range(world):
+            if not counts[q]:
+                continue
+            if q == rank:
+                d, sz = send, send_sz[:counts[q]]
+            else:
+                d = torch.empty(counts[q] * stride * ew, dtype=torch.int64, device=bdev)
+                sz = torch.empty(counts[q], dtype=torch.int32, device=bdev)
+            ws = [dist.broadcast(d, src=q, async_op=nccl), dist.broadcast(sz, src=q, async_op=nccl)]
+            if q in needs:
+                got[q], works[q] = (d, sz), ws if nccl else []
+    elif mode == "p2p":
+        # step d: send to rank - d (when its plan needs this rank), receive from
+        # rank + d (when this rank's plan needs it); every rank's step d is
+        # matched by its peers' step d, so the steps never wait on each other
+        for d in range(1, world):
+            to, frm = (rank - d) % world, (rank + d) % world
+            ops_d = []
+            if rank in peer_needs(n_genomes, world, to) and counts[rank]:
+                ops_d += [(dist.isend, send, to), (dist.isend, send_sz, to)]
+            if frm in needs:
+                rd = torch.empty(counts[frm] * stride * ew, dtype=torch.int64, device=bdev)
+                rsz = torch.empty(counts[frm], dtype=torch.int32, device=bdev)
+                ops_d += [(dist.irecv, rd, frm), (dist.irecv, rsz, frm)]
+                got[frm] = (rd, rsz)
+            if not ops_d:
+                continue
+            if nccl:
+                ws = dist.batch_isend_irecv([dist.P2POp(f, t, p) for f, t, p in ops_d])
+            else:
+                ws = [f(t, p) for f, t, p in ops_d]
+            if frm in needs:
+                works[frm] = ws
+            else:
+                for w in ws:  # gloo sends: done before the buffers go out of scope
+                    w.wait()
+    else:
+        raise ValueError(f"unknown exchange {mode!r}")
 
     def wait(q):
-        if q == rank:
-            return own
-        for w in works[q]:
-            if nccl and w is not None:
+        for w in works.get(q, []):
+            if w is not None:
                 w.wait()
-        d, sz = bufs[q]
+        works[q] = []
+        d, sz = got[q]
         if not nccl:
             d, sz = d.to(dev), sz.to(dev)
-        return Sketches(d[:totals[q] * ew], sz[:ns[q]], ew)
+        return _strided(d.reshape(-1), sz, ew, stride)
     return wait
 
 
 class JoinResult:
-    """What all_vs_all_join leaves on a rank.  tiles: int64 [T, 2] (None for one
-    rank without a process group, whose counts / ani are the dense n x n
-    matrices); counts: packed int32 [T, 64, 64]; ani: float64 [T, 2, 64, 64]
-    (both orientations, sks_ani_tiles) or dense, when asked; matrix: the n x n
-    int32 counts on the assembling rank(s), else None."""
+    """What all_vs_all_join leaves on a rank.  tiles: int64 [T, 2] of the tiles
+    this rank counted (None for one rank without a process group counting into
+    the dense matrix); counts: packed int32 [T, 64, 64] (or the dense n x n
+    matrix); ani: the n x n float64 matrix the join wrote the ANI of this rank's
+    tiles into (both orientations), when asked; matrix: the n x n int32 counts
+    on the assembling rank(s), else None.  check_layouts() (after the stream
+    has passed the call) raises if a join layout could not be built."""
 
     def __init__(self):
         self.tiles = self.counts = self.ani = self.matrix = None
+        self._stats = None
+
+    def check_layouts(self):
+        if self._stats is None:
+            return
+        torch.cuda.current_stream().synchronize()
+        bad = int(self._stats[:, 1].max()) if self._stats.numel() else 0
+        if bad:
+            raise RuntimeError("sks_dist: a join layout could not place a value group (adversarial 128-bit "
+                               "values); its counts are invalid — use sks_intersect_all")
 
 
-def _row_parts(nb, parts=6):
-    """Tile-row ranges [I0, I1) of an nb x nb upper triangle with about
-    T / parts tiles each (the early tile rows hold the most tiles)."""
-    T = nb * (nb + 1) // 2
-    target = max(1, -(-T // parts))
-    out, i0, acc = [], 0, 0
-    for i in range(nb):
-        acc += nb - i
-        if acc >= target or i == nb - 1:
-            out.append((i0, i + 1))
-            i0, acc = i + 1, 0
-    return out
-
-
-def _tiles_before(I, nb):
-    """Upper-triangle tiles (row-major) before tile row I."""
-    return I * nb - I * (I - 1) // 2
+def _all_tiles(nb):
+    I, J = np.triu_indices(nb)
+    return np.stack([I, J], axis=1).astype(np.int64)
 
 
 def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None,
-                    ani_host=None, pipelined=False, max_size=None):
+                    ani_out=None, max_size=None, size_bound=None, exchange="p2p"):
     """All-vs-all intersection counts (kmer_set.cpp:143-184 over the
     generate_all_pairs_from_vector list, generators.hpp:44-58), and ANI when
-    ani_ones (the k of binomial_estimator) is given.
+    ani_ones (the k of binomial_estimator) is given (kmer-sketching.cpp:195-200).
 
     mine: Sketches of this rank's block-aligned genomes (block_shard).
     ops: the kernels (GpuJoinOps on the GPU; a numpy restatement in the CPU
     tests): ew; bounds(src, log_b) -> group bounds tensor; build(src, log_b,
     bounds, key) -> layout (cached by key); count(n, log_b, rows, r_blk0, cols,
     c_blk0, tiles, out) — the contract of sks_intersect_layout_pair_tiles
-    (tiles None: every upper-triangle tile into the dense matrix out);
-    ani_matrix(counts, n, k); ani_tiles(tiles, packed, sizes, n, k).
+    (tiles None: every upper-triangle tile of one layout into the dense matrix
+    out); count_ani(..., out, sizes, k, ani) — the same with the ANI of every
+    counted pair written into the n x n matrix ani (sks_intersect_layout_ani);
+    pad(src, stride, data, sizes) — the sketches at a fixed stride.
     dst: the rank that assembles the n x n count matrix (None: none, "all":
-    every rank).  ani_host (one rank, no process group): a pinned host tensor of
-    n * n float64 that receives the ANI matrix (queued, not waited for);
-    pipelined: count in tile-row parts and copy each part's finished ANI rows
-    while later parts are counted (measured slower on config 4: DESIGN.md §6).
-    Returns a JoinResult."""
+    every rank).  ani_out: where the ANI goes (n * n float64: a device tensor
+    or pinned host memory, e.g. sksffi.HostBuffer — the join writes it; each
+    rank fills the cells of its own tiles); None with ani_ones: a new device
+    tensor.  max_size: the largest local sketch, known to the caller's host
+    (else one device reduction and a read-back).  size_bound: an upper bound of
+    every rank's sketch sizes that all ranks pass alike (bottom-s: s) — the
+    exchange then needs no size all-gather and no host round trip.  exchange:
+    "p2p", "allgather" or "broadcast" (see above).  Returns a JoinResult."""
     res = JoinResult()
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
     solo = _solo(world)
-    # the largest local sketch (max_size: known to the caller's host, e.g. from
-    # SketchSet.sizes(); else one device reduction and a read-back)
     mx = (int(max_size) if max_size is not None else int(mine.sizes.max().item())) if mine.n else 0
-    if solo:
-        ns, totals, mxs = [mine.n], [mine.total], [mx]
+    if size_bound is not None:
+        if mx > size_bound:
+            raise ValueError(f"all_vs_all_join: a local sketch holds {mx} > size_bound {size_bound} elements")
+        gmax = int(size_bound)
+    elif solo or world == 1:
+        gmax = mx
     else:
-        meta = _gather_flat(torch.tensor([mine.n, mine.total, mx], dtype=torch.int64, device=device), world)
-        meta = meta.view(world, 3).tolist()
-        ns, totals, mxs = [m[0] for m in meta], [m[1] for m in meta], [m[2] for m in meta]
-    log_b = log_b_for(max(max(mxs), 1))
+        gmax = _max_over(mx, world, device)  # one all-reduce and a read-back
+    log_b = log_b_for(max(gmax, 1))
+    fused = ani_ones is not None
+    if fused and ani_out is None:
+        ani_out = torch.zeros((n_genomes, n_genomes), dtype=torch.float64, device=device)
+    res.ani = ani_out if fused else None
+    stats_mark = ops.stats_mark() if hasattr(ops, "stats_mark") else None
     if solo:
         lay = ops.build(mine, log_b, None, "own")
-        out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
-        res.counts = res.matrix = out
-        if pipelined and ani_ones is not None and ani_host is not None and n_genomes and hasattr(ops, "count_range"):
-            # rows of tile rows [0, I) are final once those tile rows are counted
-            # (the row-major upper triangle; the mirror halves come from earlier
-            # rows): each part's ANI rows are computed and copied into ani_host on a
-            # copy stream while the next part's tiles are counted
-            n, nb = n_genomes, (n_genomes + TILE - 1) // TILE
-            res.ani = torch.empty((n, n), dtype=torch.float64, device=device)
-            copy = _copy_stream(device)
-            flat_d, flat_h = res.ani.view(-1), ani_host.view(-1)
-            for I0, I1 in _row_parts(nb):
-                ops.count_range(n, log_b, lay, _tiles_before(I0, nb), _tiles_before(I1, nb), out)
-                r0, r1 = I0 * TILE, min(n, I1 * TILE)
-                ops.ani_rows(out, n, r0, r1, ani_ones, res.ani)
-                ev = torch.cuda.Event()
-                ev.record()
-                copy.wait_event(ev)
-                with torch.cuda.stream(copy):
-                    flat_h[r0 * n:r1 * n].copy_(flat_d[r0 * n:r1 * n], non_blocking=True)
-            torch.cuda.current_stream().wait_stream(copy)
-            return res
-        if n_genomes:
-            ops.count(n_genomes, log_b, lay, 0, lay, 0, None, out)
-        if ani_ones is not None:
-            res.ani = ops.ani_matrix(out, n_genomes, ani_ones)
-            if ani_host is not None:
-                ani_host.view(-1).copy_(res.ani.view(-1), non_blocking=True)
+        if not fused:  # counts only: the dense matrix, both halves by the join
+            out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+            if n_genomes:
+                ops.count(n_genomes, log_b, lay, 0, lay, 0, None, out)
+            res.counts = res.matrix = out
+        else:
+            nb = (n_genomes + TILE - 1) // TILE
+            res.tiles = _all_tiles(nb)
+            res.counts = ops.parts(len(res.tiles), device)
+            if n_genomes:
+                ops.count_ani(n_genomes, log_b, lay, 0, lay, 0, None, res.counts, mine.sizes, ani_ones, ani_out)
+            if dst is not None:
+                out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+                res.matrix = place_tiles(out, res.tiles, res.counts, n_genomes)
+        if stats_mark is not None:
+            res._stats = ops.stats_since(stats_mark)
         return res
     # rank 0's group bounds, shared by every layout (blocks of different ranks
     # are joined bucket by bucket)
     gb = ops.bounds(mine, log_b) if rank == 0 else ops.bounds_like(log_b)
-    gb = _broadcast(gb, 0, world)
+    if world > 1:
+        gb = _broadcast(gb, 0, world)
     local, remote = tile_plan_by_peer(n_genomes, world, rank)
     T = len(local) + sum(len(r) for r in remote)
-    parts = torch.zeros((max(T, 1), TILE, TILE), dtype=torch.int32, device=device)
-    wait = _exchange_start(mine, ns, totals, world, rank)
+    parts = ops.parts(T, device)
+    sizes_all = torch.zeros(max(n_genomes, 1), dtype=torch.int32, device=device) if fused else None
+    if fused and mine.n:
+        sizes_all[g0:g1] = mine.sizes
+    wait = _exchange_start(mine, n_genomes, world, rank, max(gmax, 1), ops, exchange) if world > 1 else None
     own = ops.build(mine, log_b, gb, "own") if mine.n else None
-    if len(local):  # the rank's own tiles while the peers' sketches travel
-        ops.count(n_genomes, log_b, own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
-    off = len(local)
-    srcs = [None] * world
-    for q in range(world):
-        srcs[q] = wait(q)
-        tq = remote[q]
-        if q == rank or not len(tq):
-            continue
-        lq = ops.build(srcs[q], log_b, gb, ("peer", q))
-        bq = block_shard(n_genomes, world, q)[1] // TILE
-        if rank < q:
-            ops.count(n_genomes, log_b, own, g0 // TILE, lq, bq, tq, parts[off:off + len(tq)])
+
+    def count(rows, rb, cols, cb, tiles, out):
+        if fused:
+            ops.count_ani(n_genomes, log_b, rows, rb, cols, cb, tiles, out, sizes_all, ani_ones, ani_out)
         else:
-            ops.count(n_genomes, log_b, lq, bq, own, g0 // TILE, tq, parts[off:off + len(tq)])
+            ops.count(n_genomes, log_b, rows, rb, cols, cb, tiles, out)
+    if len(local):  # the rank's own tiles while the peers' sketches travel
+        count(own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
+    off = len(local)
+    order = []
+    for q in peer_needs(n_genomes, world, rank):
+        src = wait(q)
+        lq = ops.build(src, log_b, gb, ("peer", q))
+        bq = block_shard(n_genomes, world, q)[1] // TILE
+        tq = remote[q]
+        if fused:
+            sizes_all[bq * TILE:bq * TILE + src.n] = src.sizes
+        if rank < q:
+            count(own, g0 // TILE, lq, bq, tq, parts[off:off + len(tq)])
+        else:
+            count(lq, bq, own, g0 // TILE, tq, parts[off:off + len(tq)])
+        order.append(tq)
         off += len(tq)
-    res.tiles = np.concatenate([local] + list(remote)).reshape(-1, 2)
+    res.tiles = np.concatenate([local] + order).reshape(-1, 2)
     res.counts = parts[:T]
-    if ani_ones is not None:
-        sizes_all = torch.cat([srcs[q].sizes for q in range(world)])
-        res.ani = ops.ani_tiles(res.tiles, res.counts, sizes_all, n_genomes, ani_ones)
+    if stats_mark is not None:
+        res._stats = ops.stats_since(stats_mark)
     if dst is None:
         return res
-    plans = [tile_plan(n_genomes, world, q) for q in range(world)]
-    counts = [len(pl[0]) + len(pl[1]) for pl in plans]
+    plans = [_plan_in_count_order(n_genomes, world, q) for q in range(world)]
+    counts = [len(pl) for pl in plans]
     pad = torch.zeros((max(max(counts), 1), TILE, TILE), dtype=torch.int32, device=device)
     pad[:T] = res.counts
     gathered = _gather_tiles(pad, world, None if dst == "all" else dst)
     if gathered is None:
         return res
-    tiles = np.concatenate([np.concatenate(pl) for pl in plans]).reshape(-1, 2)
+    tiles = np.concatenate(plans).reshape(-1, 2)
     got = torch.cat([gathered[q, :counts[q]] for q in range(world)])
     out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
     res.matrix = place_tiles(out, tiles, got, n_genomes)
     return res
 
 
-_COPY_STREAMS = {}
-
-
-def _copy_stream(device):
-    """A high-priority side stream per device for device-to-host copies (HIP maps
-    streams onto four hardware queues; a normal-priority copy stream can land on
-    the compute stream's queue and wait behind its kernels: DESIGN.md §6)."""
-    key = str(device)
-    if key not in _COPY_STREAMS:
-        lo, hi = torch.cuda.Stream.priority_range()
-        _COPY_STREAMS[key] = torch.cuda.Stream(device=device, priority=hi)
-    return _COPY_STREAMS[key]
+def _plan_in_count_order(n_genomes, world, rank):
+    """The tiles of `rank` in the order all_vs_all_join counts them: its own,
+    then per peer in peer_needs order."""
+    local, remote = tile_plan_by_peer(n_genomes, world, rank)
+    return np.concatenate([local] + [remote[q] for q in peer_needs(n_genomes, world, rank)]).reshape(-1, 2)
 
 
 def _max_over(x, world, device):
@@ -546,12 +619,29 @@ class GpuJoinOps:
     and the k-mer width (ew = 1: u64, 2: 128-bit).  Layout buffers persist per
     build key across calls of the same shape; the context's HIP stream is
     ordered after torch's current stream before its kernels and torch's after
-    them, so a context on any stream works with the collectives on torch's."""
+    them, so a context on any stream works with the collectives on torch's.
+    Every layout build's status words are copied to a device log (no read-back;
+    JoinResult.check_layouts reads them after the join)."""
 
     def __init__(self, ctx, ew=1):
         import sksffi
         self.sksffi, self.ctx, self.ew = sksffi, ctx, ew
         self.bufs, self.tile_cache, self.keep = {}, {}, {}
+        self.stats = torch.zeros((16, 2), dtype=torch.int32, device="cuda")
+        self.n_stats = 0
+
+    def stats_mark(self):
+        """Starts a call's log of layout status words (the previous call's view
+        is overwritten from here on)."""
+        self.n_stats = 0
+        return 0
+
+    def stats_since(self, mark):
+        return self.stats[mark:self.n_stats]
+
+    def parts(self, T, device):
+        """Zeroed packed count tiles [T, 64, 64]."""
+        return torch.zeros((max(T, 1), TILE, TILE), dtype=torch.int32, device="cuda")
 
     def bounds_like(self, log_b):
         return torch.empty((self.sksffi.join_layout_groups(log_b) + 1) * self.ew, dtype=torch.int64, device="cuda")
@@ -580,9 +670,19 @@ class GpuJoinOps:
             self.ctx.join_layout_build(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
                                        log_b, *(t.data_ptr() for t in lay), stat=False, total=src.total,
                                        bounds=gb.data_ptr() if gb is not None else None, elem_words=self.ew)
+            if self.n_stats == self.stats.shape[0]:
+                self.stats = torch.cat([self.stats, torch.zeros_like(self.stats)])
+            self.ctx.join_layout_stat_copy(self.stats[self.n_stats].data_ptr())
+            self.n_stats += 1
             _torch_waits_for_ctx(self.ctx)
         self.keep[key] = (src, gb)  # alive until torch's stream is past the build
         return lay
+
+    def pad(self, src, stride, data, sizes):
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.sketches_export(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
+                                 data.data_ptr(), stride, sizes.data_ptr(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
 
     def _tiles(self, tiles):
         key = tiles.tobytes()  # the plan repeats every step: upload it once
@@ -605,36 +705,21 @@ class GpuJoinOps:
                                                  tl.shape[0], out.dim() == 3, out.data_ptr(), elem_words=self.ew)
         _torch_waits_for_ctx(self.ctx)
 
-    def count_range(self, n, log_b, lay, tile_begin, tile_end, out):
-        """Upper-triangle tiles [tile_begin, tile_end) of one layout, counts added
-        to the dense n x n matrix out (both halves)."""
-        _ctx_waits_for_torch(self.ctx)
-        self.ctx.intersect_layout_tiles(n, log_b, *(t.data_ptr() for t in lay), 0, 0, tile_begin, tile_end,
-                                        False, out.data_ptr(), elem_words=self.ew)
-        _torch_waits_for_ctx(self.ctx)
-
-    def ani_rows(self, counts, n, r0, r1, k, ani):
-        _ctx_waits_for_torch(self.ctx)
-        self.ctx.ani_rows(counts.data_ptr(), n, r0, r1, k, ani.data_ptr())
-        _torch_waits_for_ctx(self.ctx)
-
-    def ani_matrix(self, counts, n, k):
-        ani = torch.empty((n, n), dtype=torch.float64, device="cuda")
-        _ctx_waits_for_torch(self.ctx)
-        self.ctx.ani_matrix(counts.data_ptr(), n, k, ani.data_ptr())
-        _torch_waits_for_ctx(self.ctx)
-        return ani
-
-    def ani_tiles(self, tiles, packed, sizes, n, k):
-        out = torch.empty((len(tiles), 2, TILE, TILE), dtype=torch.float64, device="cuda")
-        if len(tiles):
+    def count_ani(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, out, sizes, k, ani):
+        """count + the ANI of every counted pair into ani (n * n float64: a device
+        tensor, or an object with .ptr — pinned host memory, sksffi.HostBuffer)."""
+        ani_ptr = ani.data_ptr() if hasattr(ani, "data_ptr") else ani.ptr
+        if tiles is None:
+            tl, t_end = None, self.sksffi.intersect_sym_tiles(n)
+        else:
             tl = self._tiles(tiles)
-            sz = sizes.to(device="cuda", dtype=torch.int32).contiguous()
-            _ctx_waits_for_torch(self.ctx)
-            self.ctx.ani_tiles(packed.data_ptr(), tl.data_ptr(), len(tiles), n, sz.data_ptr(), k, out.data_ptr())
-            _torch_waits_for_ctx(self.ctx)
-            self.keep["ani_sizes"] = sz
-        return out
+            t_end = tl.shape[0]
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.intersect_layout_ani(n, log_b, [t.data_ptr() for t in rows], r_blk0, [t.data_ptr() for t in cols],
+                                      c_blk0, tl.data_ptr() if tl is not None else 0, 0, t_end, out.dim() == 3,
+                                      out.data_ptr(), sizes.data_ptr(), k, ani_ptr, elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+        self.keep["ani_sizes"] = sizes
 
 
 def sketches_of(ss, ew=None):

@@ -63,6 +63,8 @@ EXPORTED = [
     "sks_join_layout_bounds", "sks_join_layout_groups", "sks_join_layout_boff_words",
     "sks_ctx_set_join_check", "sks_ctx_join_check_violations", "sks_intersect_layout_pair_tiles",
     "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_rows", "sks_ani_tiles",
+    "sks_intersect_layout_ani", "sks_host_alloc", "sks_host_free", "sks_join_layout_stat_copy",
+    "sks_sketches_export",
 ]
 
 _lib = None
@@ -135,6 +137,13 @@ def lib():
     L.sks_intersect_layout_pair_tiles.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int, vp, vp, vp, vp,
                                                   C.c_uint32, vp, vp, vp, vp, C.c_uint32, vp, C.c_uint64,
                                                   C.c_uint64, C.c_int, vp]
+    L.sks_intersect_layout_ani.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_uint32,
+                                           vp, vp, vp, vp, C.c_uint32, vp, C.c_uint64, C.c_uint64, C.c_int, vp,
+                                           vp, C.c_int, vp]
+    L.sks_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
+    L.sks_host_free.argtypes = [vp]
+    L.sks_join_layout_stat_copy.argtypes = [vp, vp]
+    L.sks_sketches_export.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp]
     L.sks_sketch_set_export_csr.argtypes = [vp, vp, vp]
     L.sks_ani_matrix.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, vp]
     L.sks_ani_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, vp, vp]
@@ -310,6 +319,32 @@ class Fasta:
         return out
 
 
+class HostBuffer:
+    """sks_host_alloc: coherent pinned host memory mapped for the devices (the
+    destination of sks_intersect_layout_ani); .array is a numpy view of it."""
+
+    def __init__(self, nbytes, dtype=np.float64):
+        p = C.c_void_p()
+        check(lib().sks_host_alloc(int(nbytes), C.byref(p)))
+        self.ptr = int(p.value or 0)
+        self.nbytes = int(nbytes)
+        n = self.nbytes // np.dtype(dtype).itemsize
+        self.array = (np.ctypeslib.as_array(C.cast(self.ptr, C.POINTER(C.c_uint8)), shape=(self.nbytes,))
+                      .view(dtype)[:n] if self.ptr else np.zeros(0, dtype=dtype))
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            check(lib().sks_host_free(C.c_void_p(self.ptr)))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 # ---- device ---------------------------------------------------------------------------------
 class Context:
     def __init__(self, device=0, stream=None):
@@ -351,6 +386,16 @@ class Context:
                                           C.c_void_p(out_bstart), C.byref(mx) if stat else None))
         return mx.value if stat else None
 
+    def sketches_export(self, data, starts, sizes, n, dst, stride, dst_sizes, elem_words=1):
+        """sks_sketches_export (device pointers): sketches padded to a fixed stride."""
+        check(lib().sks_sketches_export(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes), elem_words,
+                                        n, C.c_void_p(dst), stride, C.c_void_p(dst_sizes)))
+
+    def join_layout_stat_copy(self, d_dst):
+        """sks_join_layout_stat_copy: the last build's (max block bucket, invalid)
+        words into the device buffer d_dst (2 x u32), queued on the stream."""
+        check(lib().sks_join_layout_stat_copy(self.h, C.c_void_p(d_dst)))
+
     def join_layout_bounds(self, data_ptr, starts_ptr, sizes_ptr, n, log_b, out_bounds, elem_words=1):
         """sks_join_layout_bounds: the set's group bounds (device pointer out_bounds,
         (join_layout_groups(log_b) + 1) * elem_words words)."""
@@ -381,6 +426,18 @@ class Context:
                                                     *(C.c_void_p(p) for p in rows), r_blk0,
                                                     *(C.c_void_p(p) for p in cols), c_blk0, C.c_void_p(tiles),
                                                     tile_begin, tile_end, 1 if packed else 0, C.c_void_p(out)))
+
+    def intersect_layout_ani(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, tile_begin, tile_end, packed,
+                             out, sizes, kmer_num_ones, ani, elem_words=1):
+        """sks_intersect_layout_ani: intersect_layout_pair_tiles (tiles = 0: the
+        upper-triangle range of one layout) plus the ANI of every counted pair,
+        written by the join itself into `ani` (n * n float64; a device pointer or
+        pinned host memory from HostBuffer); sizes: device int32 |S_i|."""
+        check(lib().sks_intersect_layout_ani(self.h, n, log_b, elem_words, *(C.c_void_p(p) for p in rows), r_blk0,
+                                             *(C.c_void_p(p) for p in cols), c_blk0,
+                                             C.c_void_p(tiles) if tiles else None, tile_begin, tile_end,
+                                             1 if packed else 0, C.c_void_p(out), C.c_void_p(sizes),
+                                             kmer_num_ones, C.c_void_p(ani)))
 
     def ani_matrix(self, counts, n, kmer_num_ones, ani, cont=None):
         """sks_ani_matrix (device pointers): ANI of every ordered pair of the n x n counts."""

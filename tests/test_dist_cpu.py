@@ -1,10 +1,11 @@
-"""CPU (gloo, world_size 2 and 3): the multi-GPU orchestration of
-spaced-kmer-sketching_amd/sks_dist.py — genome / block sharding, the per-source
-sketch broadcasts and tile plan of all_vs_all_join, the padded-sketch gather of
+"""CPU (gloo, world_size 2 to 8): the multi-GPU orchestration of
+spaced-kmer-sketching_amd/sks_dist.py — genome / block sharding, the cyclic
+tile plan of all_vs_all_join and its three sketch exchanges (p2p send/recv,
+one all-gather, per-source broadcasts), the padded-sketch gather of
 all_vs_all, the seed sweep and the sharded genome — assembles exactly the
 single-process result.  The kernels are replaced by numpy restatements of the
-same contracts (sks_join_layout_build / sks_intersect_layout_pair_tiles /
-sks_ani_tiles, sks_intersect_sym)."""
+same contracts (sks_join_layout_build / sks_intersect_layout_ani /
+sks_sketches_export, sks_intersect_sym)."""
 import os
 import socket
 
@@ -222,29 +223,44 @@ class NpJoinOps:
         self.calls.append((r_blk0, c_blk0, len(tiles)))
         for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
             R, C = rows[I - r_blk0], cols[J - c_blk0]
-            for key, rv in R.items():
+            rm, cm = [], []
+            for key, rv in R.items():  # a value meets its partner only under the same bucket key
                 cv = C.get(key, {})
-                for v, rm in rv.items():
-                    cm = cv.get(v, 0)
-                    if not cm:
-                        continue
-                    for r in range(64):
-                        if rm >> r & 1:
-                            for c in range(64):
-                                if cm >> c & 1:
-                                    out[t, r, c] += 1
+                for v, m in rv.items():
+                    if cv.get(v, 0):
+                        rm.append(m)
+                        cm.append(cv[v])
+            if rm:  # every (row sketch, column sketch) pair of a shared value, as bit outer products
+                out[t] += torch.from_numpy((_bits(rm).T @ _bits(cm)).astype(np.int32))
 
-    def ani_tiles(self, tiles, packed, sizes, n, k):
-        out = torch.zeros((len(tiles), 2, 64, 64), dtype=torch.float64)
+    def count_ani(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, out, sizes, k, ani):
+        """count, then the ANI of both orientations of every counted pair into the
+        dense n x n matrix (the contract of sks_intersect_layout_ani)."""
+        self.count(n, log_b, rows, r_blk0, cols, c_blk0, tiles, out)
         for t, (I, J) in enumerate(np.asarray(tiles).reshape(-1, 2)):
             for r in range(64):
                 for c in range(64):
                     i, j = I * 64 + r, J * 64 + c
                     if i < n and j < n:
-                        x = int(packed[t, r, c])
-                        out[t, 0, r, c] = O.binomial_estimator(O.containment(x, int(sizes[i])), k)
-                        out[t, 1, c, r] = O.binomial_estimator(O.containment(x, int(sizes[j])), k)
-        return out
+                        x = int(out[t, r, c])
+                        ani[i, j] = O.binomial_estimator(O.containment(x, int(sizes[i])), k)
+                        ani[j, i] = O.binomial_estimator(O.containment(x, int(sizes[j])), k)
+
+    def parts(self, T, device):
+        return torch.zeros((max(T, 1), 64, 64), dtype=torch.int32)
+
+    def pad(self, src, stride, data, sizes):
+        """the sketches at a fixed stride, padded with ~0 words (sks_sketches_export)"""
+        st, sz = src.starts.tolist(), src.sizes.tolist()
+        for i in range(src.n):
+            a, m = st[i] * self.ew, sz[i] * self.ew
+            data[i * stride * self.ew:i * stride * self.ew + m] = src.data[a:a + m]
+        sizes[:src.n] = src.sizes
+
+
+def _bits(masks):
+    a = np.array(masks, dtype=np.uint64)
+    return ((a[:, None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(np.int64)
 
 
 def sks_dist_groups(log_b):
@@ -252,7 +268,7 @@ def sks_dist_groups(log_b):
     return 1 << (log_b - 3) if log_b > 3 else 1
 
 
-def _join_worker(rank, world, port, q, dst, n_genomes, ew):
+def _join_worker(rank, world, port, q, dst, n_genomes, ew, exchange, bound):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -263,14 +279,29 @@ def _join_worker(rank, world, port, q, dst, n_genomes, ew):
     src = sks_dist.Sketches(torch.from_numpy(flat.copy()), torch.tensor([len(x) for x in mine], dtype=torch.int32),
                             ew)
     ops = NpJoinOps(ew, rank)
-    res = sks_dist.all_vs_all_join(n_genomes, world, rank, src, ops, lambda m: 5, dst=dst, ani_ones=21)
+    res = sks_dist.all_vs_all_join(n_genomes, world, rank, src, ops, lambda m: 5, dst=dst, ani_ones=21,
+                                   exchange=exchange,
+                                   size_bound=max(len(x) for x in sk) + 3 if bound else None)
     q.put((rank, None if res.matrix is None else res.matrix.numpy(), ops.built, ops.calls,
            res.tiles, res.counts.numpy(), res.ani.numpy()))
     dist.destroy_process_group()
 
 
+def _sketches_n(n):
+    """n small related sketches (six families, 50-90 elements) for the N = 8 plans"""
+    m = O.mask(21, 21, 0)
+    out = []
+    for g in range(n):
+        seq = synth.bases(1200, seed=80 + g % 6, mut_seed=2000 + g, mut_rate=0.004 * (g % 5))
+        sk, _ = O.sketch(O.cut_runs(seq.tobytes()), 21, m, "bottom", 50 + (g % 5) * 10)
+        out.append(np.sort(sk[:, 0].astype(np.int64)))
+    return out
+
+
 def _join_sketches(n_genomes, ew):
     if ew == 1:
+        if n_genomes not in (N_GENOMES, N_200):
+            return [s.astype(np.uint64) for s in _sketches_n(n_genomes)]
         return [s.astype(np.uint64) for s in (_sketches() if n_genomes == N_GENOMES else _sketches_200())]
     m = O.mask(40, 30, 0)
     out = []
@@ -281,21 +312,28 @@ def _join_sketches(n_genomes, ew):
     return out
 
 
-@pytest.mark.parametrize("world,dst,n_genomes,ew", [(2, 0, N_GENOMES, 1), (3, "all", N_GENOMES, 1),
-                                                    (2, 1, 200, 1), (3, 0, 200, 1), (3, 0, 130, 2)])
-def test_all_vs_all_join_broadcasts_gloo(world, dst, n_genomes, ew):
+@pytest.mark.parametrize("world,dst,n_genomes,ew,exchange,bound", [
+    (2, 0, N_GENOMES, 1, "p2p", True), (3, "all", N_GENOMES, 1, "p2p", False),
+    (2, 1, 200, 1, "allgather", True), (3, 0, 200, 1, "broadcast", True), (3, 0, 200, 1, "p2p", True),
+    (3, 0, 130, 2, "allgather", False), (4, "all", 200, 1, "p2p", True), (8, 0, 600, 1, "p2p", True),
+    (8, 3, 600, 1, "allgather", False)])
+def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bound):
     """Ranks build the layout of their own block-aligned genomes with rank 0's
-    bounds, count their own blocks' tiles first, then — as each source rank's
-    broadcast sketches land — build that source's layout and count their share
-    of the tiles pairing the two (rows from the lower rank's blocks); the
-    packed tiles go to dst (every rank for "all"), whose matrix equals the
-    single-process merge counts; the per-tile ANI of both orientations equals
-    the reference formula.  n = 200 at world 3 leaves the last rank without
-    genomes; ew = 2 moves 128-bit (lo, hi) k-mers (w = 40)."""
+    bounds, count their own blocks' tiles first, then — as each peer's sketches
+    land (p2p send/recv, one all-gather, or per-source broadcasts; padded to the
+    caller's size bound, or to the all-reduced largest sketch) — build that
+    peer's layout and count the tiles of the cyclic plan pairing the two (rows
+    from the lower rank's blocks); the packed tiles go to dst (every rank for
+    "all"), whose matrix equals the single-process merge counts, and the ANI
+    each rank wrote for its tiles (both orientations) equals the reference
+    formula, every ordered pair written by exactly one rank.  n = 200 at world
+    3 and 4 leaves ranks without genomes; ew = 2 moves 128-bit (lo, hi) k-mers
+    (w = 40); world 8 over 600 genomes (10 blocks) is the N = 8 plan with
+    ragged block ranges."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes, ew))
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes, ew, exchange, bound))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -304,10 +342,11 @@ def test_all_vs_all_join_broadcasts_gloo(world, dst, n_genomes, ew):
         p.join(timeout=60)
         assert p.exitcode == 0
     sk = _join_sketches(n_genomes, ew)
-    want = np.array([[O.intersect(_w(sk[i]), _w(sk[j])) for j in range(n_genomes)] for i in range(n_genomes)])
+    want = _all_pairs(sk)
     sizes = [len(x) for x in sk]
     bnds = {b for r in range(world) for (_, _, b) in results[r][1]}
     assert len(bnds) == 1  # every layout on every rank used rank 0's bounds
+    written = np.zeros((n_genomes, n_genomes), np.int32)
     for r in range(world):
         mat, built, calls, tiles, counts, ani = results[r]
         if dst == "all" or r == dst:
@@ -317,23 +356,52 @@ def test_all_vs_all_join_broadcasts_gloo(world, dst, n_genomes, ew):
         loc, rem = sks_dist.tile_plan_by_peer(n_genomes, world, r)
         _, g0, _ = sks_dist.block_shard(n_genomes, world, r)
         expect = [(g0 // 64, g0 // 64, len(loc))] if len(loc) else []
-        for qq in range(world):
-            if len(rem[qq]):
-                bq = sks_dist.block_shard(n_genomes, world, qq)[1] // 64
-                expect.append((g0 // 64, bq, len(rem[qq])) if r < qq else (bq, g0 // 64, len(rem[qq])))
+        for qq in sks_dist.peer_needs(n_genomes, world, r):
+            bq = sks_dist.block_shard(n_genomes, world, qq)[1] // 64
+            expect.append((g0 // 64, bq, len(rem[qq])) if r < qq else (bq, g0 // 64, len(rem[qq])))
         assert calls == expect, (r, calls, expect)
+        # the cyclic plan: at most world // 2 peer layouts per rank
+        assert len([k for (k, _, _) in built if k != "own"]) <= world // 2
         for t, (I, J) in enumerate(tiles):
             for a, b in ((0, 0), (3, 7), (63, 62)):
                 i, j = I * 64 + a, J * 64 + b
                 if i < n_genomes and j < n_genomes:
                     assert counts[t, a, b] == want[i, j]
-                    assert ani[t, 0, a, b] == O.binomial_estimator(O.containment(int(want[i, j]), sizes[i]), 21)
-                    assert ani[t, 1, b, a] == O.binomial_estimator(O.containment(int(want[i, j]), sizes[j]), 21)
+            for a in range(64):
+                for b in range(64):
+                    i, j = I * 64 + a, J * 64 + b
+                    if i < n_genomes and j < n_genomes:
+                        written[i, j] += 1
+                        if I != J:
+                            written[j, i] += 1
+    assert (written == 1).all()  # every ordered pair counted (and its ANI written) by exactly one rank
+    # each rank's matrix holds the ANI of its own tiles' pairs (zero elsewhere)
+    full = sum(np.asarray(results[r][5]) for r in range(world))
+    want_ani = np.array([[O.binomial_estimator(O.containment(int(want[i, j]), sizes[i]), 21)
+                          for j in range(n_genomes)] for i in range(n_genomes)])
+    assert np.array_equal(full, want_ani)
 
 
 def _w(x):
     x = np.asarray(x, dtype=np.uint64)
     return x if x.ndim == 2 else np.stack([x, 0 * x], 1)
+
+
+def _all_pairs(sk):
+    """|S_i ∩ S_j| for all pairs of distinct-valued sketches: the value incidence
+    matrix times its transpose (checked against the oracle merge on a sample)."""
+    rows = [_w(x) for x in sk]
+    allv = np.concatenate(rows + [np.zeros((0, 2), np.uint64)])
+    uniq, inv = np.unique(allv, axis=0, return_inverse=True)
+    M = np.zeros((len(sk), len(uniq)), np.int64)
+    o = 0
+    for i, r in enumerate(rows):
+        M[i, inv.reshape(-1)[o:o + len(r)]] = 1
+        o += len(r)
+    want = M @ M.T
+    for i, j in ((0, 1), (len(sk) - 1, 0), (len(sk) // 2, len(sk) // 3)):
+        assert want[i, j] == O.intersect(rows[i], rows[j])
+    return want
 
 
 def test_block_shard_covers_whole_blocks():
@@ -421,7 +489,8 @@ def _sketches_200():
     return out
 
 
-@pytest.mark.parametrize("n,world", [(1000, 8), (1000, 3), (200, 3), (64, 2), (1, 4), (5000, 7)])
+@pytest.mark.parametrize("n,world", [(1000, 8), (1000, 4), (1000, 2), (1024, 8), (1000, 3), (200, 3), (64, 2),
+                                     (1, 4), (5000, 7), (600, 8)])
 def test_tile_plan_partitions_upper_triangle(n, world):
     for r in range(world):  # remote tiles by peer: rows in the lower rank's blocks
         _, rem = sks_dist.tile_plan_by_peer(n, world, r)
@@ -443,26 +512,12 @@ def test_tile_plan_partitions_upper_triangle(n, world):
             assert (I, J) not in seen
             seen[(I, J)] = r
     assert len(seen) == nb * (nb + 1) // 2
-    full = [s for r, s in enumerate(sizes) if sks_dist.block_shard(n, world, r)[2] -
-            sks_dist.block_shard(n, world, r)[1] == sks_dist.block_shard(n, world, r)[0] * 64]
-    if full:  # ranks holding whole block ranges get near-equal shares
-        assert max(full) - min(full) <= world
+    # the cyclic plan: a rank joins with at most world // 2 peers' layouts
+    for r in range(world):
+        assert len(sks_dist.peer_needs(n, world, r)) <= world // 2
+    full = all(sks_dist.block_shard(n, world, r)[2] - sks_dist.block_shard(n, world, r)[1] ==
+               sks_dist.block_shard(n, world, r)[0] * 64 for r in range(world))
+    if full:  # every rank holds a whole block range (config 4 at N = 1, 2, 4, 8): near-equal shares
+        assert max(sizes) - min(sizes) <= 1, sizes
 
 
-@pytest.mark.parametrize("nb", [1, 2, 3, 5, 16, 17, 40])
-def test_row_parts_finish_rows(nb):
-    """The pipelined one-rank ANI (sks_dist.all_vs_all_join ani_host) converts
-    and copies the rows of tile rows [I0, I1) after counting upper-triangle
-    tiles [tiles_before(I0), tiles_before(I1)): the parts cover every tile
-    once, in order, and when a part ends every tile a finished row needs —
-    (I, J) for J >= I and the mirrored (J, I) for J < I — has been counted."""
-    parts = sks_dist._row_parts(nb)
-    assert parts[0][0] == 0 and parts[-1][1] == nb
-    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
-    order = [(i, j) for i in range(nb) for j in range(i, nb)]  # intersect.hip sym_tile order
-    assert sks_dist._tiles_before(nb, nb) == len(order)
-    for I0, I1 in parts:
-        done = set(order[:sks_dist._tiles_before(I1, nb)])
-        for I in range(I0, I1):
-            for J in range(nb):
-                assert (min(I, J), max(I, J)) in done, (I0, I1, I, J)

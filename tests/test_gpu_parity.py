@@ -991,14 +991,17 @@ def test_config3_contig_against_oracle(torch_cuda, ctx):
     assert got.size == want.size and np.array_equal(got, want)
 
 
-def test_all_vs_all_join_ani_rows_to_host(torch_cuda, ctx):
-    """The one-rank all-vs-all with a host ANI buffer (sks_dist.all_vs_all_join
-    ani_host: tile-row parts, sks_ani_rows per part, copies on a side stream):
-    counts equal the oracle's, and the host ANI equals sks_ani_from_counts
-    (kmer-sketching.cpp:195-200, ani_estimation.cpp:24-42) within 1e-12."""
+def test_all_vs_all_join_fused_ani_to_host(torch_cuda, ctx):
+    """The one-rank all-vs-all with the ANI written by the join itself
+    (sks_intersect_layout_ani: the last workgroup of each tile converts it)
+    straight into pinned host memory — sksffi.HostBuffer (sks_host_alloc,
+    coherent) and a torch pinned tensor — and into device memory: counts equal
+    the oracle's, and every ANI equals sks_ani_from_counts
+    (kmer-sketching.cpp:195-200, ani_estimation.cpp:24-42) within 1e-12; rows
+    of the dense sks_ani_rows kernel agree too."""
     import sks_dist
     torch = torch_cuda
-    n = 300  # 5 blocks, ragged last block: 15 tiles in 5 row parts
+    n = 300  # 5 blocks, ragged last block: 15 tiles
     genomes = [synth.bases(2500 + 37 * (i % 13), seed=50 + i % 7, mut_seed=60 + i,
                            mut_rate=0.002 * (i % 5)).tobytes() for i in range(n)]
     w, k = 31, 21
@@ -1006,14 +1009,28 @@ def test_all_vs_all_join_ani_rows_to_host(torch_cuda, ctx):
     ss, _ = build(torch, ctx, genomes, w, m, "frac", 2)
     sk = [O.sketch(O.cut_runs(g), w, m, "frac", 2)[0] for g in genomes]
     ops = sks_dist.GpuJoinOps(ctx)
-    host = torch.empty(n * n, dtype=torch.float64, pin_memory=True)
-    res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
-                                   device="cuda", dst=None, ani_ones=k, ani_host=host, pipelined=True)
-    torch.cuda.synchronize()
-    got = res.matrix.cpu().numpy()
+    hb = sksffi.HostBuffer(n * n * 8)
+    hb.array[:] = -1.0
+    pinned = torch.full((n * n,), -1.0, dtype=torch.float64, pin_memory=True)
+    outs = []
+    for dst in (hb, pinned, None):
+        res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
+                                       device="cuda", dst=0, ani_ones=k, ani_out=dst)
+        torch.cuda.synchronize()
+        res.check_layouts()
+        outs.append(res)
+    got = outs[0].matrix.cpu().numpy()
     for i in range(0, n, 37):
         for j in range(0, n, 11):
             assert got[i, j] == O.intersect(sk[i], sk[j]), (i, j)
     size_first = np.repeat(np.diag(got).astype(np.int32), n)
     _, want = sksffi.ani_from_counts(got.reshape(-1), size_first, k)
-    assert np.abs(host.numpy() - want).max() <= 1e-12
+    assert np.abs(hb.array - want).max() <= 1e-12
+    assert np.abs(pinned.numpy() - want).max() <= 1e-12
+    assert np.abs(outs[2].ani.cpu().numpy().reshape(-1) - want).max() <= 1e-12
+    dense = torch.from_numpy(got.astype(np.int32)).cuda()
+    rows = torch.zeros((n, n), dtype=torch.float64, device="cuda")
+    ctx.ani_rows(dense.data_ptr(), n, 64, 200, k, rows.data_ptr())
+    torch.cuda.synchronize()
+    assert np.abs(rows.cpu().numpy()[64:200].reshape(-1) - want.reshape(n, n)[64:200].reshape(-1)).max() <= 1e-12
+    hb.free()

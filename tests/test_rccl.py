@@ -70,15 +70,15 @@ def _merge_counts(sk):
                      for i in range(n)], dtype=np.int64)
 
 
-@pytest.mark.parametrize("side_stream,w", [(False, W), (True, W), (False, 45)])
-def test_join_layout_all_vs_all_on_rccl(env, side_stream, w):
-    """sks_dist.all_vs_all_join through the collective branch on RCCL: the
-    metadata gather, rank 0's bounds broadcast, the per-source sketch / size
-    broadcasts (each joined as it lands), the packed tile gather to rank 0
-    (dist.gather), the matrix assembly and the per-tile device ANI — 130 genomes
-    (3 blocks, a ragged last one, an empty sketch), u64 and (w = 45) 128-bit
-    k-mers.  With side_stream the context's kernels run on a non-default HIP
-    stream: GpuJoinOps orders it against torch's stream both ways."""
+@pytest.mark.parametrize("side_stream,w,bound", [(False, W, True), (True, W, False), (False, 45, True)])
+def test_join_layout_all_vs_all_on_rccl(env, side_stream, w, bound):
+    """sks_dist.all_vs_all_join through the collective branch on RCCL: the size
+    all-reduce (without a size bound), the packed tile gather to rank 0
+    (dist.gather), the matrix assembly and the ANI the join writes into pinned
+    host memory — 130 genomes (3 blocks, a ragged last one, an empty sketch),
+    u64 and (w = 45) 128-bit k-mers.  With side_stream the context's kernels
+    run on a non-default HIP stream: GpuJoinOps orders it against torch's
+    stream both ways."""
     torch, dist, ctx = env
     import sks_dist
     n, s = 130, 600
@@ -98,19 +98,18 @@ def test_join_layout_all_vs_all_on_rccl(env, side_stream, w):
     stream = torch.cuda.Stream() if side_stream else None
     cctx = sksffi.Context(0, stream.cuda_stream) if side_stream else ctx
     ops = sks_dist.GpuJoinOps(cctx, ss.elem_words)
+    hb = sksffi.HostBuffer(n * n * 8)
     res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
-                                   device="cuda", dst=0, ani_ones=k)
+                                   device="cuda", dst=0, ani_ones=k, ani_out=hb,
+                                   size_bound=s if bound else None)
     torch.cuda.synchronize()
+    res.check_layouts()
     assert np.array_equal(res.matrix.cpu().numpy().astype(np.int64), want), side_stream
-    # per-tile ANI (both orientations) against the host formula on the oracle counts
-    ani = res.ani.cpu().numpy()
-    for t, (I, J) in enumerate(res.tiles):
-        for r, c in ((0, 0), (5, 9), (63, 1)):
-            i, j = I * 64 + r, J * 64 + c
-            if i < n and j < n:
-                for a, b, got in ((i, j, ani[t, 0, r, c]), (j, i, ani[t, 1, c, r])):
-                    want_ani = sksffi.binomial_estimator(sksffi.containment(int(want[a, b]), int(sizes[a])), k)
-                    assert abs(got - want_ani) <= 1e-9, (a, b)
+    # every ordered pair's ANI against the host formula on the oracle counts
+    size_first = np.repeat(sizes.astype(np.int32), n)
+    _, want_ani = sksffi.ani_from_counts(want.reshape(-1).astype(np.int32), size_first, k)
+    assert np.abs(hb.array - want_ani).max() <= 1e-9
+    hb.free()
     if side_stream:
         cctx.close()
 

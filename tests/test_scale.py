@@ -7,7 +7,9 @@ s=10000, counted all-vs-all through exactly the path bench.py times
 sks_intersect_sym_layout, world 1).  Checked: 8 genomes' sketches against the
 oracle (oracle/sks_oracle.cpp) on the same 5 Mb bytes; the whole 1000 x 1000
 count matrix against an independent host count of the exported sketches
-(sparse 0/1 membership product); symmetry and diagonal = sizes.
+(sparse 0/1 membership product); symmetry and diagonal = sizes; the ANI the
+join writes into pinned host memory against the host's.  The same at w = 45 /
+k = 30 (128-bit k-mers, the bench's pairs_wide leg).
 
 Config 5: mask seeds 0..7 over the first 200 genomes, per seed all-vs-all and
 ANI (kmer-sketching.cpp:185-200), consensus = mean over seeds through
@@ -86,12 +88,16 @@ def test_config4_all_vs_all_1000x5mb(env):
         want, nw = O.sketch(O.cut_runs(raw), bench.W, mask, "bottom", s)
         assert np.array_equal(ss.sketch(g), want), g
         assert int(ss.windows()[g]) == nw
-    # the bench's pair path, world 1: counts and device ANI
+    # the bench's pair path, world 1: counts, and the ANI the join writes into
+    # pinned host memory
     ones = bin(mask).count("1") // 2
+    hb = sksffi.HostBuffer(n * n * 8)
     res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), sks_dist.GpuJoinOps(ctx),
-                                   sksffi.join_layout_log_b, device="cuda", ani_ones=ones)
+                                   sksffi.join_layout_log_b, device="cuda", ani_ones=ones, ani_out=hb,
+                                   size_bound=s, max_size=int(sizes.max()))
     mat = res.matrix
     torch.cuda.synchronize()
+    res.check_layouts()
     got = mat.cpu().numpy().astype(np.int64)
     want = _host_counts(_exported(ss, n))
     assert np.array_equal(got, got.T)
@@ -103,9 +109,60 @@ def test_config4_all_vs_all_1000x5mb(env):
     # (kmer-sketching.cpp:195-200, ani_estimation.cpp:24-42): within 1e-9
     size_first = np.repeat(np.diag(got).astype(np.int32), n)
     _, host_ani = sksffi.ani_from_counts(got.reshape(-1), size_first, ones)
-    dev_ani = res.ani.cpu().numpy().reshape(-1)
+    dev_ani = hb.array.copy()
+    hb.free()
     assert np.abs(dev_ani - host_ani).max() <= 1e-9
     assert (dev_ani == host_ani).mean() > 0.99  # the device pow is within 1 ulp; nearly all bit-equal
+
+
+def _host_counts_wide(sketches):
+    """_host_counts for (lo, hi) 128-bit k-mers: rows over the union of values."""
+    import scipy.sparse as sp
+    n = len(sketches)
+    allv = np.ascontiguousarray(np.concatenate(sketches)).view(np.dtype((np.void, 16))).reshape(-1)
+    rows = np.repeat(np.arange(n), [len(s) for s in sketches])
+    _, inv = np.unique(allv, return_inverse=True)
+    M = sp.csr_matrix((np.ones(len(allv), np.int32), (rows, inv)), shape=(n, int(inv.max()) + 1))
+    return (M @ M.T).toarray().astype(np.int64)
+
+
+def test_config4_wide_all_vs_all_1000x5mb(env):
+    """Config 4 at w = 45 / k = 30 — a (k + 10, k) shape of the reference's sweep
+    (kmer-sketching.cpp:228-239), 128-bit k-mers — through the bench's
+    pairs_wide path (sks_dist.all_vs_all_join with GpuJoinOps(ew = 2): the
+    (lo, hi) join layout, k_join<2> and the fused ANI into pinned host memory):
+    4 genomes' sketches against the oracle, the whole 1000 x 1000 matrix
+    against a host count of the exported (lo, hi) sketches, every ANI within
+    1e-9 of the host's."""
+    torch, bench, ctx = env
+    import sks_dist
+    n, s, w, k = bench.C4_GENOMES, bench.C4_S, bench.C4W_W, bench.C4W_K
+    buf, seg = _genomes(torch, bench, ctx, n)
+    mask = sksffi.mask_generate(w, k, bench.MASK_SEED)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, w, mask, sksffi.SKS_BOTTOM_S, s)
+    assert ss.elem_words == 2
+    sizes = ss.sizes().copy()
+    assert (sizes == s).all()
+    for g in (0, 377, 640, 999):
+        raw = buf[seg[g]:seg[g + 1]].cpu().numpy().tobytes()
+        want, _ = O.sketch(O.cut_runs(raw), w, mask, "bottom", s)
+        assert np.array_equal(ss.sketch(g), want), g
+    ones = bin(mask).count("1") // 2
+    hb = sksffi.HostBuffer(n * n * 8)
+    res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), sks_dist.GpuJoinOps(ctx, 2),
+                                   sksffi.join_layout_log_b, device="cuda", ani_ones=ones, ani_out=hb,
+                                   size_bound=s, max_size=int(sizes.max()))
+    torch.cuda.synchronize()
+    res.check_layouts()
+    got = res.matrix.cpu().numpy().astype(np.int64)
+    want = _host_counts_wide([ss.sketch(i) for i in range(n)])
+    assert np.array_equal(np.diag(got), sizes.astype(np.int64))
+    assert np.array_equal(got, want)
+    assert got[0, 1] > 0 and got[0, 999] < 50
+    size_first = np.repeat(np.diag(got).astype(np.int32), n)
+    _, host_ani = sksffi.ani_from_counts(got.reshape(-1), size_first, ones)
+    assert np.abs(hb.array - host_ani).max() <= 1e-9
+    hb.free()
 
 
 def test_config5_seed_sweep_8x200x5mb(env):
