@@ -258,15 +258,18 @@ int sks_sketch_union_wide(sks_ctx* ctx, const uint64_t* d_in, uint64_t n, uint64
  * sks_join_layout_groups(log_b) value groups cut by bounds (G + 1 values of
  * elem_words words each, non-decreasing, bounds[0] = 0, bounds[G] = the
  * largest value), each split into 8 (or 2^log_b when log_b < 3) hash buckets;
- * 8 consecutive groups form a region (NR = regions per block).  A region's
- * entries start at its raw offset in the block (the block's sketch elements in
- * earlier regions), so its tail up to the next region is unused.  Exposing the
+ * 2^rg consecutive groups form a region (NR = regions per block; the build
+ * picks rg in 1..3 by its size: 8-group regions when the blocks give >= 1024
+ * of them, smaller ones for small builds).  A region's entries start at its
+ * raw offset in the block (the block's sketch elements in earlier regions),
+ * so its tail up to the next region is unused.  Exposing the
  * layout lets a multi-GPU caller build the layout of its own sketches only and
  * all-gather layouts instead of raw sketches (no replicated build):
  *   vals   u64[total * elem_words]  entry values, block-major (total = sum of sizes)
  *   masks  u64[total]               sketch mask of each entry
  *   boff   u32[nb * sks_join_layout_boff_words(log_b)]  per block (nb = ceil(n/64)):
  *          2^log_b bucket starts, then NR region ends, relative to bstart[block]
+ *          (room for G), and in the row's last word log2 of the buckets per region
  *   bstart u64[nb + 1]              raw block starts (prefix of the sizes); [nb] = total
  * Layouts of consecutive sketch ranges that each start at a multiple of 64 can
  * be concatenated (append vals/masks/boff and add the data offset to bstart)
@@ -279,7 +282,8 @@ uint32_t sks_join_layout_log_b(uint32_t max_sketch_size);
 uint32_t sks_join_layout_capacity(void);
 /* Value groups of a layout with 2^log_b buckets (bounds hold groups + 1 values). */
 uint32_t sks_join_layout_groups(uint32_t log_b);
-/* Words of one block's boff row: 2^log_b bucket starts + the region ends. */
+/* Words of one block's boff row: 2^log_b bucket starts + room for the region
+ * ends + the region size word. */
 uint32_t sks_join_layout_boff_words(uint32_t log_b);
 /* Group bounds balanced for the set (quantiles averaged over up to 64 sample
  * sketches), queued on the context stream.  Any bounds give exact counts. */
@@ -365,11 +369,13 @@ int sks_intersect_layout_ani(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_
  * d_sizes[i] must be <= stride (the caller's bound; larger sketches are cut). */
 int sks_sketches_export(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
                         int elem_words, uint32_t n, uint64_t* d_dst, uint64_t stride, uint32_t* d_dst_sizes);
-/* Pinned host memory the device reads and writes directly (coherent, mapped
- * into every device's address space): the destination of a fused ANI matrix.
- * No reference counterpart (the reference's result vectors are plain host
- * vectors, kmer-sketching.cpp:193). */
-int sks_host_alloc(uint64_t bytes, void** out);
+/* Pinned host memory the device reads and writes directly (mapped into every
+ * device's address space): the destination of a fused ANI matrix.  coherent:
+ * fine-grained (every device store goes to the host as issued); 0: coarse-
+ * grained (device stores are cached and written back by the end of the kernel,
+ * in whole lines).  No reference counterpart (the reference's result vectors
+ * are plain host vectors, kmer-sketching.cpp:193). */
+int sks_host_alloc(uint64_t bytes, int coherent, void** out);
 int sks_host_free(void* p);
 /* The set's sketches back to back (sizes[i] * elem_words words each, in order)
  * and its sizes, copied into caller device buffers (a send buffer). */

@@ -1681,12 +1681,14 @@ int sks_intersect_layout_ani(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_wo
   return SKS_OK;
 }
 
-int sks_host_alloc(uint64_t bytes, void** out) {
+int sks_host_alloc(uint64_t bytes, int coherent, void** out) {
   if (!out) return sks::fail(SKS_E_ARG, "sks_host_alloc: null out");
   *out = nullptr;
   if (!bytes) return SKS_OK;
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+  const unsigned flags = (coherent ? hipHostMallocCoherent : hipHostMallocNonCoherent) | hipHostMallocPortable |
+                         hipHostMallocMapped;
+  if (hipHostMalloc(&p, bytes, flags) != hipSuccess) {
     (void)hipGetLastError();
     return sks::fail(SKS_E_NOMEM, "sks_host_alloc: hipHostMalloc of " + std::to_string(bytes) + " bytes failed");
   }

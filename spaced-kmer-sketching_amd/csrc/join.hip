@@ -55,7 +55,12 @@ constexpr int kJB = 512;
 constexpr int kJCap = 1024;             // column entries per chunk (10-bit entry index)
 constexpr int kJMade = kJCap / kJB;     // column entries per thread per chunk
 constexpr int kJRowPf = 1536 / kJB;     // row entries per thread held in registers per chunk
-constexpr int kJWin = 1 << (jc::kGLog + jc::kRGLog);  // buckets per region (a window)
+// buckets per window: a workgroup stages the bucket offsets of 64 buckets at a
+// time; a window may hold several layout regions (each region's entries are
+// contiguous, with a gap before the next region: chunks map their entries
+// piecewise, at most kJPieces regions per chunk)
+constexpr int kJWinLog = 6, kJWin = 1 << kJWinLog;
+constexpr uint32_t kJPieces = 4;
 // 16 planes hold counts below 2^16 per workgroup; a carry out of the top plane
 // (a pair sharing >= 65536 values in one workgroup's buckets) is added to the
 // output directly
@@ -73,7 +78,7 @@ constexpr int kWaitVmcnt0 = 0x0F70;
 struct JoinArgs {
   JoinLayout r, c;          // row blocks (tile row I = block r_blk0 + I) and column blocks
   uint32_t r_blk0, c_blk0;  // (tile column J = block c_blk0 + J; uint32 arithmetic, -blk0 works)
-  uint32_t log_b, B, BW, rb_log, n, n_col_blocks, n_groups, buckets_per_group;
+  uint32_t log_b, B, BW, n, n_col_blocks, n_groups, buckets_per_group;
   int sym;
   uint32_t row_begin, row_end;
   uint64_t tile_begin;
@@ -97,23 +102,59 @@ struct JoinChunk {
   unsigned long long rm[kJRowPf];
 };
 
-template <int EW>
+// A chunk's entries in a window's "virtual" index space (the window's buckets
+// back to back, without the gaps between layout regions), mapped to block
+// positions piecewise: one piece per region the chunk touches (wave-uniform).
+struct Pieces {
+  uint32_t v1, v2, v3;      // virtual start of pieces 1..3 (~0u: no such piece)
+  uint32_t d0, d1, d2, d3;  // block position - virtual index, per piece
+};
+__device__ __forceinline__ uint32_t phys(const Pieces p, uint32_t k) {
+  return k + (k < p.v1 ? p.d0 : k < p.v2 ? p.d1 : k < p.v3 ? p.d2 : p.d3);
+}
+
+template <int EW, bool PIECES>
 __device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cvals,
                                            const unsigned long long* __restrict__ cmasks,
                                            const uint64_t* __restrict__ rvals,
                                            const unsigned long long* __restrict__ rmasks, uint32_t cs,
-                                           uint32_t ce, uint32_t rs, uint32_t re, int tid, JoinChunk<EW>& c) {
+                                           uint32_t ce, const Pieces cp, uint32_t rs, uint32_t re,
+                                           const Pieces rp, int tid, JoinChunk<EW>& c) {
+  // a chunk inside one region (the common case; a wave-uniform branch): the
+  // entries are contiguous, no per-element piece compares
+  if (!PIECES || cp.v1 == ~0u) {
+    const unsigned long long* cm = cmasks + cp.d0;
+    const uint64_t* cv = cvals + (uint64_t)cp.d0 * EW;
 #pragma unroll
-  for (int u = 0; u < kJMade; ++u) {
-    const uint32_t k = cs + tid + kJB * u;
-    c.cv[u] = k < ce ? kv_load<EW>(cvals, k) : KV{0, 0};
-    c.cm[u] = k < ce ? cmasks[k] : 0ull;
+    for (int u = 0; u < kJMade; ++u) {
+      const uint32_t k = cs + tid + kJB * u;
+      c.cv[u] = k < ce ? kv_load<EW>(cv, k) : KV{0, 0};
+      c.cm[u] = k < ce ? cm[k] : 0ull;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kJMade; ++u) {
+      const uint32_t k = cs + tid + kJB * u, q = phys(cp, k);
+      c.cv[u] = k < ce ? kv_load<EW>(cvals, q) : KV{0, 0};
+      c.cm[u] = k < ce ? cmasks[q] : 0ull;
+    }
   }
+  if (!PIECES || rp.v1 == ~0u) {
+    const unsigned long long* rm = rmasks + rp.d0;
+    const uint64_t* rv = rvals + (uint64_t)rp.d0 * EW;
 #pragma unroll
-  for (int u = 0; u < kJRowPf; ++u) {
-    const uint32_t k = rs + tid + kJB * u;
-    c.rv[u] = k < re ? kv_load<EW>(rvals, k) : KV{0, 0};
-    c.rm[u] = k < re ? rmasks[k] : 0ull;
+    for (int u = 0; u < kJRowPf; ++u) {
+      const uint32_t k = rs + tid + kJB * u;
+      c.rv[u] = k < re ? kv_load<EW>(rv, k) : KV{0, 0};
+      c.rm[u] = k < re ? rm[k] : 0ull;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kJRowPf; ++u) {
+      const uint32_t k = rs + tid + kJB * u, q = phys(rp, k);
+      c.rv[u] = k < re ? kv_load<EW>(rvals, q) : KV{0, 0};
+      c.rm[u] = k < re ? rmasks[q] : 0ull;
+    }
   }
 }
 
@@ -157,13 +198,21 @@ __device__ __forceinline__ uint32_t window_end(const uint32_t* off, uint32_t we,
   return (we & ((1u << rb_log) - 1)) == 0 ? off[B + ((we - 1) >> rb_log)] : off[we];
 }
 
-template <int EW, bool CHECK>
-__global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
+// PIECES = false: windows also end at every region end of either layout, so a
+// chunk is always contiguous (the kernel for layouts of 64-bucket regions,
+// where the piece code, never taken, still cost 8% of the join); true: windows
+// of 64 buckets across small regions, chunks mapped piecewise
+// three workgroups per CU (24 waves; LDS allows three): at most 80 VGPRs for
+// u64 values — a build of 82 dropped the kernel to two workgroups per CU and
+// ran 20% slower; 128-bit values need more registers and take two
+template <int EW, bool CHECK, bool PIECES>
+__global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
   __shared__ uint32_t s_slot[kFSlots];
   __shared__ uint64_t s_ev[kJCap * EW];          // staged column entries: values
   __shared__ unsigned long long s_em[kJCap];     // ... and column masks
   __shared__ unsigned long long s_pl[kPlanes * kTile];  // plane b of row r at [b * 64 + r]
-  __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];
+  __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];  // block positions of the window's buckets
+  __shared__ uint32_t s_rv[kJWin + 1], s_cv[kJWin + 1];      // ... and their virtual starts
   __shared__ uint8_t s_next[kJWin];
   __shared__ uint32_t s_self[kTile];
   __shared__ uint32_t s_top;  // planes used (the highest carry chain)
@@ -193,11 +242,14 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   const unsigned long long* cmasks = reinterpret_cast<const unsigned long long*>(a.c.masks) + cb;
   const uint32_t* roff = a.r.boff + (uint64_t)rblk * a.BW;
   const uint32_t* coff = a.c.boff + (uint64_t)cblk * a.BW;
+  // each layout's region bucket log (the last word of its boff rows): the
+  // regions of the row and the column block may differ in size
+  const uint32_t r_rb = roff[a.BW - 1], c_rb = coff[a.BW - 1];
   const uint32_t r_valid = min<uint32_t>(kTile, row_lim - row0);
   const unsigned long long rvm = r_valid >= 64 ? ~0ull : ((1ull << r_valid) - 1);
   // a tile on the diagonal: row block = column block of the same layout (rows
   // taken from a separate layout start off a block boundary, so never match)
-  const bool self_tile = row0 == col0 && a.r.vals == a.c.vals;
+  const bool self_tile = row0 == col0 && rblk == cblk && a.r.vals == a.c.vals;
 
   for (int i = tid; i < kFSlots / 4; i += kJB)
     reinterpret_cast<uint4*>(s_slot)[i] = make_uint4(kFFree, kFFree, kFFree, kFFree);
@@ -303,9 +355,9 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   const uint32_t b1 = min(a.B, b0 + a.buckets_per_group);
   if (self_tile) {
     // ---- diagonal tile: every entry's hits are its own mask ----------------------------------
-    for (uint32_t wb = b0; wb < b1;) {
-      const uint32_t we = min(b1, ((wb >> a.rb_log) + 1) << a.rb_log);
-      const uint32_t es = coff[wb], ee = window_end(coff, we, a.B, a.rb_log);
+    for (uint32_t wb = b0; wb < b1;) {  // one region (contiguous entries) at a time
+      const uint32_t we = min(b1, ((wb >> c_rb) + 1) << c_rb);
+      const uint32_t es = coff[wb], ee = window_end(coff, we, a.B, c_rb);
       for (uint32_t k0 = es; k0 < ee; k0 += 4 * kJB) {
         unsigned long long m[4];
 #pragma unroll
@@ -324,49 +376,104 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
 #pragma unroll
     for (int u = 0; u < kJMade; ++u) made[u] = kNoSlot;
     for (uint32_t wb = b0; wb < b1;) {
-      const uint32_t we = min(b1, ((wb >> a.rb_log) + 1) << a.rb_log);
+      uint32_t we = min(b1, ((wb >> kJWinLog) + 1) << kJWinLog);
+      if constexpr (!PIECES) we = min(we, min(((wb >> c_rb) + 1) << c_rb, ((wb >> r_rb) + 1) << r_rb));
       const uint32_t nw = we - wb;
       __syncthreads();  // previous window fully consumed
-      for (uint32_t i = tid; i <= nw; i += kJB) {
-        s_roff[i] = i < nw ? roff[wb + i] : window_end(roff, we, a.B, a.rb_log);
-        s_coff[i] = i < nw ? coff[wb + i] : window_end(coff, we, a.B, a.rb_log);
+      // the window's bucket positions and, by a wave scan of the bucket sizes,
+      // their virtual starts (wave 0: columns, wave 1: rows; nw <= 64)
+      if (tid < 128) {
+        const bool col = tid < 64;
+        const uint32_t i = (uint32_t)lane;
+        const uint32_t* off = col ? coff : roff;
+        const uint32_t rb = col ? c_rb : r_rb;
+        const uint32_t st = i < nw ? off[wb + i] : 0u;
+        const uint32_t len = i < nw ? window_end(off, wb + i + 1, a.B, rb) - st : 0u;
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)st);
+        const uint32_t incl = wave_scan(len);
+        uint32_t* sp = col ? s_coff : s_roff;
+        uint32_t* sv = col ? s_cv : s_rv;
+        if (i < nw) {
+          sp[i] = st;
+          sv[i + 1] = v0 + incl;
+        }
+        if (i == 0) sv[0] = v0;
       }
       __syncthreads();
-      // chunk ends: the most whole buckets from bucket i on that fit cap
+      // chunk ends: the most whole buckets from bucket i on that fit cap, within
+      // kJPieces regions
       for (uint32_t i = tid; i < nw; i += kJB) {
-        const uint32_t cs = s_coff[i];
-        uint32_t lo = i + 1, hi = nw;
+        const uint32_t cs = s_cv[i];
+        const uint32_t lim = min(nw, min((((wb + i) >> c_rb) + kJPieces) << c_rb,
+                                         (((wb + i) >> r_rb) + kJPieces) << r_rb) - wb);
+        uint32_t lo = i + 1, hi = lim;
         while (lo < hi) {
           const uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_coff[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
+          if (s_cv[mid] - cs <= a.cap) lo = mid; else hi = mid - 1;
         }
         s_next[i] = (uint8_t)lo;
       }
       __syncthreads();
+      // the pieces of buckets [bs, be) (window-relative) of a layout with
+      // regions of 2^rl buckets, wave-uniform, straight line (a loop filling the
+      // struct put it in scratch); a window inside one region of the layout
+      // (one_region: every large layout) maps virtual = block position
+      const bool c_one = (wb >> c_rb) == ((we - 1) >> c_rb), r_one = (wb >> r_rb) == ((we - 1) >> r_rb);
+      auto pieces = [&](const uint32_t* sp, const uint32_t* sv, uint32_t bs, uint32_t be, uint32_t rl, bool one) {
+        if (!PIECES || one) return Pieces{~0u, ~0u, ~0u, 0u, 0u, 0u, 0u};
+        const uint32_t f1 = min(nw, ((((wb + bs) >> rl) + 1) << rl) - wb);
+        Pieces p{~0u, ~0u, ~0u, sp[bs] - sv[bs], 0u, 0u, 0u};
+        if (f1 >= be) {  // inside one region
+          p.d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.d0);
+          return p;
+        }
+        const uint32_t f2 = min(nw, ((((wb + bs) >> rl) + 2) << rl) - wb);
+        const uint32_t f3 = min(nw, ((((wb + bs) >> rl) + 3) << rl) - wb);
+        p.v1 = f1 < be ? sv[f1] : ~0u;
+        p.d1 = f1 < be ? sp[f1] - sv[f1] : 0u;
+        p.v2 = f2 < be ? sv[f2] : ~0u;
+        p.d2 = f2 < be ? sp[f2] - sv[f2] : 0u;
+        p.v3 = f3 < be ? sv[f3] : ~0u;
+        p.d3 = f3 < be ? sp[f3] - sv[f3] : 0u;
+        p.v1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.v1);
+        p.v2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.v2);
+        p.v3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.v3);
+        p.d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.d0);
+        p.d1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.d1);
+        p.d2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.d2);
+        p.d3 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.d3);
+        return p;
+      };
       // chunks of whole buckets; a bucket above cap is cut into sub-chunks of
       // cap column entries, each joined with all of the bucket's row entries
       // (its column entries are distinct, so each hit is counted once)
       auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
       uint32_t bs = wb, be = chunk_end(wb);
-      uint32_t cs = s_coff[0], ce = min(s_coff[be - wb], cs + a.cap);
+      uint32_t cs = s_cv[0], ce = min(s_cv[be - wb], cs + a.cap);
+      Pieces cp = pieces(s_coff, s_cv, 0, be - wb, c_rb, c_one), rp = pieces(s_roff, s_rv, 0, be - wb, r_rb, r_one);
       JoinChunk<EW> cur;
-      join_fetch<EW>(cvals, cmasks, rvals, rmasks, cs, ce, s_roff[0], s_roff[be - wb], tid, cur);
+      join_fetch<EW, PIECES>(cvals, cmasks, rvals, rmasks, cs, ce, cp, s_rv[0], s_rv[be - wb], rp, tid, cur);
       while (bs < we) {
-        const uint32_t rs = s_roff[bs - wb], re = s_roff[be - wb];
+        const uint32_t rs = s_rv[bs - wb], re = s_rv[be - wb];
+        const Pieces crp = rp;  // this chunk's row pieces (the rows beyond the prefetch)
         __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);  // this chunk's entries have landed
         uint32_t nbs, nbe, ncs, nce;
-        if (ce < s_coff[be - wb]) {
+        if (ce < s_cv[be - wb]) {
           nbs = bs;
           nbe = be;
           ncs = ce;
         } else {
           nbs = be;
           nbe = nbs < we ? chunk_end(nbs) : nbs;
-          ncs = s_coff[nbs - wb];
+          ncs = s_cv[nbs - wb];
         }
-        nce = min(s_coff[nbe - wb], ncs + a.cap);
+        nce = min(s_cv[nbe - wb], ncs + a.cap);
         JoinChunk<EW> nxt;
-        if (nbs < we) join_fetch<EW>(cvals, cmasks, rvals, rmasks, ncs, nce, s_roff[nbs - wb], s_roff[nbe - wb], tid, nxt);
+        if (nbs < we) {
+          cp = pieces(s_coff, s_cv, nbs - wb, nbe - wb, c_rb, c_one);
+          rp = pieces(s_roff, s_rv, nbs - wb, nbe - wb, r_rb, r_one);
+          join_fetch<EW, PIECES>(cvals, cmasks, rvals, rmasks, ncs, nce, cp, s_rv[nbs - wb], s_rv[nbe - wb], rp, tid, nxt);
+        }
 
         // 0) free the previous chunk's slots (its probes are done: barrier below
         //    the probe loop) and stage this chunk's entries
@@ -430,11 +537,11 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
           rows_add(m ? rows : 0ull, m, false);
         }
         for (uint32_t k0 = rs + kJB * kJRowPf; k0 < re; k0 += kJB) {  // (rare) rows beyond the prefetch
-          const uint32_t k = k0 + tid;
-          const unsigned long long rows = k < re ? rmasks[k] & rvm : 0ull;
+          const uint32_t k = k0 + tid, q = PIECES ? phys(crp, k) : k;
+          const unsigned long long rows = k < re ? rmasks[q] & rvm : 0ull;
           unsigned long long m = 0;
           if (rows) {
-            const KV v = kv_load<EW>(rvals, k);
+            const KV v = kv_load<EW>(rvals, q);
             const uint32_t h = fp_slot<EW>(v);
             const uint32_t x0 = s_slot[h];
             if (x0 != kFFree) {
@@ -493,20 +600,25 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   }
   if (!a.ani) return;
   // ---- fused containment / ANI: the tile's last workgroup converts it --------------------------
-  // Every workgroup of the tile releases its count atomics (agent scope) before
-  // counting itself done; the one that completes the tile acquires and reads the
-  // tile's counts back with agent-scope loads (per-XCD L2s are not coherent), then
-  // writes both orientations of the tile's ANI: (r, c) with lanes over columns and
-  // (c, r) with lanes over rows, so every wave's stores are one contiguous 512-byte
-  // row segment of the n x n matrix (ani may be pinned host memory: PCIe writes).
-  __threadfence();
+  // The counts are only ever written by device-scope atomics, which every
+  // workgroup's result reaches at the device's coherence point (that is what
+  // makes the cross-XCD sums right).  So the hand-off needs no release / acquire
+  // fence — on gfx950 those write back and invalidate the whole XCD L2
+  // (buffer_wbl2 / buffer_inv sc1), and 4352 of them per call cost ~1 ms: every
+  // wave drains its atomics (s_waitcnt vmcnt(0)), the workgroup meets at a
+  // barrier, one lane counts the workgroup done, and the workgroup that completes
+  // the tile reads the counts back with sc1 loads (agent-scope atomic loads, past
+  // the non-coherent L2s).  It writes both orientations of the tile's ANI: (r, c)
+  // with lanes over columns and (c, r) with lanes over rows, so every wave's
+  // stores are one contiguous 512-byte row segment of the n x n matrix (ani may
+  // be pinned host memory: PCIe writes).
+  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
   __syncthreads();
   if (tid == 0)
-    s_top = __hip_atomic_fetch_add(a.tile_done + (t - a.tile_begin), 1u, __ATOMIC_ACQ_REL,
+    s_top = __hip_atomic_fetch_add(a.tile_done + (t - a.tile_begin), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT) + 1 == a.n_groups;
   __syncthreads();
   if (!s_top) return;
-  __threadfence();
   int32_t* s_cnt = reinterpret_cast<int32_t*>(s_slot);  // the table is free: 4096 counts
   for (uint32_t q = tid; q < (uint32_t)(kTile * kTile); q += kJB) {
     const uint32_t r = q / kTile, c = q % kTile, gr = row0 + r, gc = col0 + c;
@@ -532,7 +644,7 @@ __global__ __launch_bounds__(kJB) void k_join(JoinArgs a) {
   }
 }
 
-template <int EW, bool CHECK>
+template <int EW, bool CHECK, bool PIECES>
 hipError_t launch_join_slices(JoinArgs ja, uint64_t tile_begin, uint64_t tile_end, bool packed, int32_t* out,
                               uint32_t* tile_done, hipStream_t s) {
   const uint64_t tiles_per_launch = std::max<uint64_t>(1, kMaxGrid / ja.n_groups);
@@ -541,7 +653,7 @@ hipError_t launch_join_slices(JoinArgs ja, uint64_t tile_begin, uint64_t tile_en
     ja.tile_begin = t0;
     if (packed) ja.out = out + (t0 - tile_begin) * (uint64_t)(kTile * kTile);
     if (ja.ani) ja.tile_done = tile_done + (t0 - tile_begin);
-    hipLaunchKernelGGL((k_join<EW, CHECK>), dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
+    hipLaunchKernelGGL((k_join<EW, CHECK, PIECES>), dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -599,7 +711,6 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.log_b = log_b;
   ja.B = B;
   ja.BW = jc::lay_boff_words(log_b);
-  ja.rb_log = jc::lay_rb_log(log_b);
   ja.n = n;
   ja.n_col_blocks = n_cb;
   ja.sym = (sym || d_tiles) ? 1 : 0;
@@ -630,11 +741,21 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   const uint32_t groups = (uint32_t)std::min<uint64_t>(B, std::max<uint64_t>(1, want));
   ja.buckets_per_group = (B + groups - 1) / groups;
   ja.n_groups = (B + ja.buckets_per_group - 1) / ja.buckets_per_group;
-  if (ew == 1)
-    return check ? launch_join_slices<1, true>(ja, tile_begin, tile_end, packed, out, tile_done, s)
-                 : launch_join_slices<1, false>(ja, tile_begin, tile_end, packed, out, tile_done, s);
-  return check ? launch_join_slices<2, true>(ja, tile_begin, tile_end, packed, out, tile_done, s)
-               : launch_join_slices<2, false>(ja, tile_begin, tile_end, packed, out, tile_done, s);
+  // windows across regions (PIECES) unless both layouts have 64-bucket regions:
+  // known only for one layout covering all n sketches (the build picks its
+  // region size from its block count, join_layout_region_log); a tile list
+  // joins per-rank layouts, small ones
+  const bool big = !d_tiles && r_blk0 == 0 && c_blk0 == 0 && rows.vals == cols.vals &&
+                   jc::lay_rb_log(log_b, join_layout_region_log(n_cb, log_b)) >= (uint32_t)kJWinLog;
+  const bool pieces = !big;
+#define SKS_JOIN_LAUNCH(E, C, P) launch_join_slices<E, C, P>(ja, tile_begin, tile_end, packed, out, tile_done, s)
+  if (ew == 1) {
+    if (pieces) return check ? SKS_JOIN_LAUNCH(1, true, true) : SKS_JOIN_LAUNCH(1, false, true);
+    return check ? SKS_JOIN_LAUNCH(1, true, false) : SKS_JOIN_LAUNCH(1, false, false);
+  }
+  if (pieces) return check ? SKS_JOIN_LAUNCH(2, true, true) : SKS_JOIN_LAUNCH(2, false, true);
+  return check ? SKS_JOIN_LAUNCH(2, true, false) : SKS_JOIN_LAUNCH(2, false, false);
+#undef SKS_JOIN_LAUNCH
 }
 
 }  // namespace sks

@@ -16,8 +16,9 @@
 //   vals   u64[T * EW]  entry values (EW = 1: u64 k-mers, w <= 32; EW = 2:
 //                       (lo, hi) 128-bit k-mers, 32 < w <= 64)
 //   masks  u64[T]       sketch mask of each entry
-//   boff   u32[nb * (B + NR)]  per block: B bucket starts, then the NR region
-//                       ends, relative to bstart[blk]
+//   boff   u32[nb * BW]  per block (BW = lay_boff_words): B bucket starts,
+//                       then the NR region ends, relative to bstart[blk], and
+//                       in the row's last word the region bucket log
 //   bstart u64[nb + 1]  raw block starts (prefix of the sizes); bstart[nb] = T
 #pragma once
 #include <hip/hip_runtime.h>
@@ -35,20 +36,26 @@ namespace jc {
 
 // ---- layout geometry ----------------------------------------------------------------------
 constexpr uint32_t kGLog = 3;   // hash buckets per value group: 8
-#ifndef SKS_LAYOUT_RG_LOG
-#define SKS_LAYOUT_RG_LOG 3
-#endif
-constexpr uint32_t kRGLog = SKS_LAYOUT_RG_LOG;  // value groups per region: 8 (64 buckets)
+// value groups per region: 2^rg, rg in [0, kRGLogMax], chosen per build (a
+// large build takes 8-group regions, a small one smaller regions so its grid
+// fills the chip; layout.hip join_layout_build); the region bucket log is
+// stored in the last word of every block's boff row, so each layout tells the
+// join its own region size
+constexpr uint32_t kRGLogMax = 3;
 constexpr uint32_t kMaxLogB = 14;
 
 __host__ __device__ inline uint32_t lay_gb_log(uint32_t log_b) { return log_b < kGLog ? log_b : kGLog; }
 __host__ __device__ inline uint32_t lay_groups(uint32_t log_b) { return 1u << (log_b - lay_gb_log(log_b)); }
-// log2 of the buckets of one region
-__host__ __device__ inline uint32_t lay_rb_log(uint32_t log_b) {
-  return log_b < kGLog + kRGLog ? log_b : kGLog + kRGLog;
+// log2 of the buckets of one region of 2^rg groups
+__host__ __device__ inline uint32_t lay_rb_log(uint32_t log_b, uint32_t rg) {
+  return log_b < kGLog + rg ? log_b : kGLog + rg;
 }
-__host__ __device__ inline uint32_t lay_regions(uint32_t log_b) { return 1u << (log_b - lay_rb_log(log_b)); }
-__host__ __device__ inline uint32_t lay_boff_words(uint32_t log_b) { return (1u << log_b) + lay_regions(log_b); }
+__host__ __device__ inline uint32_t lay_regions(uint32_t log_b, uint32_t rg) {
+  return 1u << (log_b - lay_rb_log(log_b, rg));
+}
+// one block's boff row: B bucket starts, room for the region ends of the
+// finest regions (one group each), then the region bucket log
+__host__ __device__ inline uint32_t lay_boff_words(uint32_t log_b) { return (1u << log_b) + lay_regions(log_b, 0) + 1; }
 
 // ---- values -------------------------------------------------------------------------------
 // A k-mer of EW 64-bit words (hi = 0 when EW == 1).

@@ -37,6 +37,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "join_common.hpp"
 #include "sks_internal.hpp"
@@ -249,17 +250,27 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
 __device__ unsigned long long g_layout_check;  // SKS check build: dedup invariant violations
 
 #ifdef SKS_LAYOUT_STAMPS  // diagnostic build: cycles per k_gl_place phase (thread 0 of each workgroup)
+// slots 0-4: phase cycles, summed in registers and stored per workgroup at the
+// end (no atomics on the timed path); slots 5-9: event counts (atomics, rare)
+constexpr int kMaxStampWgs = 16384;
 __device__ unsigned long long g_layout_stamps[10];
+__device__ unsigned long long g_layout_stamps_wg[kMaxStampWgs * 5];
 #define LSTAMP(i)                                              \
   do {                                                         \
     if (threadIdx.x == 0) {                                    \
       const uint64_t t_ = __builtin_amdgcn_s_memtime();        \
-      atomicAdd(&g_layout_stamps[i], (unsigned long long)(t_ - st_last)); \
+      st_acc[i] += t_ - st_last;                               \
       st_last = t_;                                            \
     }                                                          \
   } while (0)
+#define LSTAMP_FLUSH()                                                                  \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < kMaxStampWgs)                                  \
+      for (int q_ = 0; q_ < 5; ++q_) g_layout_stamps_wg[blockIdx.x * 5 + q_] = st_acc[q_]; \
+  } while (0)
 #else
 #define LSTAMP(i) do {} while (0)
+#define LSTAMP_FLUSH() do {} while (0)
 #endif
 
 #ifndef SKS_PLACE_DIAG
@@ -271,7 +282,7 @@ constexpr int kRegPer = 12;                  // elements of its sketch per threa
 constexpr uint32_t kSkCap = kTPS * kRegPer;  // a group with a sketch holding more (48) takes the bucket passes
 constexpr int kSlowPer = kGCap / kPB;        // slice path: slice elements per thread
 constexpr uint32_t kSpt = kTab / kPB;        // table slots per thread in the emit scan (16)
-constexpr uint32_t kMaxRG = 1u << jc::kRGLog;
+constexpr uint32_t kMaxRG = 1u << jc::kRGLogMax;
 constexpr int kPassU = 4;                    // bucket passes: 64-element chunks loaded per round
 static_assert(kSpt % 4 == 0, "emit reads the slots as uint4");
 
@@ -462,7 +473,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
                                                   uint64_t* __restrict__ out_vals,
                                                   unsigned long long* __restrict__ out_masks,
                                                   uint32_t* __restrict__ out_boff, uint32_t* __restrict__ stat,
-                                                  uint32_t gcap) {
+                                                  uint32_t gcap, uint32_t rg) {
   __shared__ uint64_t s_key[kGCap * EW];
   __shared__ unsigned long long s_msk[kGCap];
   __shared__ uint32_t s_tab[kTab];
@@ -471,19 +482,21 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
   __shared__ uint32_t s_wsum[kPB / 64];
   __shared__ uint32_t s_bcnt[1u << jc::kGLog];
   __shared__ uint32_t s_full, s_pcnt, s_gd, s_qn, s_qd;
-  __shared__ uint32_t s_stk[2 * 72];  // slice path: (slice, level) work stack
+  __shared__ unsigned long long s_stk[2 * 72];  // slice path: (slice prefix, level) work stack (prefixes up to 64 bits)
 
   const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
-  const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b);
-  const uint32_t RG = (1u << jc::lay_rb_log(log_b)) >> gb_log;
+  const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b, rg), BW = jc::lay_boff_words(log_b);
+  const uint32_t RG = (1u << jc::lay_rb_log(log_b, rg)) >> gb_log;
   const uint32_t blk = blockIdx.x / NR, r = blockIdx.x % NR;
   // the wave index in an SGPR: the per-wave loop bounds stay scalar
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SKS_LAYOUT_STAMPS
   uint64_t st_last = __builtin_amdgcn_s_memtime();
+  uint64_t st_acc[5] = {0, 0, 0, 0, 0};
 #endif
   const uint32_t s_end = min((uint32_t)kTile, count - kTile * blk);
-  uint32_t* boff = out_boff + (uint64_t)blk * (B + NR);
+  uint32_t* boff = out_boff + (uint64_t)blk * BW;
+  if (r == 0 && threadIdx.x == 0) boff[BW - 1] = jc::lay_rb_log(log_b, rg);  // the join reads the region size here
   const uint64_t base = bstart[blk];
   const bool sv = (uint32_t)lane < s_end;
   const uint64_t stt = sv ? starts[kTile * blk + lane] : 0;
@@ -729,7 +742,8 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
           for (;;) {
             const uint32_t depth = s_qd;
             if (depth == 0) break;
-            const uint32_t q = s_stk[2 * (depth - 1)], lvl = s_stk[2 * (depth - 1) + 1];
+            const uint64_t q = s_stk[2 * (depth - 1)];
+            const uint32_t lvl = (uint32_t)s_stk[2 * (depth - 1) + 1];
             __syncthreads();
             if (tid == 0) {
               s_qd = depth - 1;
@@ -744,7 +758,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
               const uint64_t sts = __shfl(stt, s);
               for (uint32_t e = a + lane; e < b; e += 64) {
                 const KV x = kv_load<EW>(data, sts + e);
-                if ((kv_mix<EW>(x) >> (64 - lvl)) == (uint64_t)q) {
+                if ((kv_mix<EW>(x) >> (64 - lvl)) == q) {
                   const uint32_t idx = atomicAdd(&s_qn, 1u);
                   if (idx < gcap) {
                     if constexpr (EW == 1) s_key[idx] = x.lo;
@@ -774,7 +788,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
               __syncthreads();
               continue;
             }
-            const uint32_t bq = (uint32_t)((uint64_t)q >> (lvl - gb_log));  // the slice's bucket
+            const uint32_t bq = (uint32_t)(q >> (lvl - gb_log));  // the slice's bucket
             if (bq != bk_cur) {  // first slice of a bucket
               if (bk_cur != ~0u) maxb = max(maxb, cur - bk_start);
               bk_cur = bq;
@@ -825,6 +839,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
     }
   }
   if (tid == 0) boff[B + r] = cur;
+  LSTAMP_FLUSH();
   // the largest block-bucket: one word for every workgroup; the stat only
   // grows, so a workgroup whose maximum is not above the value it reads skips
   // the atomic (one word takes ~88 atomics per microsecond)
@@ -887,7 +902,7 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
                                                    uint64_t* __restrict__ out_vals,
                                                    unsigned long long* __restrict__ out_masks,
                                                    uint32_t* __restrict__ out_boff, uint32_t* __restrict__ stat,
-                                                   uint32_t gcap) {
+                                                   uint32_t gcap, uint32_t rg) {
   __shared__ unsigned long long s_vt[kVT];  // values (0: empty)
   __shared__ unsigned long long s_vm[kVT];  // their sketch masks
   __shared__ uint32_t s_pos[(kMaxRG + 1) * kTile];
@@ -899,15 +914,17 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
   __shared__ uint32_t s_w8[(1u << jc::kGLog) * (kPB / 64)];  // pass emit: per-bucket wave totals
 
   const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
-  const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b);
-  const uint32_t RG = (1u << jc::lay_rb_log(log_b)) >> gb_log;
+  const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b, rg), BW = jc::lay_boff_words(log_b);
+  const uint32_t RG = (1u << jc::lay_rb_log(log_b, rg)) >> gb_log;
   const uint32_t blk = blockIdx.x / NR, r = blockIdx.x % NR;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SKS_LAYOUT_STAMPS
   uint64_t st_last = __builtin_amdgcn_s_memtime();
+  uint64_t st_acc[5] = {0, 0, 0, 0, 0};
 #endif
   const uint32_t s_end = min((uint32_t)kTile, count - kTile * blk);
-  uint32_t* boff = out_boff + (uint64_t)blk * (B + NR);
+  uint32_t* boff = out_boff + (uint64_t)blk * BW;
+  if (r == 0 && threadIdx.x == 0) boff[BW - 1] = jc::lay_rb_log(log_b, rg);  // the join reads the region size here
   const uint64_t base = bstart[blk];
   const bool sv = (uint32_t)lane < s_end;
   const uint64_t stt = sv ? starts[kTile * blk + lane] : 0;
@@ -933,6 +950,7 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
   GroupView gv = group_view(s_pos, s_pos + kTile, sv, stt, lane, my_s);
   group_load<1>(data, gv, sub, v);
   uint32_t dshare = 1u << 16;  // distinct / raw of the region's last placed group (16.16)
+  LSTAMP(0);
 
   // emit of a pass (thread t reads slots [8 t, 8 t + 8)): the pass's table holds
   // the values of buckets [q0, q0 + span) (a slice of one bucket when span = 1)
@@ -1043,6 +1061,7 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
           h[k] = (uint32_t)((gb_log ? m << gb_log : m) >> (64 - kVLog));  // (the bits after the bucket)
           if (e < gj.gc && v[k].lo != 0ull && bk[k] - blo < bn) x0[k] = atomicCAS(&s_vt[h[k]], 0ull, v[k].lo);
         }
+        LSTAMP(1);
         bool full = false;
         uint32_t rep[kRegPer];
 #pragma unroll
@@ -1234,9 +1253,11 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (p.span == 1) maxb = max(maxb, cur - bk_start);
       }
       dshare = (uint32_t)(((uint64_t)(cur - cur0) << 16) / gn_j);
+      LSTAMP(4);
     }
   }
   if (tid == 0) boff[B + r] = cur;
+  LSTAMP_FLUSH();
   if (wave == 0) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxb = max(maxb, (uint32_t)__shfl_xor(maxb, o, 64));
@@ -1246,6 +1267,18 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
 }
 
 }  // namespace
+
+uint32_t join_layout_region_log(uint32_t n_blk, uint32_t log_b) {
+  // region size: 8 groups when the grid fills the chip at 8 groups per
+  // workgroup (1024 or more workgroups), else fewer, down to 2, so a small
+  // build (a rank's own blocks, config 5's four blocks) is not one long
+  // sequence of groups per workgroup on a few CUs (SKS_LAYOUT_RG forces one)
+  static const char* force = getenv("SKS_LAYOUT_RG");
+  if (force) return std::min<uint32_t>(jc::kRGLogMax, (uint32_t)atoi(force));
+  uint32_t rg = jc::kRGLogMax;
+  while (rg > 1 && (uint64_t)n_blk * jc::lay_regions(log_b, rg) < 1024) --rg;
+  return rg;
+}
 
 uint32_t join_layout_groups(uint32_t log_b) { return jc::lay_groups(log_b); }
 uint32_t join_layout_boff_words(uint32_t log_b) { return jc::lay_boff_words(log_b); }
@@ -1300,7 +1333,12 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   // in every sketch, then the placement: a workgroup per (block, region)
   const uint32_t nb_bounds = d_bounds ? 0 : (G + 1 + kPT / 64 - 1) / (kPT / 64);
   const uint64_t* bounds = d_bounds ? d_bounds : bounds_tmp;
-  const dim3 grid_place(n_blk * jc::lay_regions(log_b));
+  // region size: 8 groups when the grid fills the chip at 8 groups per
+  // workgroup (1024 or more workgroups), else fewer, down to 2, so a small
+  // build (a rank's own blocks, config 5's four blocks) is not one long
+  // sequence of groups per workgroup on a few CUs (SKS_LAYOUT_RG forces one)
+  const uint32_t rg = join_layout_region_log(n_blk, log_b);
+  const dim3 grid_place(n_blk * jc::lay_regions(log_b, rg));
   auto* masks = reinterpret_cast<unsigned long long*>(out_masks);
   if (ew == 1) {
     hipLaunchKernelGGL(k_gl_prep<1>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
@@ -1308,20 +1346,20 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
     hipLaunchKernelGGL(k_gl_pos<1>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
     if (check)
       hipLaunchKernelGGL((k_gl_place1<true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), rg);
     else
       hipLaunchKernelGGL((k_gl_place1<false>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), rg);
   } else {
     hipLaunchKernelGGL(k_gl_prep<2>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
                        bounds_tmp, nb_bounds, out_bstart);
     hipLaunchKernelGGL(k_gl_pos<2>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
     if (check)
       hipLaunchKernelGGL((k_gl_place<2, true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), rg);
     else
       hipLaunchKernelGGL((k_gl_place<2, false>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
-                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap());
+                         out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), rg);
   }
 #ifdef SKS_LAYOUT_STAMPS
   {
@@ -1330,9 +1368,14 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_layout_stamps), sizeof h);
     const unsigned long long z[10] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_layout_stamps), z, sizeof z);
-    const double wgs = (double)grid_place.x;
-    fprintf(stderr, "[k_gl_place stamps] cycles per workgroup: setup+first load %.0f P1+next map+loads %.0f P2 %.0f "
-            "P3+P4 %.0f bucket passes / slow %.0f | groups in passes %llu (fat %llu, above cap %llu, full %llu), "
+    const uint32_t nw = std::min<uint32_t>(grid_place.x, kMaxStampWgs);
+    std::vector<unsigned long long> wg((size_t)nw * 5);
+    (void)hipMemcpyFromSymbol(wg.data(), HIP_SYMBOL(g_layout_stamps_wg), wg.size() * 8);
+    for (uint32_t b = 0; b < nw; ++b)
+      for (int q = 0; q < 5; ++q) h[q] += wg[(size_t)b * 5 + q];
+    const double wgs = (double)nw;
+    fprintf(stderr, "[k_gl_place stamps] cycles per workgroup: setup %.0f load wait+first CAS %.0f chains %.0f "
+            "emit %.0f passes %.0f | groups in passes %llu (fat %llu, above cap %llu, full %llu), "
             "pass splits %llu (%.0f workgroups)\n",
             h[0] / wgs, h[1] / wgs, h[2] / wgs, h[3] / wgs, h[4] / wgs, h[8], h[5], h[6], h[7], h[9], wgs);
   }

@@ -189,6 +189,8 @@ uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch 
 // d_stat[1] counts groups the build could not place (layout invalid).  Three
 // launches, no host synchronisation.
 uint32_t join_layout_groups(uint32_t log_b);
+// log2 of the value groups per region a build of n_blk blocks uses (1..3)
+uint32_t join_layout_region_log(uint32_t n_blk, uint32_t log_b);
 uint32_t join_layout_boff_words(uint32_t log_b);  // B + NR: one block's boff row
 hipError_t join_layout_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                               uint32_t count, uint32_t log_b, int ew, uint64_t* bounds, hipStream_t s);

@@ -140,7 +140,7 @@ def lib():
     L.sks_intersect_layout_ani.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_uint32,
                                            vp, vp, vp, vp, C.c_uint32, vp, C.c_uint64, C.c_uint64, C.c_int, vp,
                                            vp, C.c_int, vp]
-    L.sks_host_alloc.argtypes = [C.c_uint64, C.POINTER(vp)]
+    L.sks_host_alloc.argtypes = [C.c_uint64, C.c_int, C.POINTER(vp)]
     L.sks_host_free.argtypes = [vp]
     L.sks_join_layout_stat_copy.argtypes = [vp, vp]
     L.sks_sketches_export.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp]
@@ -320,12 +320,13 @@ class Fasta:
 
 
 class HostBuffer:
-    """sks_host_alloc: coherent pinned host memory mapped for the devices (the
-    destination of sks_intersect_layout_ani); .array is a numpy view of it."""
+    """sks_host_alloc: pinned host memory mapped for the devices (the destination
+    of sks_intersect_layout_ani), coherent (fine-grained) or not; .array is a
+    numpy view of it."""
 
-    def __init__(self, nbytes, dtype=np.float64):
+    def __init__(self, nbytes, dtype=np.float64, coherent=False):
         p = C.c_void_p()
-        check(lib().sks_host_alloc(int(nbytes), C.byref(p)))
+        check(lib().sks_host_alloc(int(nbytes), 1 if coherent else 0, C.byref(p)))
         self.ptr = int(p.value or 0)
         self.nbytes = int(nbytes)
         n = self.nbytes // np.dtype(dtype).itemsize

@@ -1,6 +1,6 @@
 # whole all-pairs call timings (config 4 family / unrelated, config-5 size) per variant, then kernel times
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/pt
+O=$R/gpurun_out/var
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for tag in "$@"; do

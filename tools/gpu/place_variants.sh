@@ -1,7 +1,7 @@
 # k_gl_place / k_join kernel time per library variant (kernel trace of tools/bench_pairs.py, 2 reps):
 #   bash tools/gpu/place_variants.sh base diag2 ...
 R=${GRAFT_REPO_ROOT:-/root/repo}
-O=$R/gpurun_out/pv
+O=$R/gpurun_out/var
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for tag in "$@"; do
