@@ -36,6 +36,7 @@ workload (rank 0, N=1 only).
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -456,13 +457,13 @@ def host_info(threads):
             "cpu_model": model, "thread_cap": "min(16, affinity): the box's CPU share"}
 
 
-def _codes_lens(seq_bytes):
+def _codes_lens(seq_bytes, w=W):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     runs = pyoracle.cut_runs(seq_bytes)
     codes = np.frombuffer(b"".join(runs), dtype=np.uint8)
     lens = np.array([len(r) for r in runs], dtype=np.uint64)
-    windows = int(sum(max(0, int(L) - W + 1) for L in lens))
+    windows = int(sum(max(0, int(L) - w + 1) for L in lens))
     return codes, lens, windows
 
 
@@ -485,19 +486,19 @@ def cpu_baseline_c2(host_genome, mask, gpu_sketch):
             "host": host_info(1)}
 
 
-def cpu_sketch_many(host_genomes, mask, kind, param, threads):
+def cpu_sketch_many(host_genomes, mask, kind, param, threads, w=W):
     """Reference-style port over genomes, `threads` workers over genomes (the
     reference's cilk_for over files, kmer_set.cpp:112-133). Returns (sets, windows, s)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from concurrent.futures import ThreadPoolExecutor
-    prepared = [_codes_lens(g) for g in host_genomes]
+    prepared = [_codes_lens(g, w) for g in host_genomes]
 
     def one(i):
         codes, lens, _ = prepared[i]
         if kind == "bottom":
-            return pyoracle.refport_bottom_codes(codes, lens, W, mask, param)
-        return pyoracle.refport_sketch_codes(codes, lens, W, mask, param)
+            return pyoracle.refport_bottom_codes(codes, lens, w, mask, param)
+        return pyoracle.refport_sketch_codes(codes, lens, w, mask, param)
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
         sets = list(ex.map(one, range(len(prepared))))
@@ -669,7 +670,7 @@ def c4_genome_seeds(g):
     return 100 + anc, 1000 + g, desc * 0.001
 
 
-def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100):
+def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100, w=W):
     """Reference-faithful pair phase on the host (oracle/ref_port.cpp: unordered_map
     kmer_sets, probe-the-larger intersection, threads over pairs like the
     reference's cilk_for, kmer_set.cpp:23-41,167-184) over all ordered pairs of
@@ -680,9 +681,9 @@ def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     T = cpu_threads()
-    ss = ctx.sketch_build(buf.data_ptr(), seg[n_sets], seg[:n_sets + 1], W, mask,
+    ss = ctx.sketch_build(buf.data_ptr(), seg[n_sets], seg[:n_sets + 1], w, mask,
                           sksffi.SKS_BOTTOM_S, C4_S)
-    sets = [pyoracle.refport_set_from_elems(ss.sketch(i), W, mask) for i in range(n_sets)]
+    sets = [pyoracle.refport_set_from_elems(ss.sketch(i), w, mask) for i in range(n_sets)]
     ones = bin(mask).count("1") // 2
     t0 = time.perf_counter()
     got = pyoracle.refport_all_pairs(sets, threads=T)
@@ -695,26 +696,27 @@ def cpu_baseline_pairs(ctx, buf, seg, mask, counts, n_sets=100):
     return {"value": n_sets * n_sets / dt, "unit": "ordered pairs/s (count + containment + ANI)", "cores": T,
             "kind": "port",
             "sample": f"all {n_sets}x{n_sets} ordered pairs of the first {n_sets} genomes "
-                      f"(s={C4_S}), oracle/ref_port.cpp, {T} threads over pairs + serial ANI, {dt:.2f} s; "
+                      f"(s={C4_S}, w={w}: {'128' if w > 32 else '64'}-bit k-mers in heap bitsets), "
+                      f"oracle/ref_port.cpp, {T} threads over pairs + serial ANI, {dt:.2f} s; "
                       f"counts equal the GPU's",
             "host": host_info(T)}
 
 
-def cpu_baseline_c4_sketch(ctx, buf, seg, mask):
+def cpu_baseline_c4_sketch(ctx, buf, seg, mask, w=W):
     """Config 4's sketch phase on the host: the reference-style port over a
     bounded sample of the genomes, one worker thread per host core over genomes
     (the reference's cilk_for over files, kmer_set.cpp:112-133); every sampled
     set is checked equal to the GPU's."""
     T = cpu_threads()
     n = min(len(seg) - 1, 4 * T)
-    ss = ctx.sketch_build(buf.data_ptr(), seg[n], seg[:n + 1], W, mask, sksffi.SKS_BOTTOM_S, C4_S)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[n], seg[:n + 1], w, mask, sksffi.SKS_BOTTOM_S, C4_S)
     host = [buf[seg[i]:seg[i + 1]].cpu().numpy().tobytes() for i in range(n)]
-    sets, windows, dt = cpu_sketch_many(host, mask, "bottom", C4_S, T)
+    sets, windows, dt = cpu_sketch_many(host, mask, "bottom", C4_S, T, w=w)
     for i in range(n):
         assert np.array_equal(sets[i].elems(), ss.sketch(i)), f"config-4 CPU set {i} differs"
     return {"value": windows / dt, "unit": "k-mers/s", "cores": T, "kind": "port",
             "sample": f"{n} of the {C4_GENOMES} config-4 genomes (5 Mb each, {windows} windows, "
-                      f"bottom-s {C4_S}), oracle/ref_port.cpp bottom_runs, {T} threads over "
+                      f"w={w}, bottom-s {C4_S}), oracle/ref_port.cpp bottom_runs, {T} threads over "
                       f"genomes, {dt:.2f} s; sets equal to the GPU's",
             "host": host_info(T)}
 
@@ -824,9 +826,9 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
         assert (counts == counts.T).all() and counts[0, 1] > 0
         assert (np.diag(counts) == sizes).all()
     cpu = cpu_sk = None
-    if cpu_pairs and rank == 0 and solo and w == W:
-        cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts)
-        cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask)
+    if cpu_pairs and rank == 0 and solo:
+        cpu = cpu_baseline_pairs(ctx, buf, seg, mask, counts, w=w)
+        cpu_sk = cpu_baseline_c4_sketch(ctx, buf, seg, mask, w=w)
     ani_bytes = int(covered.sum()) * 8
     return {
         "metric": "genome-pairs ANI/s", "value": C4_GENOMES * C4_GENOMES / t_pairs,
@@ -848,7 +850,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
             "pairs_this_rank": C4_GENOMES * C4_GENOMES / world,
             "achieved_GBps": (8 * 2 * C4_S + 4) * C4_GENOMES * C4_GENOMES / world / (k_ms * 1e-3) / 1e9
             if k_ms else None},
-        "roofline": pairs_lds_roofline(k_ms) if solo and w == W else None,
+        "roofline": pairs_lds_roofline(k_ms, "pair_lds.json" if w == W else "pair_lds_wide.json") if solo else None,
         "sketch_kmers_per_s": C4_GENOMES * (C4_LEN - w + 1) / t_sketch,
         "ani_mean_all_pairs": ani_mean,
         "config": {"workload": "config4 all-vs-all", "genomes": C4_GENOMES,
@@ -865,6 +867,174 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),
         "ms_end_to_end": (t_sketch + t_pairs) * 1e3,
     }
+
+
+# ---- the reference's own flow: main's 62 (w, k) configurations --------------------------
+REF_SWEEP_GENOMES, REF_SWEEP_CPU_GENOMES = 64, 16
+REF_SWEEP_CPU_CONFIGS = ((21, 21), (31, 31), (45, 35), (50, 40))
+
+
+def ref_sweep_configs():
+    """kmer-sketching.cpp:218-238: (10,10); (k,k) k = 11..40; (k+10,k) k = 10..40."""
+    return [(10, 10)] + [(k, k) for k in range(11, 41)] + [(k + 10, k) for k in range(10, 41)]
+
+
+def _fasta_files(ctx, n, d):
+    """The first n config-4 genomes as FASTA files (80-column lines) in d."""
+    files = []
+    dev = torch.empty(C4_LEN, dtype=torch.uint8, device="cuda")
+    for g in range(n):
+        a, m, r = c4_genome_seeds(g)
+        ctx.synth_bases(dev.data_ptr(), C4_LEN, a, m, r)
+        seq = dev.cpu().numpy().tobytes()
+        path = os.path.join(d, f"g{g:03d}.fa")
+        with open(path, "wb") as f:
+            f.write(b">syn_%d_0\n" % g)
+            f.write(b"\n".join(seq[i:i + 80] for i in range(0, len(seq), 80)) + b"\n")
+        files.append(path)
+    return files
+
+
+def cpu_ref_sweep(files, configs):
+    """The reference's per-configuration flow on the host (kmer-sketching.cpp:151-212)
+    for a bounded sample: every file parsed again (the reference re-reads its
+    files per configuration, :168; oracle/sks_oracle.cpp's restatement of
+    fasta_processing.cpp), sketched with sketching_condition (c = 200) by the
+    reference-faithful port, threads over files (kmer_set.cpp:112-133); every
+    ordered pair counted, threads over pairs (kmer_set.cpp:167-184); ANI serial
+    (:195-200).  Returns per-config (sketch s, compare s, windows, counts)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from concurrent.futures import ThreadPoolExecutor
+    T = cpu_threads()
+    out = []
+    for w, k in configs:
+        m = pyoracle.mask(w, k, 0)
+        ones = bin(m).count("1") // 2
+
+        def one(path):
+            runs = pyoracle.fasta_runs(path)
+            codes = np.frombuffer(b"".join(runs), dtype=np.uint8)
+            lens = np.array([len(r) for r in runs], dtype=np.uint64)
+            nw = int(sum(max(0, int(L) - w + 1) for L in lens))
+            return pyoracle.refport_sketch_codes(codes, lens, w, m, 200), nw
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(T) as ex:
+            res = list(ex.map(one, files))
+        t1 = time.perf_counter()
+        sets = [r[0] for r in res]
+        counts = pyoracle.refport_all_pairs(sets, threads=T)
+        sz = np.diag(counts)
+        ani = [pyoracle.binomial_estimator(pyoracle.containment(int(counts[i, j]), int(sz[i])), ones)
+               for i in range(len(files)) for j in range(len(files))]
+        t2 = time.perf_counter()
+        out.append({"w": w, "k": k, "sketch_s": t1 - t0, "compare_s": t2 - t1,
+                    "windows": sum(r[1] for r in res), "counts": counts, "ani": ani})
+    return out, T
+
+
+def run_ref_sweep(ctx, cpu=False):
+    """The reference's own workload (kmer-sketching.cpp:214-239, main): its 62
+    (w, k) configurations — 36 of them at w <= 32 (u64 k-mers), 26 at w > 32
+    (128-bit) — each sketching every file (FracMinHash c = 200, the reference's
+    sketching_condition, :29-34) and comparing all ordered pairs into ANI and
+    the CSV, run by this engine's drop-in driver bin/kmer-sketching (the facade:
+    sks::genome_batch parses the files once on the device and keeps them in HBM,
+    then sketch + all-pairs per configuration) on 64 config-4 genome files.  The
+    driver prints the reference's two timing lines per configuration; the CPU
+    baseline runs the same flow, reference-style, on the first 16 files for 4
+    configurations, and its ANI equals the CSV's for those pairs."""
+    import subprocess
+    import tempfile
+    n = REF_SWEEP_GENOMES
+    d = tempfile.mkdtemp(prefix="sks_refsweep_", dir="/tmp")
+    try:
+        files = _fasta_files(ctx, n, d)
+        torch.cuda.synchronize()
+        exe = os.path.join(PKG, "bin", "kmer-sketching")
+        out_csv = os.path.join(d, "out.csv")
+        t0 = time.perf_counter()
+        p = subprocess.run([exe, out_csv] + files, capture_output=True, text=True, timeout=900)
+        wall = time.perf_counter() - t0
+        if p.returncode != 0:
+            raise RuntimeError(f"bin/kmer-sketching failed ({p.returncode}): {p.stderr[-2000:]}")
+        sk = [float(l.split("=")[1].split()[0]) for l in p.stdout.splitlines() if "Time taken for sketching" in l]
+        cp = [float(l.split("=")[1].split()[0]) for l in p.stdout.splitlines() if "Time taken for comparison" in l]
+        cfg = ref_sweep_configs()
+        assert len(sk) == len(cp) == len(cfg), (len(sk), len(cp))
+        rows = sum(1 for _ in open(out_csv)) - 1
+        assert rows == len(cfg) * n * n, rows
+        narrow = [i for i, (w, _) in enumerate(cfg) if w <= 32]
+        wide = [i for i, (w, _) in enumerate(cfg) if w > 32]
+        wins = {i: n * (C4_LEN - w + 1) for i, (w, _) in enumerate(cfg)}
+
+        def part(ix):
+            s, c = sum(sk[i] for i in ix), sum(cp[i] for i in ix)
+            return {"configs": len(ix), "sketch_ms_per_config": s / len(ix), "compare_ms_per_config": c / len(ix),
+                    "sketch_kmers_per_s": sum(wins[i] for i in ix) / (s * 1e-3),
+                    "compare_pairs_per_s": len(ix) * n * n / (c * 1e-3)}
+        res = {"metric": "reference sweep (kmer-sketching main), 62 (w, k) configs",
+               "genomes": n, "genome_len": C4_LEN, "pairs_per_config": n * n,
+               "driver": "spaced-kmer-sketching_amd/bin/kmer-sketching (the reference main on the facade)",
+               "wall_s": wall, "csv_rows": rows,
+               "sketch_ms_total": sum(sk), "compare_ms_total": sum(cp),
+               "w_le_32": part(narrow), "w_gt_32": part(wide),
+               "note": "per-configuration times are the driver's own 'Time taken for sketching / comparison' "
+                       "lines (kmer-sketching.cpp:174-175, 202-203 on the same boundaries); the files are parsed "
+                       "once, on the device, before the first configuration (the reference re-parses them per "
+                       "configuration); wall_s includes process start, that parse and the CSV writing"}
+        if cpu:
+            csel = REF_SWEEP_CPU_CONFIGS
+            cres, T = cpu_ref_sweep(files[:REF_SWEEP_CPU_GENOMES], csel)
+            # the GPU's CSV values for the same pairs (6 significant digits, the
+            # reference's default ostream formatting) equal the CPU's ANI
+            vals = {}
+            want_rows = {}
+            for c in cres:
+                ci = cfg.index((c["w"], c["k"]))
+                for i in range(REF_SWEEP_CPU_GENOMES):
+                    for j in range(REF_SWEEP_CPU_GENOMES):
+                        want_rows[1 + ci * n * n + i * n + j] = (c["ani"][i * REF_SWEEP_CPU_GENOMES + j])
+            with open(out_csv) as f:
+                for ln, line in enumerate(f):
+                    if ln in want_rows:
+                        vals[ln] = line.split(",")[2]
+            bad = [ln for ln, a in want_rows.items() if vals[ln] != f"{a:.6g}"]
+            assert not bad, f"{len(bad)} CSV values differ from the CPU flow's, e.g. row {bad[0]}"
+            g = REF_SWEEP_CPU_GENOMES
+            per = []
+            for c in cres:
+                ci = cfg.index((c["w"], c["k"]))
+                per.append({"w": c["w"], "k": c["k"], "cpu_sketch_ms": c["sketch_s"] * 1e3,
+                            "cpu_compare_ms": c["compare_s"] * 1e3,
+                            "cpu_sketch_kmers_per_s": c["windows"] / c["sketch_s"],
+                            "cpu_compare_pairs_per_s": g * g / c["compare_s"],
+                            "gpu_sketch_kmers_per_s": wins[ci] / (sk[ci] * 1e-3),
+                            "gpu_compare_pairs_per_s": n * n / (cp[ci] * 1e-3)})
+            # projected reference-style host time of the whole sweep on the 64 files,
+            # from the sampled rates (sketch per window, compare per pair)
+            rk = {32: [], 64: []}
+            for x in per:
+                rk[32 if x["w"] <= 32 else 64].append(x)
+            proj = 0.0
+            for i, (w, _) in enumerate(cfg):
+                xs = rk[32 if w <= 32 else 64]
+                ks = statistics.mean(x["cpu_sketch_kmers_per_s"] for x in xs)
+                ps = statistics.mean(x["cpu_compare_pairs_per_s"] for x in xs)
+                proj += wins[i] / ks + n * n / ps
+            res["cpu_baseline"] = {
+                "kind": "port", "cores": T,
+                "sample": f"the first {g} of the {n} files, configurations {list(csel)}: per configuration every file "
+                          f"parsed again, sketched (oracle/ref_port.cpp, c = 200, {T} threads over files) and every "
+                          f"ordered pair counted ({T} threads over pairs) + serial ANI; ANI equal to the GPU CSV's",
+                "per_config": per,
+                "projected_sweep_s_64_files": proj,
+                "gpu_sweep_s_64_files": (sum(sk) + sum(cp)) * 1e-3,
+                "host": host_info(T)}
+        return res
+    finally:
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
 
 
 # ---- config 5 ------------------------------------------------------------------------
@@ -1043,39 +1213,50 @@ def scan_valu_roofline(kernel_ms):
     insts = t["sq_insts_valu_per_launch"]
     achieved = insts / (kernel_ms * 1e-3)
     peak = SIMDS / (t["mean_ns_per_valu_per_simd"] * 1e-9)
+    hw = t.get("valu_inst_per_simd_cycle")
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "VALU wave-instructions/s",
             "frac": achieved / peak, "valu_per_window": t["valu_per_window"],
+            # the hardware's count: VALU instructions issued per SIMD per cycle of the
+            # profiled launch (SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM cycles)); a
+            # wave64 VALU op holds its SIMD 2 (add/xor) to 4+ (64-bit mul/shift) cycles
+            "hw_valu_inst_per_simd_cycle": hw,
+            "hw_valu_busy_at_mix": hw * t["mean_cycles_per_valu"] if hw else None,
             "hot_block_valu": t["hot_block_valu"], "mean_cycles_per_valu": t["mean_cycles_per_valu"],
             "source": src,
             "note": "SQ_INSTS_VALU per launch (PMC) / live kernel time, against 1024 SIMDs at the hot "
                     "block's cycle-weighted mix (profiles/r01/isa_rates_microbench.txt)"}
 
 
-def pairs_lds_roofline(kernel_ms):
-    """k_join's LDS bound: LDS wave-instructions per all-pairs call (PMC,
-    profiles/rNN/pair_lds.json) over the live kernel time, against 256 CUs x
-    2.4 GHz x the microbench's fastest random LDS rate.  Null when the profile
-    was measured on other join sources."""
+def pairs_lds_roofline(kernel_ms, name="pair_lds.json"):
+    """k_join's LDS roofline from the hardware's own busy counter: LDS-array
+    cycles per all-pairs call (SQ_LDS_IDX_ACTIVE, PMC, profiles/rNN/<name>;
+    summed over the CUs, bank-conflict cycles included) over the live kernel
+    time, against every CU's LDS busy every cycle (256 CUs x the clock measured
+    in the same profile, GRBM_GUI_ACTIVE / 8 XCDs / profiled time).  Beside it:
+    LDS wave-instructions per call and the conflict share.  Null when the
+    profile was measured on other join sources."""
     import srchash
-    path = latest_profile_json("pair_lds.json")
+    path = latest_profile_json(name)
     if not path or not kernel_ms:
-        return {"note": "no profiles/rNN/pair_lds.json"}
+        return {"note": f"no profiles/rNN/{name}"}
     t = json.load(open(path))
     src = os.path.relpath(path, ROOT)
-    if t.get("join_source_hash") != srchash.join_hash() or not t.get("sq_insts_lds_per_call"):
+    if t.get("join_source_hash") != srchash.join_hash() or not t.get("sq_lds_idx_active_per_call"):
         return {"note": f"stale: {src} measured on join sources {t.get('join_source_hash')}, "
                         f"these are {srchash.join_hash()}", "source": src}
-    insts = t["sq_insts_lds_per_call"]
-    achieved = insts / (kernel_ms * 1e-3)
-    peak = CUS * PEAK_CLK_GHZ * 1e9 * LDS_PEAK_WAVE_INST_PER_CLK_CU
+    act = t["sq_lds_idx_active_per_call"]
+    clk = t["grbm_gui_active_per_call"] / 8 / (t["profiled_ms"] * 1e-3)  # Hz under the profiled load
+    achieved = act / (kernel_ms * 1e-3)
+    peak = CUS * clk
     conf = t.get("sq_lds_bank_conflict_per_call")
-    act = t.get("sq_lds_idx_active_per_call")
-    return {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "LDS wave-instructions/s",
-            "frac": achieved / peak, "lds_insts_per_call": insts,
+    return {"bound": "lds", "achieved": achieved, "peak": peak, "unit": "LDS-array cycles/s",
+            "frac": achieved / peak, "lds_insts_per_call": t.get("sq_insts_lds_per_call"),
             "bank_conflict_frac_of_lds_active": (conf / act) if conf and act else None,
-            "source": src,
-            "peak_note": "256 CUs x 2.4 GHz x 0.152 wave-instructions/clk/CU (ds_add_u32 random, "
-                         "profiles/r01/lds_atomics_microbench.txt; ds_cmpst_rtn_b32 0.088)"}
+            "wave_cycles_waiting_frac": (t["sq_wait_any_per_call"] / t["sq_wave_cycles_per_call"])
+            if t.get("sq_wait_any_per_call") and t.get("sq_wave_cycles_per_call") else None,
+            "clock_ghz": clk / 1e9, "kernel": t.get("kernel"), "source": src,
+            "peak_note": "every CU's LDS array busy every cycle (SQ_LDS_IDX_ACTIVE counts LDS-array "
+                         "cycles per CU, MI355X_MICROARCH.md LDS section); clock from GRBM_GUI_ACTIVE"}
 
 
 def latest_traffic_json():
@@ -1123,6 +1304,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-c3-sharded", action="store_true")
     ap.add_argument("--no-c2", action="store_true")
+    ap.add_argument("--no-ref-sweep", action="store_true",
+                    help="skip the reference main's 62-config sweep (bin/kmer-sketching on 64 files)")
     ap.add_argument("--sweep-inflight", type=int, default=2,
                     help="config-5 seeds in flight (one context + HIP stream each)")
     ap.add_argument("--inflight", type=int, default=3,
@@ -1202,7 +1385,8 @@ def main():
     pairs_wide = None
     if not args.no_pairs and not args.no_pairs_wide:
         pairs_wide = run_pairs(ctx, world, rank, sksffi.mask_generate(C4W_W, C4W_K, MASK_SEED),
-                               steps=max(1, min(args.steps, 10)), warmup=1, w=C4W_W)
+                               steps=max(1, min(args.steps, 10)), warmup=1, w=C4W_W,
+                               cpu_pairs=not args.no_cpu_baseline)
 
     c3s = None
     if not args.no_c3_sharded:
@@ -1217,6 +1401,10 @@ def main():
         sweep = run_seed_sweep(ctx, world, rank, steps=max(1, min(args.steps, 2)), warmup=1,
                                lanes_n=args.sweep_inflight,
                                cpu=rank == 0 and world == 1 and not args.no_cpu_baseline)
+
+    ref_sweep = None
+    if rank == 0 and world == 1 and not args.no_ref_sweep:
+        ref_sweep = run_ref_sweep(ctx, cpu=not args.no_cpu_baseline)
 
     cpu = cpu_x = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1252,6 +1440,7 @@ def main():
             "pairs": pairs,
             "pairs_wide": pairs_wide,
             "seed_sweep": sweep,
+            "reference_sweep": ref_sweep,
             "end_to_end": e2e,
             "c3_one_genome_sharded": c3s,
         }

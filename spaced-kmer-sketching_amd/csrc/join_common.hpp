@@ -35,13 +35,16 @@ namespace sks {
 namespace jc {
 
 // ---- layout geometry ----------------------------------------------------------------------
-constexpr uint32_t kGLog = 3;   // hash buckets per value group: 8
+#ifndef SKS_LAYOUT_GLOG
+#define SKS_LAYOUT_GLOG 3
+#endif
+constexpr uint32_t kGLog = SKS_LAYOUT_GLOG;   // hash buckets per value group: 8
 // value groups per region: 2^rg, rg in [0, kRGLogMax], chosen per build (a
 // large build takes 8-group regions, a small one smaller regions so its grid
 // fills the chip; layout.hip join_layout_build); the region bucket log is
 // stored in the last word of every block's boff row, so each layout tells the
 // join its own region size
-constexpr uint32_t kRGLogMax = 3;
+constexpr uint32_t kRGLogMax = 6 - kGLog;  // regions of at most 64 buckets
 constexpr uint32_t kMaxLogB = 14;
 
 __host__ __device__ inline uint32_t lay_gb_log(uint32_t log_b) { return log_b < kGLog ? log_b : kGLog; }

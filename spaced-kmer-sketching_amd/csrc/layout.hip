@@ -56,8 +56,8 @@ using jc::kv_store;
 
 constexpr int kTile = 64;
 constexpr int kPT = 256;                 // threads of the layout kernels
-constexpr uint32_t kGCap = 2048;         // elements of one dedup batch (a group)
-constexpr int kTabLog = 12;              // dedup table: 4096 slots (load <= 1/2)
+constexpr uint32_t kGCap = 256u << jc::kGLog;  // elements of one dedup batch (a group): 2048
+constexpr int kTabLog = 9 + jc::kGLog;         // dedup table: 4096 slots (load <= 1/2)
 constexpr uint32_t kTab = 1u << kTabLog;
 constexpr uint32_t kIdxBits = 11;        // slot word: tag21 << 11 | element index
 constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1;
@@ -278,7 +278,10 @@ __device__ unsigned long long g_layout_stamps_wg[kMaxStampWgs * 5];
 #endif
 constexpr int kPB = 256;                     // threads of the placement kernel
 constexpr int kTPS = kPB / 64;               // threads per sketch in the register path (4)
-constexpr int kRegPer = 12;                  // elements of its sketch per thread held in registers
+#ifndef SKS_LAYOUT_REGPER
+#define SKS_LAYOUT_REGPER 12
+#endif
+constexpr int kRegPer = SKS_LAYOUT_REGPER;   // elements of its sketch per thread held in registers
 constexpr uint32_t kSkCap = kTPS * kRegPer;  // a group with a sketch holding more (48) takes the bucket passes
 constexpr int kSlowPer = kGCap / kPB;        // slice path: slice elements per thread
 constexpr uint32_t kSpt = kTab / kPB;        // table slots per thread in the emit scan (16)
@@ -858,11 +861,11 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
 // no key array: 35 KB of LDS, four workgroups per CU).  The table's empty word is
 // 0, so the value 0 (a poly-A k-mer) is kept apart as s_zero: its mix is 0, so
 // it is the first value of bucket 0 (and of the first slice of bucket 0).
-constexpr uint32_t kVLog = 11, kVT = 1u << kVLog;  // value slots
+constexpr uint32_t kVLog = 8 + jc::kGLog, kVT = 1u << kVLog;  // value slots (2048)
 constexpr uint32_t kVSpt = kVT / kPB;              // slots per thread in a scan emit (8)
 static_assert(kGCap <= kVT, "a normal-path group fits the value table");
 #ifndef SKS_LAYOUT_HALF_AT
-#define SKS_LAYOUT_HALF_AT 1024
+#define SKS_LAYOUT_HALF_AT (kVT / 2)
 #endif
 constexpr uint32_t kHalfAt = SKS_LAYOUT_HALF_AT;   // predicted distinct values above which a group takes two halves
 static_assert(kVSpt % 2 == 0, "scan emit reads slot pairs");
@@ -895,7 +898,10 @@ __device__ __forceinline__ bool vp_in(const VPass& p, uint64_t mix) {
   return top - p.q0 < p.span;
 }
 template <bool CHECK>
-__global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k_gl_place1(const uint64_t* __restrict__ data,
+#ifndef SKS_LAYOUT_WAVES
+#define SKS_LAYOUT_WAVES 4
+#endif
+__global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(SKS_LAYOUT_WAVES))) void k_gl_place1(const uint64_t* __restrict__ data,
                                                    const uint64_t* __restrict__ starts, uint32_t count,
                                                    uint32_t log_b, const uint32_t* __restrict__ pos,
                                                    const uint64_t* __restrict__ bstart,
@@ -1154,7 +1160,7 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(4))) void k
       __syncthreads();
       if (tid == 0) {
         uint32_t parts = 1;  // predicted distinct values (raw x the running distinct share) per part <= 1536
-        while (parts < GB && (uint64_t)gn_j * dshare > (1536ull << 16) * parts) parts <<= 1;
+        while (parts < GB && (uint64_t)gn_j * dshare > ((uint64_t)(3 * kVT / 4) << 16) * parts) parts <<= 1;
         const uint32_t sp_log = gb_log - (31 - __builtin_clz(parts));  // log2(GB / parts)
         for (uint32_t q = 0; q < parts; ++q) {  // rightmost first: the leftmost is on top
           s_sq[q] = (uint64_t)(parts - 1 - q) << sp_log;

@@ -1,7 +1,7 @@
 """A/B of the all-pairs intersection kernels on config 4 (1000 x 5 Mb, bottom-s
 10000) or config 5's 200 genomes: sketches once, then times sks_intersect_sym
 over all tiles per kernel (median of reps) and checks the matrices agree.
-    python tools/bench_pairs.py [n_genomes] [reps]"""
+    python tools/bench_pairs.py [n_genomes] [reps] [family|indep|same] [w]"""
 import os
 import statistics
 import sys
@@ -19,6 +19,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     mode = sys.argv[3] if len(sys.argv) > 3 else "family"  # family | indep | same
+    w = int(sys.argv[4]) if len(sys.argv) > 4 else 31  # 45: config 4's 128-bit leg (k = 30)
     ctx = sksffi.Context(0)
     L = bench.C4_LEN
     seg = [0]
@@ -33,12 +34,14 @@ def main():
             a, r = 100, 0.0
         ctx.synth_bases(buf.data_ptr() + seg[g], L, a, m, r)
         buf[seg[g] + L] = ord("\n")
-    mask = sksffi.mask_generate(31, 21, 0)
-    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, 31, mask, sksffi.SKS_BOTTOM_S, 10000)
+    mask = sksffi.mask_generate(w, 21 if w == 31 else w - 15, 0)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, w, mask, sksffi.SKS_BOTTOM_S, 10000)
     data, starts, sizes = ss.device_ptrs()
+    ew = ss.elem_words
     T = sksffi.intersect_sym_tiles(n)
     ref = None
-    kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN))
+    kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN)) if ew == 1 else \
+        (("join", sksffi.INTERSECT_JOIN),)
     only = os.environ.get("SKS_BENCH_KERNELS")
     if only:
         kernels = tuple(x for x in kernels if x[0] in only.split(","))
@@ -47,7 +50,7 @@ def main():
         out = torch.empty((n, n), dtype=torch.int32, device="cuda")
         ms = []
         for _ in range(reps + 1):
-            ctx.intersect_sym(data, starts, sizes, 1, n, 0, T, out.data_ptr())
+            ctx.intersect_sym(data, starts, sizes, ew, n, 0, T, out.data_ptr())
             ms.append(ctx.last_intersect_ms())
         got = out.cpu()
         if ref is None:

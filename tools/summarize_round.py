@@ -131,7 +131,17 @@ def main(src, dst, warmup, steps):
             windows = json.loads(line)["config"]["windows_per_genome"]
         except (OSError, IndexError, KeyError, ValueError):
             pass
+        # the hardware's own view: VALU instructions issued per SIMD per cycle
+        # (SQ_ACTIVE_INST_VALU summed over the SIMDs; cycles from GRBM_GUI_ACTIVE,
+        # summed over the 8 XCDs) — beside the priced-mix peak above
+        act = _pmc_kernel(sq, SCAN, "SQ_ACTIVE_INST_VALU")
+        grbm = _pmc_kernel(sq, SCAN, "GRBM_GUI_ACTIVE")
+        cyc = statistics.median(grbm) / 8 if grbm else None
+        hw = {"sq_active_inst_valu_per_launch": statistics.median(act) if act else None,
+              "kernel_cycles_per_launch": cyc,
+              "valu_inst_per_simd_cycle": (statistics.median(act) / (1024 * cyc)) if act and cyc else None}
         valu = {"kernel": SCAN, "sq_insts_valu_per_launch": statistics.median(insts) if insts else None,
+                **hw,
                 "windows_per_launch": windows,
                 "valu_per_window": (64 * statistics.median(insts) / windows) if insts and windows else None,
                 "hot_block_valu": mix["hot_block_valu"], "hot_block_cycles": mix["hot_block_cycles"],
@@ -140,17 +150,22 @@ def main(src, dst, warmup, steps):
                 "rates": mix["cycles_unit"], "scan_source_hash": srchash.scan_hash()}
         with open(os.path.join(dst, "scan_valu.json"), "w") as f:
             json.dump(valu, f, indent=1)
-    # k_join LDS instructions per all-pairs call (pairs.roofline in bench.py)
-    pr = os.path.join(src, "pairs")
-    if os.path.isdir(pr):
-        lds = {"kernel": "k_join<1, false> (config 4, 1000 x bottom-s 10000, tools/bench_pairs.py family)",
-               "join_source_hash": srchash.join_hash()}
+    # k_join LDS counters per all-pairs call (pairs.roofline / pairs_wide.roofline in bench.py)
+    for sub, out, what in (("pairs", "pair_lds.json", "k_join<1, ...> (config 4, 1000 x bottom-s 10000, w = 31, "
+                                                      "tools/bench_pairs.py family)"),
+                           ("pairs_wide", "pair_lds_wide.json", "k_join<2, ...> (config 4, 1000 x bottom-s 10000, "
+                                                                "w = 45 / k = 30, tools/bench_pairs.py family 45)")):
+        pr = os.path.join(src, sub)
+        if not os.path.isdir(pr):
+            continue
+        lds = {"kernel": what, "join_source_hash": srchash.join_hash()}
         for c in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
-                  "SQ_WAVE_CYCLES", "SQ_WAIT_INST_LDS", "GRBM_GUI_ACTIVE"):
+                  "SQ_WAVE_CYCLES", "SQ_WAIT_INST_LDS", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_BUSY_CYCLES",
+                  "GRBM_GUI_ACTIVE"):
             v = _pmc_kernel(pr, "k_join", c)
             lds[c.lower() + "_per_call"] = statistics.median(v) if v else None
         lds["profiled_ms"] = _pmc_kernel_ms(pr, "k_join")
-        with open(os.path.join(dst, "pair_lds.json"), "w") as f:
+        with open(os.path.join(dst, out), "w") as f:
             json.dump(lds, f, indent=1)
     print(json.dumps({"launches": {k: launches[k] for k in ("median_ms", "mean_ms", "bench_line_hipevent_kernel_ms")},
                       "traffic": traffic["scan_hbm_bytes_per_launch"]}, indent=1))
