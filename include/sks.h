@@ -26,7 +26,7 @@ extern "C" {
                               the layout entry points, sks_ctx_set_join_check; later additions
                               within 2 (new symbols only): sks_ani_rows, sks_intersect_layout_ani,
                               sks_host_alloc, sks_host_free, sks_join_layout_stat_copy,
-                              sks_sketches_export */
+                              sks_sketches_export, sks_all_pairs_ani */
 
 typedef enum sks_status {
   SKS_OK = 0,
@@ -369,6 +369,21 @@ int sks_intersect_layout_ani(sks_ctx* ctx, uint32_t n, uint32_t log_b, int elem_
  * d_sizes[i] must be <= stride (the caller's bound; larger sketches are cut). */
 int sks_sketches_export(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
                         int elem_words, uint32_t n, uint64_t* d_dst, uint64_t stride, uint32_t* d_dst_sizes);
+/* The whole "comparison" of kmer-sketching.cpp:185-200 in one call, for one
+ * process and one device: every ordered pair of the n sketches (d_data,
+ * d_starts, d_sizes — e.g. a set's device arrays) counted over a join layout
+ * of all of them (built in context scratch), and, when ani != NULL, their
+ * containment / ANI written by the join as in sks_intersect_layout_ani
+ * (ani[i * n + j], n * n doubles in device or pinned host memory).
+ * d_counts: the packed upper-triangle tiles [sks_intersect_sym_tiles(n)][64][64]
+ * int32 (sks_intersect_layout_tiles' packed format), or NULL to keep them in
+ * scratch.  max_size: the largest sketch (sizes the buckets); total: the sizes'
+ * sum (or an upper bound).  d_status (device, 2 x u32, may be NULL) receives the
+ * layout's status words (sks_join_layout_stat_copy).  Queued on the context
+ * stream; nothing waits. */
+int sks_all_pairs_ani(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
+                      int elem_words, uint32_t n, uint32_t max_size, uint64_t total, int kmer_num_ones,
+                      double* ani, int32_t* d_counts, uint32_t* d_status);
 /* Pinned host memory the device reads and writes directly (mapped into every
  * device's address space): the destination of a fused ANI matrix.  coherent:
  * fine-grained (every device store goes to the host as issued); 0: coarse-

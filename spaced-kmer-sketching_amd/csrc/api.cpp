@@ -205,6 +205,7 @@ struct sks_ctx {
   sks::Scratch meta;                // small per-segment device arrays
   sks::Scratch iwork;               // intersection bucket tables
   sks::Scratch tdone;               // fused ANI: workgroups finished per join tile
+  sks::Scratch lay;                 // sks_all_pairs_ani: the join layout, its temp and packed counts
   const uint32_t* layout_stat = nullptr;  // the last join-layout build's 2 status words (in iwork)
   std::vector<uint64_t> meta_host;  // staging for `meta`
   sks_timings last{};
@@ -562,7 +563,7 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
   c->stream = reinterpret_cast<hipStream_t>(stream);
   // every scratch buffer is used on the context's stream only
   for (sks::Scratch* sc : {&c->ingress, &c->tmp, &c->rec[0], &c->rec[1], &c->rec[2], &c->flag,
-                           &c->pos, &c->meta, &c->iwork, &c->tdone})
+                           &c->pos, &c->meta, &c->iwork, &c->tdone, &c->lay})
     sc->owner = &c->stream;
   for (auto& b : c->buf) b.owner = &c->stream;
   if (hipEventCreate(&c->ev_begin) != hipSuccess || hipEventCreate(&c->ev_end) != hipSuccess ||
@@ -587,6 +588,7 @@ int sks_ctx_destroy(sks_ctx* c) {
   c->meta.release();
   c->iwork.release();
   c->tdone.release();
+  c->lay.release();
   c->ingress.release();
   trim_device_cache(c->device);
   (void)hipEventDestroy(c->ev_begin);
@@ -1677,6 +1679,68 @@ int sks_intersect_layout_ani(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_wo
     SKS_HIP(sks::join_launch(R, 0u - r_blk0, C, 0u - c_blk0, n, log_b, elem_words, true, 0, n, tile_begin,
                              tile_end, d_tiles, packed != 0, d_out, c->join_check, c->stream, &A));
   }
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
+                      int elem_words, uint32_t n, uint32_t max_size, uint64_t total, int kmer_num_ones,
+                      double* ani, int32_t* d_counts, uint32_t* d_status) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_all_pairs_ani: null ctx");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (ani && kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_all_pairs_ani: kmer_num_ones must be positive");
+  if (n && (!d_starts || !d_sizes)) return sks::fail(SKS_E_ARG, "sks_all_pairs_ani: null argument");
+  if (total >= (1ull << 32)) return sks::fail(SKS_E_UNSUPPORTED, "sks_all_pairs_ani: >= 2^32 elements");
+  DeviceGuard g(c->device);
+  double* d_ani = ani;
+  if (ani && n) {
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, ani) == hipSuccess && at.type == hipMemoryTypeHost) {
+      void* dp = nullptr;
+      SKS_HIP(hipHostGetDevicePointer(&dp, ani, 0));
+      d_ani = static_cast<double*>(dp);
+    }
+    (void)hipGetLastError();
+  }
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  if (n == 0) {
+    if (d_status) SKS_HIP(hipMemsetAsync(d_status, 0, 8, c->stream));
+    SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+    return SKS_OK;
+  }
+  // one layout of all n sketches (context scratch), then every upper-triangle
+  // tile in one join launch: packed counts and, when asked, the fused ANI
+  const uint32_t log_b = sks::join_log_b(std::max<uint32_t>(max_size, 1));
+  const uint32_t nb = (n + 63) / 64;
+  const uint64_t T = sks::intersect_sym_tiles(n);
+  const uint64_t tot = std::max<uint64_t>(total, 1);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_vals = 0, o_masks = al(o_vals + tot * 8 * elem_words), o_boff = al(o_masks + tot * 8);
+  const size_t o_bst = al(o_boff + (size_t)nb * sks::join_layout_boff_words(log_b) * 4);
+  const size_t o_stat = al(o_bst + (size_t)(nb + 1) * 8);
+  const size_t o_cnt = al(o_stat + 16);
+  const size_t o_tmp = al(o_cnt + (d_counts ? 0 : (size_t)T * 4096 * 4));
+  const size_t need = o_tmp + sks::join_layout_temp_bytes(n, log_b, elem_words) + 256;
+  SKS_HIP(c->lay.reserve(need));
+  SKS_HIP(c->tdone.reserve(T * sizeof(uint32_t)));
+  char* w = static_cast<char*>(c->lay.ptr);
+  uint64_t* vals = reinterpret_cast<uint64_t*>(w + o_vals);
+  uint64_t* masks = reinterpret_cast<uint64_t*>(w + o_masks);
+  uint32_t* boff = reinterpret_cast<uint32_t*>(w + o_boff);
+  uint64_t* bst = reinterpret_cast<uint64_t*>(w + o_bst);
+  uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
+  int32_t* cnt = d_counts ? d_counts : reinterpret_cast<int32_t*>(w + o_cnt);
+  SKS_HIP(hipMemsetAsync(stat, 0, 8, c->stream));
+  SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, elem_words, nullptr, w + o_tmp, vals, masks,
+                                 boff, bst, stat, c->join_check, c->stream));
+  if (d_status) SKS_HIP(hipMemcpyAsync(d_status, stat, 8, hipMemcpyDeviceToDevice, c->stream));
+  SKS_HIP(hipMemsetAsync(cnt, 0, T * 4096 * 4, c->stream));
+  const sks::JoinLayout L{vals, masks, boff, bst};
+  const sks::JoinAni A{d_ani, reinterpret_cast<const int32_t*>(d_sizes), kmer_num_ones,
+                       static_cast<uint32_t*>(c->tdone.ptr)};
+  if (ani) SKS_HIP(hipMemsetAsync(c->tdone.ptr, 0, T * sizeof(uint32_t), c->stream));
+  SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, elem_words, true, 0, n, 0, T, nullptr, true, cnt, c->join_check,
+                           c->stream, ani ? &A : nullptr));
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;
 }

@@ -485,6 +485,19 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
         ani_out = torch.zeros((n_genomes, n_genomes), dtype=torch.float64, device=device)
     res.ani = ani_out if fused else None
     stats_mark = ops.stats_mark() if hasattr(ops, "stats_mark") else None
+    if solo and hasattr(ops, "all_pairs") and (fused or dst is None):
+        # one call: layout + every tile (+ the fused ANI) natively (sks_all_pairs_ani)
+        nb = (n_genomes + TILE - 1) // TILE
+        res.tiles = _all_tiles(nb)
+        res.counts = ops.parts(len(res.tiles), device)
+        if n_genomes:
+            ops.all_pairs(mine, mx, res.counts, ani_ones if fused else None, ani_out if fused else None)
+        if dst is not None:
+            out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
+            res.matrix = place_tiles(out, res.tiles, res.counts, n_genomes)
+        if stats_mark is not None:
+            res._stats = ops.stats_since(stats_mark)
+        return res
     if solo:
         lay = ops.build(mine, log_b, None, "own")
         if not fused:  # counts only: the dense matrix, both halves by the join
@@ -670,13 +683,27 @@ class GpuJoinOps:
             self.ctx.join_layout_build(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
                                        log_b, *(t.data_ptr() for t in lay), stat=False, total=src.total,
                                        bounds=gb.data_ptr() if gb is not None else None, elem_words=self.ew)
-            if self.n_stats == self.stats.shape[0]:
-                self.stats = torch.cat([self.stats, torch.zeros_like(self.stats)])
-            self.ctx.join_layout_stat_copy(self.stats[self.n_stats].data_ptr())
-            self.n_stats += 1
+            self.ctx.join_layout_stat_copy(self._stat_slot())
             _torch_waits_for_ctx(self.ctx)
         self.keep[key] = (src, gb)  # alive until torch's stream is past the build
         return lay
+
+    def _stat_slot(self):
+        if self.n_stats == self.stats.shape[0]:
+            self.stats = torch.cat([self.stats, torch.zeros_like(self.stats)])
+        self.n_stats += 1
+        return self.stats[self.n_stats - 1].data_ptr()
+
+    def all_pairs(self, src, max_size, out, k, ani):
+        """sks_all_pairs_ani: one layout of src, every upper-triangle tile into the
+        packed out [T, 64, 64], and the ANI into ani when k is given."""
+        ani_ptr = (ani.data_ptr() if hasattr(ani, "data_ptr") else ani.ptr) if k is not None else 0
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.all_pairs_ani(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
+                               max(int(max_size), 1), max(src.total, 1), k or 0, ani_ptr, out.data_ptr(),
+                               self._stat_slot(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+        self.keep["all_pairs"] = src
 
     def pad(self, src, stride, data, sizes):
         _ctx_waits_for_torch(self.ctx)

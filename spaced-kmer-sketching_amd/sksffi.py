@@ -64,7 +64,7 @@ EXPORTED = [
     "sks_ctx_set_join_check", "sks_ctx_join_check_violations", "sks_intersect_layout_pair_tiles",
     "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_rows", "sks_ani_tiles",
     "sks_intersect_layout_ani", "sks_host_alloc", "sks_host_free", "sks_join_layout_stat_copy",
-    "sks_sketches_export",
+    "sks_sketches_export", "sks_all_pairs_ani",
 ]
 
 _lib = None
@@ -144,6 +144,8 @@ def lib():
     L.sks_host_free.argtypes = [vp]
     L.sks_join_layout_stat_copy.argtypes = [vp, vp]
     L.sks_sketches_export.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp]
+    L.sks_all_pairs_ani.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, vp, vp,
+                                    vp]
     L.sks_sketch_set_export_csr.argtypes = [vp, vp, vp]
     L.sks_ani_matrix.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, vp]
     L.sks_ani_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, vp, vp]
@@ -386,6 +388,14 @@ class Context:
                                           C.c_void_p(out_vals), C.c_void_p(out_masks), C.c_void_p(out_boff),
                                           C.c_void_p(out_bstart), C.byref(mx) if stat else None))
         return mx.value if stat else None
+
+    def all_pairs_ani(self, data, starts, sizes, n, max_size, total, kmer_num_ones, ani, counts, status,
+                      elem_words=1):
+        """sks_all_pairs_ani (device pointers; ani: device or pinned host pointer, or 0
+        for counts only; counts / status may be 0)."""
+        check(lib().sks_all_pairs_ani(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes), elem_words,
+                                      n, max_size, total, kmer_num_ones, C.c_void_p(ani) if ani else None,
+                                      C.c_void_p(counts) if counts else None, C.c_void_p(status) if status else None))
 
     def sketches_export(self, data, starts, sizes, n, dst, stride, dst_sizes, elem_words=1):
         """sks_sketches_export (device pointers): sketches padded to a fixed stride."""
