@@ -376,8 +376,8 @@ int sks_sketches_export(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_
  * containment / ANI written by the join as in sks_intersect_layout_ani
  * (ani[i * n + j], n * n doubles in device or pinned host memory).
  * d_counts: the packed upper-triangle tiles [sks_intersect_sym_tiles(n)][64][64]
- * int32 (sks_intersect_layout_tiles' packed format), or NULL to keep them in
- * scratch.  max_size: the largest sketch (sizes the buckets); total: the sizes'
+ * int32 (sks_intersect_layout_tiles' packed format; the call clears them, the
+ * caller need not), or NULL to keep them in scratch.  max_size: the largest sketch (sizes the buckets); total: the sizes'
  * sum (or an upper bound).  d_status (device, 2 x u32, may be NULL) receives the
  * layout's status words (sks_join_layout_stat_copy).  Queued on the context
  * stream; nothing waits.  sks_ctx_last_intersect_ms then times the join launch

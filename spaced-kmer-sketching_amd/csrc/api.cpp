@@ -942,6 +942,129 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   return SKS_OK;
 }
 
+// The scan's parameters for the m segments whose metadata sit in `arena` at the
+// given word offsets (survivor / window counters zeroed there).
+sks::ScanParams scan_params(const BuildState& S, const uint8_t* d_seq, const MetaArena& arena, size_t o_beg,
+                            size_t o_end, size_t o_tp, size_t o_thr, size_t o_cap, size_t o_off, size_t o_cnt,
+                            size_t o_win, uint32_t m, uint64_t n_tiles) {
+  sks_ctx* c = S.c;
+  sks::ScanParams p{};
+  p.seq = d_seq;
+  p.seg_begin = arena.ptr(o_beg);
+  p.seg_end = arena.ptr(o_end);
+  p.tile_prefix = arena.ptr(o_tp);
+  p.n_seg = m;
+  p.n_tiles = n_tiles;
+  p.w = S.w;
+  p.mask_lo = S.mask_lo;
+  p.mask_hi = S.mask_hi;
+  p.kconst = S.kconst;
+  p.low_mask = S.dt.low_mask;
+  p.high_mask = S.dt.rot > 32 ? (uint32_t)((1ull << (S.dt.rot - 32)) - 1) : 0u;
+  p.dinv = S.dt.dinv;
+  p.dlim = S.dt.lim;
+  p.seg_thresh = arena.ptr(o_thr);
+  p.out_key = reinterpret_cast<uint64_t*>(c->rec[0].ptr);
+  p.out_val = reinterpret_cast<uint64_t*>(c->rec[1].ptr);
+  p.out_hi = reinterpret_cast<uint64_t*>(c->rec[2].ptr);
+  p.seg_out_off = arena.ptr(o_off);
+  p.seg_out_cap = arena.ptr(o_cap);
+  p.seg_count = reinterpret_cast<unsigned long long*>(arena.ptr(o_cnt));
+  p.seg_windows = reinterpret_cast<unsigned long long*>(arena.ptr(o_win));
+  return p;
+}
+
+constexpr int kFastFallback = -1;  // not an SKS status: take the general build
+
+// One narrow bottom-s genome (kmer_set_from_fasta_file's shape, kmer_set.cpp:
+// 54-68) whose candidates fit k_bottom_fused: the scan and the fused
+// post-processing write the sketch set's own arrays, and the build's only host
+// round trip is one read-back of (survivors, windows, size) at the end — instead
+// of a count read-back, compaction, a device-wide sort and unique with a
+// distinct-count read-back, select and a metadata upload.  A genome whose scan
+// overflows the candidate region or that has fewer than s distinct candidates
+// (both rare) returns kFastFallback and the general build runs instead.
+int build_bottom_single(BuildState& S, const uint8_t* d_seq, const uint64_t* seg_off, uint64_t thresh,
+                        uint64_t cap, sks_timings& tm, sks_sketch_set** out) {
+  sks_ctx* c = S.c;
+  hipStream_t st = c->stream;
+  const uint64_t s = S.pol.param;
+  const uint64_t n_tiles = sks::scan_tiles_for(seg_off[1] - seg_off[0]);
+  SKS_HIP(c->rec[0].reserve(std::max<uint64_t>(cap, 1) * sizeof(uint64_t)));
+  SKS_HIP(c->rec[1].reserve(std::max<uint64_t>(cap, 1) * sizeof(uint64_t)));
+  const uint64_t slots = std::max<uint64_t>(std::min(s, cap), 1);
+  MetaArena arena(c);
+  const size_t o_beg = arena.add({seg_off[0]}), o_end = arena.add({seg_off[1]}), o_tp = arena.add({0, n_tiles}),
+               o_thr = arena.add({thresh}), o_cap = arena.add({cap}), o_off = arena.add({0}),
+               o_retry = arena.add({thresh != ~0ull ? 1ull : 0ull}), o_dst = arena.add({0, slots}),
+               o_cnt = arena.add_zero(1), o_win = arena.add_zero(1), o_res = arena.add_zero(1);
+  if (o_win != o_cnt + 2 || o_res != o_win + 2) return sks::fail(SKS_E_HIP, "sks_sketch_build: arena layout");
+  SKS_TRY(arena.upload());
+  sks_sketch_set* set = new (std::nothrow) sks_sketch_set();
+  if (!set) return sks::fail(SKS_E_NOMEM, "sks_sketch_build: out of memory");
+  set->device = c->device;
+  set->n = 1;
+  int rc = alloc_u64(&set->d_data, slots);
+  if (rc == SKS_OK) rc = alloc_u64(&set->d_starts, 1);
+  if (rc == SKS_OK && dev_alloc(reinterpret_cast<void**>(&set->d_sizes), sizeof(uint32_t)) != hipSuccess)
+    rc = sks::fail(SKS_E_HIP, "sks_sketch_build: device allocation failed");
+  auto drop = [&]() {  // arrays still unused by the device or idle after a sync
+    dev_release(set->d_data, slots * 8);
+    dev_release(set->d_starts, 8);
+    dev_release(set->d_sizes, 8);
+    delete set;
+  };
+  if (rc != SKS_OK) {
+    drop();
+    return rc;
+  }
+  const sks::ScanParams p =
+      scan_params(S, d_seq, arena, o_beg, o_end, o_tp, o_thr, o_cap, o_off, o_cnt, o_win, 1, n_tiles);
+  const sks::BitRuns runs = sks::bit_runs(S.mask_lo);
+  const int kb = std::max(1, __builtin_popcountll(S.mask_lo));
+  hipError_t e = hipEventRecord(c->ev_s0, st);
+  if (e == hipSuccess) e = sks::launch_scan(p, sks::kModeBottom, S.pol.flavour, false, c->device, st, c->grid_override);
+  if (e == hipSuccess) e = hipEventRecord(c->ev_s1, st);
+  if (e == hipSuccess)
+    e = sks::launch_bottom_fused(reinterpret_cast<uint64_t*>(c->rec[0].ptr), arena.ptr(o_off), arena.ptr(o_cnt),
+                                 arena.ptr(o_retry), arena.ptr(o_dst), 1, cap, s, kb, runs, S.kconst,
+                                 S.pol.flavour, set->d_data, arena.ptr(o_res), st, arena.ptr(o_cap), set->d_sizes,
+                                 set->d_starts);
+  if (e == hipSuccess) e = hipEventRecord(c->ev_end, st);
+  uint64_t h[6] = {0, 0, 0, 0, 0, 0};  // survivors, -, windows, -, size, -
+  if (e == hipSuccess) e = sks::pinned_d2h(h, arena.ptr(o_cnt), sizeof h, st);  // synchronises the stream
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(st);
+    drop();
+    return sks::fail(SKS_E_HIP, std::string("sks_sketch_build: ") + hipGetErrorString(e));
+  }
+  const uint64_t survivors = h[0], windows = h[2], size = h[4];
+  if (survivors > cap || size == ~0ull || size == sks::kBottomOverflow || size > slots) {
+    drop();
+    return kFastFallback;
+  }
+  float ms = 0, tot = 0;
+  (void)hipEventElapsedTime(&ms, c->ev_s0, c->ev_s1);
+  (void)hipEventElapsedTime(&tot, c->ev_begin, c->ev_end);
+  tm.scan_ms = ms;
+  tm.scan_launches = n_tiles ? 1 : 0;
+  tm.survivors = survivors;
+  tm.windows = windows;
+  tm.total_ms = tot;
+  tm.post_ms = tot - ms;
+  set->elem_words = 1;
+  set->sizes = {(uint32_t)size};
+  set->starts = {0};
+  set->windows = {windows};
+  set->window = S.w;
+  set->mask[0] = S.mask_lo;
+  set->mask[1] = S.mask_hi;
+  set->policy = S.pol;
+  c->last = tm;
+  *out = set;
+  return SKS_OK;
+}
+
 // Argument checks shared by sks_sketch_build and sks_kmer_list_build.
 int validate_build(const char* fn, sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes,
                    const uint64_t* seg_off, uint32_t n_seg, int window, const uint64_t mask[2],
@@ -1019,6 +1142,21 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
     cap_g[g] = (uint64_t)std::min<double>(cap, (double)L + 1.0);
   }
 
+  // one narrow bottom-s genome: the single-round-trip path when its candidate
+  // region fits the fused post-processing (8 standard deviations of the
+  // candidate count above its mean, not the general margin, so the kernel runs
+  // at the smaller register tile)
+  if (bottom && !S.wide && n_seg == 1 && getenv("SKS_NO_FAST_BOTTOM") == nullptr) {
+    const uint64_t L = seg_off[1] - seg_off[0];
+    const double expect = std::min<double>((double)L, alpha * (double)policy->param);
+    const uint64_t cap = std::min<uint64_t>(cap_g[0], (uint64_t)(expect + 8.0 * std::sqrt(expect) + 256.0));
+    if (L > 0 && cap <= sks::bottom_fused_capacity()) {
+      const int rc = build_bottom_single(S, d_seq, seg_off, thresh_g[0], cap, tm, out);
+      if (rc != kFastFallback) return rc;
+      tm = sks_timings{};
+    }
+  }
+
   std::vector<PassOut> passes;
   std::vector<uint32_t> pending(n_seg);
   std::iota(pending.begin(), pending.end(), 0);
@@ -1050,29 +1188,8 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
            o_cnt = arena.add_zero(m), o_win = arena.add_zero(m);
     SKS_TRY(arena.upload());
 
-    sks::ScanParams p{};
-    p.seq = d_seq;
-    p.seg_begin = arena.ptr(o_beg);
-    p.seg_end = arena.ptr(o_end);
-    p.tile_prefix = arena.ptr(o_tp);
-    p.n_seg = m;
-    p.n_tiles = n_tiles;
-    p.w = window;
-    p.mask_lo = S.mask_lo;
-    p.mask_hi = S.mask_hi;
-    p.kconst = S.kconst;
-    p.low_mask = S.dt.low_mask;
-    p.high_mask = S.dt.rot > 32 ? (uint32_t)((1ull << (S.dt.rot - 32)) - 1) : 0u;
-    p.dinv = S.dt.dinv;
-    p.dlim = S.dt.lim;
-    p.seg_thresh = arena.ptr(o_thr);
-    p.out_key = reinterpret_cast<uint64_t*>(c->rec[0].ptr);
-    p.out_val = reinterpret_cast<uint64_t*>(c->rec[1].ptr);
-    p.out_hi = reinterpret_cast<uint64_t*>(c->rec[2].ptr);
-    p.seg_out_off = arena.ptr(o_off);
-    p.seg_out_cap = arena.ptr(o_cap);
-    p.seg_count = reinterpret_cast<unsigned long long*>(arena.ptr(o_cnt));
-    p.seg_windows = reinterpret_cast<unsigned long long*>(arena.ptr(o_win));
+    const sks::ScanParams p =
+        scan_params(S, d_seq, arena, o_beg, o_end, o_tp, o_thr, o_cap, o_off, o_cnt, o_win, m, n_tiles);
 
     SKS_HIP(hipEventRecord(c->ev_s0, st));
     SKS_HIP(sks::launch_scan(p, bottom ? sks::kModeBottom : sks::kModeFrac, policy->flavour,
@@ -1729,17 +1846,18 @@ int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   uint64_t* masks = reinterpret_cast<uint64_t*>(w + o_masks);
   uint32_t* boff = reinterpret_cast<uint32_t*>(w + o_boff);
   uint64_t* bst = reinterpret_cast<uint64_t*>(w + o_bst);
-  uint32_t* stat = reinterpret_cast<uint32_t*>(w + o_stat);
+  // the build's status words go straight to the caller's d_status
+  uint32_t* stat = d_status ? d_status : reinterpret_cast<uint32_t*>(w + o_stat);
   int32_t* cnt = d_counts ? d_counts : reinterpret_cast<int32_t*>(w + o_cnt);
-  SKS_HIP(hipMemsetAsync(stat, 0, 8, c->stream));
+  // the status words, the count tiles and the tiles' finisher counters are
+  // cleared by the build's second launch (no memsets of their own)
+  const sks::ZeroSpans zs{{stat, reinterpret_cast<uint32_t*>(cnt), ani ? static_cast<uint32_t*>(c->tdone.ptr) : nullptr},
+                          {2, T * 4096, ani ? T : 0}};
   SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, elem_words, nullptr, w + o_tmp, vals, masks,
-                                 boff, bst, stat, c->join_check, c->stream));
-  if (d_status) SKS_HIP(hipMemcpyAsync(d_status, stat, 8, hipMemcpyDeviceToDevice, c->stream));
-  SKS_HIP(hipMemsetAsync(cnt, 0, T * 4096 * 4, c->stream));
+                                 boff, bst, stat, c->join_check, c->stream, &zs));
   const sks::JoinLayout L{vals, masks, boff, bst};
   const sks::JoinAni A{d_ani, reinterpret_cast<const int32_t*>(d_sizes), kmer_num_ones,
                        static_cast<uint32_t*>(c->tdone.ptr)};
-  if (ani) SKS_HIP(hipMemsetAsync(c->tdone.ptr, 0, T * sizeof(uint32_t), c->stream));
   // sks_ctx_last_intersect_ms: the join launch alone (the layout build before it
   // is the call's fixed part)
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));

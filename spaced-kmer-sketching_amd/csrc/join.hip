@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <vector>
 
 #include "join_common.hpp"
 #include "sks_ani.hpp"
@@ -198,6 +199,29 @@ __device__ __forceinline__ uint32_t window_end(const uint32_t* off, uint32_t we,
   return (we & ((1u << rb_log) - 1)) == 0 ? off[B + ((we - 1) >> rb_log)] : off[we];
 }
 
+#ifdef SKS_JOIN_STAMPS  // diagnostic build: cycles per k_join phase, summed by thread 0 of each workgroup
+// slots: 0 setup, 1 window bookkeeping, 2 stage (incl. waiting for the chunk's
+// loads), 3 insert, 4 probe + hit adds, 5 flush, 6 fused ANI, 7 diagonal tile
+constexpr int kMaxJoinStampWgs = 65536;
+__device__ unsigned long long g_join_stamps_wg[kMaxJoinStampWgs * 8];
+#define JSTAMP(i)                                    \
+  do {                                               \
+    if (threadIdx.x == 0) {                          \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      js_acc[i] += t_ - js_last;                     \
+      js_last = t_;                                  \
+    }                                                \
+  } while (0)
+#define JSTAMP_FLUSH()                                                                          \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < kMaxJoinStampWgs)                                      \
+      for (int q_ = 0; q_ < 8; ++q_) g_join_stamps_wg[(uint64_t)blockIdx.x * 8 + q_] = js_acc[q_]; \
+  } while (0)
+#else
+#define JSTAMP(i) do {} while (0)
+#define JSTAMP_FLUSH() do {} while (0)
+#endif
+
 // PIECES = false: windows also end at every region end of either layout, so a
 // chunk is always contiguous (the kernel for layouts of 64-bucket regions,
 // where the piece code, never taken, still cost 8% of the join); true: windows
@@ -216,6 +240,10 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
   __shared__ uint8_t s_next[kJWin];
   __shared__ uint32_t s_self[kTile];
   __shared__ uint32_t s_top;  // planes used (the highest carry chain)
+#ifdef SKS_JOIN_STAMPS
+  uint64_t js_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t js_last = __builtin_amdgcn_s_memtime();
+#endif
 
   const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
   const uint32_t grp = blockIdx.x % a.n_groups;
@@ -258,6 +286,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
   if (tid == 0) s_top = 0;
   uint32_t top = 0;
   __syncthreads();  // table, planes and self counts cleared before any chain (the diagonal path has no other barrier)
+  JSTAMP(0);
 
   // output of count `cnt` for tile cell (r, c) (both halves of a symmetric
   // off-diagonal tile): the carry-out path of add_hits
@@ -370,6 +399,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
       }
       wb = we;
     }
+    JSTAMP(7);
   } else {
     // ---- off-diagonal tile: chunks of the column block's entries -----------------------------
     uint32_t made[kJMade];  // slots this thread created in the current chunk
@@ -447,6 +477,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
       // chunks of whole buckets; a bucket above cap is cut into sub-chunks of
       // cap column entries, each joined with all of the bucket's row entries
       // (its column entries are distinct, so each hit is counted once)
+      JSTAMP(1);
       auto chunk_end = [&](uint32_t bs) { return wb + (uint32_t)s_next[bs - wb]; };
       uint32_t bs = wb, be = chunk_end(wb);
       uint32_t cs = s_cv[0], ce = min(s_cv[be - wb], cs + a.cap);
@@ -474,6 +505,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
           rp = pieces(s_roff, s_rv, nbs - wb, nbe - wb, r_rb, r_one);
           join_fetch<EW, PIECES>(cvals, cmasks, rvals, rmasks, ncs, nce, cp, s_rv[nbs - wb], s_rv[nbe - wb], rp, tid, nxt);
         }
+        JSTAMP(1);
 
         // 0) free the previous chunk's slots (its probes are done: barrier below
         //    the probe loop) and stage this chunk's entries
@@ -489,6 +521,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
           }
         }
         __syncthreads();
+        JSTAMP(2);
         // 1) insert: the chunk's values are distinct, so a compare-swap walk to
         //    the first free slot
 #pragma unroll
@@ -505,6 +538,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
           made[u] = h;
         }
         __syncthreads();
+        JSTAMP(3);
         if (CHECK) {  // every inserted value is found, naming its own entry
 #pragma unroll
           for (int u = 0; u < kJMade; ++u) {
@@ -552,6 +586,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
           rows_add(m ? rows : 0ull, m, false);
         }
         __syncthreads();
+        JSTAMP(4);
         cur = nxt;
         bs = nbs;
         be = nbe;
@@ -598,7 +633,11 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
       atomicAdd(&a.out[(uint64_t)gc * a.ld + gr], (int32_t)cnt);
     }
   }
-  if (!a.ani) return;
+  JSTAMP(5);
+  if (!a.ani) {
+    JSTAMP_FLUSH();
+    return;
+  }
   // ---- fused containment / ANI: the tile's last workgroup converts it --------------------------
   // The counts are only ever written by device-scope atomics, which every
   // workgroup's result reaches at the device's coherence point (that is what
@@ -618,7 +657,11 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
     s_top = __hip_atomic_fetch_add(a.tile_done + (t - a.tile_begin), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT) + 1 == a.n_groups;
   __syncthreads();
-  if (!s_top) return;
+  if (!s_top) {
+    JSTAMP(6);
+    JSTAMP_FLUSH();
+    return;
+  }
   int32_t* s_cnt = reinterpret_cast<int32_t*>(s_slot);  // the table is free: 4096 counts
   for (uint32_t q = tid; q < (uint32_t)(kTile * kTile); q += kJB) {
     const uint32_t r = q / kTile, c = q % kTile, gr = row0 + r, gc = col0 + c;
@@ -642,6 +685,8 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
         a.ani[(uint64_t)gc * a.n + gr] = ani_of(s_cnt[lane * kTile + c], a.sizes[gc], a.inv_k, nullptr);
     }
   }
+  JSTAMP(6);
+  JSTAMP_FLUSH();
 }
 
 template <int EW, bool CHECK, bool PIECES>
@@ -656,6 +701,20 @@ hipError_t launch_join_slices(JoinArgs ja, uint64_t tile_begin, uint64_t tile_en
     hipLaunchKernelGGL((k_join<EW, CHECK, PIECES>), dim3((unsigned)(nt * ja.n_groups)), dim3(kJB), 0, s, ja);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+#ifdef SKS_JOIN_STAMPS
+    {
+      (void)hipStreamSynchronize(s);
+      const uint64_t nw = std::min<uint64_t>(nt * ja.n_groups, kMaxJoinStampWgs);
+      std::vector<unsigned long long> h(nw * 8);
+      (void)hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_join_stamps_wg), h.size() * 8);
+      double sum[8] = {0};
+      for (uint64_t b = 0; b < nw; ++b)
+        for (int q = 0; q < 8; ++q) sum[q] += (double)h[b * 8 + q];
+      fprintf(stderr, "[k_join stamps] %llu workgroups, cycles per workgroup: setup %.0f window %.0f stage %.0f "
+              "insert %.0f probe+hits %.0f flush %.0f ani %.0f diagonal %.0f\n", (unsigned long long)nw,
+              sum[0] / nw, sum[1] / nw, sum[2] / nw, sum[3] / nw, sum[4] / nw, sum[5] / nw, sum[6] / nw, sum[7] / nw);
+    }
+#endif
   }
   return hipSuccess;
 }

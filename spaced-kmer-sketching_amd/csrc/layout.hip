@@ -215,9 +215,25 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
                                                 const uint64_t* __restrict__ starts,
                                                 const uint32_t* __restrict__ sizes, uint32_t count,
                                                 uint32_t G, const uint64_t* __restrict__ bounds,
-                                                uint32_t* __restrict__ pos) {
+                                                uint32_t* __restrict__ pos, const ZeroSpans z) {
   __shared__ uint64_t s_smp[kPosSamples * EW];
   const uint32_t i = blockIdx.x;
+  {  // the caller's spans to clear: 16-B stores over the grid, dwords at the ends
+    const uint64_t nthr = (uint64_t)gridDim.x * kPT, t0 = (uint64_t)i * kPT + threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      uint32_t* p = z.p[q];
+      const uint64_t nw = z.words[q];
+      if (!p || !nw) continue;
+      const uint64_t head = min(nw, (uint64_t)(((16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u) >> 2));
+      if (t0 < head) p[t0] = 0;
+      uint4* v = reinterpret_cast<uint4*>(p + head);
+      const uint64_t nv = (nw - head) >> 2;
+      for (uint64_t k = t0; k < nv; k += nthr) v[k] = make_uint4(0, 0, 0, 0);
+      const uint64_t tail = head + nv * 4;
+      if (t0 < nw - tail) p[tail + t0] = 0;
+    }
+  }
   const uint32_t sz = sizes[i];
   const uint64_t st = starts[i];
   uint32_t stride = kPosStride;
@@ -1328,9 +1344,11 @@ unsigned long long layout_check_take() {
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                              uint32_t count, uint32_t log_b, int ew, const uint64_t* d_bounds, void* temp,
                              uint64_t* out_vals, uint64_t* out_masks, uint32_t* out_boff,
-                             uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s) {
+                             uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s,
+                             const ZeroSpans* zero) {
   if (log_b > jc::kMaxLogB || (ew != 1 && ew != 2)) return hipErrorInvalidValue;
   if (count == 0) return hipSuccess;
+  const ZeroSpans zs = zero ? *zero : ZeroSpans{};
   const uint32_t G = jc::lay_groups(log_b);
   const uint32_t n_blk = (count + kTile - 1) / kTile;
   uint64_t* bounds_tmp = static_cast<uint64_t*>(temp);
@@ -1349,7 +1367,7 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   if (ew == 1) {
     hipLaunchKernelGGL(k_gl_prep<1>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
                        bounds_tmp, nb_bounds, out_bstart);
-    hipLaunchKernelGGL(k_gl_pos<1>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
+    hipLaunchKernelGGL(k_gl_pos<1>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos, zs);
     if (check)
       hipLaunchKernelGGL((k_gl_place1<true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
                          out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), rg);
@@ -1359,7 +1377,7 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   } else {
     hipLaunchKernelGGL(k_gl_prep<2>, dim3(nb_bounds + 1), dim3(kPT), 0, s, data, starts, sizes, count, G,
                        bounds_tmp, nb_bounds, out_bstart);
-    hipLaunchKernelGGL(k_gl_pos<2>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos);
+    hipLaunchKernelGGL(k_gl_pos<2>, dim3(count), dim3(kPT), 0, s, data, starts, sizes, count, G, bounds, pos, zs);
     if (check)
       hipLaunchKernelGGL((k_gl_place<2, true>), grid_place, dim3(kPB), 0, s, data, starts, count, log_b, pos,
                          out_bstart, out_vals, masks, out_boff, d_stat, group_cap(), rg);

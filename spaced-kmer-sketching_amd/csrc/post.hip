@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 #include <rocprim/block/block_radix_sort.hpp>
@@ -104,16 +105,28 @@ hipError_t sort_impl(const uint64_t* keys_in, uint64_t* keys_out, const uint64_t
                                               (unsigned)n_seg, d_off, d_off + 1, 0, end_bit, s);
 }
 
+// pext / pdep of the mask's bits (BitRuns): the masks are kernel arguments
+// (SGPRs), a zero step is skipped by a uniform branch
 __device__ __forceinline__ uint64_t runs_pack(uint64_t x, const BitRuns& r) {
-  uint64_t o = 0;
-  for (uint32_t i = 0; i < r.n; ++i) o |= ((x >> r.src[i]) & r.bits[i]) << r.dst[i];
-  return o;
+  x &= r.mask;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const uint64_t mv = r.mv[i];
+    if (mv) {
+      const uint64_t t = x & mv;
+      x = (x ^ t) | (t >> (1 << i));
+    }
+  }
+  return x;
 }
 
 __device__ __forceinline__ uint64_t runs_expand(uint64_t x, const BitRuns& r) {
-  uint64_t o = 0;
-  for (uint32_t i = 0; i < r.n; ++i) o |= ((x >> r.dst[i]) & r.bits[i]) << r.src[i];
-  return o;
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    const uint64_t mv = r.mv[i];
+    if (mv) x = (x & ~mv) | ((x << (1 << i)) & mv);
+  }
+  return x & r.mask;
 }
 
 template <bool PACK>
@@ -493,6 +506,57 @@ constexpr size_t fuse_lds() {
   return rp > cs ? rp : cs;
 }
 
+// Sorting networks (odd-even merge sort, checked over all 0-1 inputs) for one
+// bucket of c <= N keys in LDS: loaded into registers padded with ~0 (the
+// largest key), sorted branch-free, the first c written back.
+constexpr uint8_t kNet8[19][2] = {{0, 2}, {1, 3}, {4, 6}, {5, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}, {0, 1}, {2, 3},
+                                  {4, 5}, {6, 7}, {2, 4}, {3, 5}, {1, 4}, {3, 6}, {1, 2}, {3, 4}, {5, 6}};
+constexpr uint8_t kNet16[63][2] = {
+    {0, 1},  {2, 3},   {0, 2},   {1, 3},  {1, 2},   {4, 5},   {6, 7},   {4, 6},   {5, 7},   {5, 6},  {0, 4},
+    {2, 6},  {2, 4},   {1, 5},   {3, 7},  {3, 5},   {1, 2},   {3, 4},   {5, 6},   {8, 9},   {10, 11}, {8, 10},
+    {9, 11}, {9, 10},  {12, 13}, {14, 15}, {12, 14}, {13, 15}, {13, 14}, {8, 12},  {10, 14}, {10, 12}, {9, 13},
+    {11, 15}, {11, 13}, {9, 10}, {11, 12}, {13, 14}, {0, 8},   {4, 12},  {4, 8},   {2, 10},  {6, 14},  {6, 10},
+    {2, 4},  {6, 8},   {10, 12}, {1, 9},  {5, 13},  {5, 9},   {3, 11},  {7, 15},  {7, 11},  {3, 5},   {7, 9},
+    {11, 13}, {1, 2},  {3, 4},   {5, 6},  {7, 8},   {9, 10},  {11, 12}, {13, 14}};
+template <int N>
+__device__ __forceinline__ void bucket_sort(uint64_t* b, uint32_t c) {
+  if (c > (uint32_t)N) {  // beyond the network: insertion sort in LDS (c <= kBkMax)
+    for (uint32_t i = 1; i < c; ++i) {
+      const uint64_t key = b[i];
+      uint32_t j = i;
+      while (j > 0 && b[j - 1] > key) {
+        b[j] = b[j - 1];
+        --j;
+      }
+      b[j] = key;
+    }
+    return;
+  }
+  uint64_t r[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) r[i] = (uint32_t)i < c ? b[i] : ~0ull;
+  constexpr int E = N == 8 ? 19 : 63;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int x = N == 8 ? kNet8[e][0] : kNet16[e][0], y = N == 8 ? kNet8[e][1] : kNet16[e][1];
+    const uint64_t lo = r[x] < r[y] ? r[x] : r[y], hi = r[x] < r[y] ? r[y] : r[x];
+    r[x] = lo;
+    r[y] = hi;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if ((uint32_t)i < c) b[i] = r[i];
+}
+
+#ifdef SKS_FUSE_STAMPS  // diagnostic build: cycles from start to the end of each phase (workgroup 0)
+__device__ unsigned long long g_fuse_stamps[10];
+#define FSTAMP(i)                                                                   \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_fuse_stamps[i] = __builtin_amdgcn_s_memtime() - f_t0; \
+  } while (0)
+#else
+#define FSTAMP(i) do {} while (0)
+#endif
 template <int FLAVOUR, int ITEMS>
 __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ rec,
                                                         const uint64_t* __restrict__ src_off,
@@ -502,7 +566,10 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
                                                         uint64_t s_param, int key_bits,
                                                         const BitRuns runs, uint64_t kconst,
                                                         uint64_t* __restrict__ out,
-                                                        uint64_t* __restrict__ res) {
+                                                        uint64_t* __restrict__ res,
+                                                        const uint64_t* __restrict__ cap,
+                                                        uint32_t* __restrict__ set_sizes,
+                                                        uint64_t* __restrict__ set_starts) {
   constexpr uint32_t kCap = kSelB * ITEMS;
   extern __shared__ unsigned char smem[];
   auto& sort_storage = *reinterpret_cast<typename FuseSort<ITEMS>::storage_type*>(smem);
@@ -514,12 +581,25 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   const uint32_t g = blockIdx.x;
   const int tid = threadIdx.x;
   const uint64_t base = src_off[g];
-  const uint32_t n = (uint32_t)cnt[g];  // <= kCap (host-checked)
+  const uint64_t n64 = cnt[g];
+  if (cap && n64 > cap[g]) {  // the scan counted more than its region kept
+    if (tid == 0) {
+      res[g] = kBottomOverflow;
+      if (set_sizes) set_sizes[g] = 0;
+    }
+    return;
+  }
+  const uint32_t n = (uint32_t)n64;  // <= kCap (host-checked: max_cnt or the caps)
+#ifdef SKS_FUSE_STAMPS
+  const uint64_t f_t0 = __builtin_amdgcn_s_memtime();
+#endif
 
+  // striped (coalesced) loads: the counting sort takes the keys in any order;
+  // blocked order (thread t: positions t * ITEMS ..) starts after the sort
   unsigned long long k[ITEMS];
 #pragma unroll
   for (uint32_t j = 0; j < ITEMS; ++j) {
-    const uint32_t i = tid * ITEMS + j;
+    const uint32_t i = j * kSelB + tid;
     k[j] = i < n ? runs_pack(rec[base + i], runs) : ~0ull;  // pads sort after equal keys
   }
   {
@@ -533,10 +613,12 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
 #pragma unroll
     for (uint32_t q = 0; q < kBkPer; ++q) sbin[tid * kBkPer + q] = 0;
     __syncthreads();
+    FSTAMP(0);
 #pragma unroll
     for (uint32_t j = 0; j < ITEMS; ++j)
-      if (tid * ITEMS + j < n) atomicAdd(&sbin[bk_of(k[j])], 1u);
+      if (j * kSelB + tid < n) atomicAdd(&sbin[bk_of(k[j])], 1u);
     __syncthreads();
+    FSTAMP(1);
     uint32_t cb[kBkPer], sum = 0, mx = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kBkPer; ++q) {
@@ -565,6 +647,8 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     }
     __syncthreads();
     if (bmax > kBkMax) {  // uniform: the keys are still in registers
+      // the block sort takes blocked input: pads (~0) are the largest keys, so
+      // the striped arrangement sorts to the same result
       FuseSort<ITEMS>().sort(k, sort_storage, 0, key_bits);
     } else {
       uint32_t run = excl;
@@ -576,21 +660,25 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
       __syncthreads();
 #pragma unroll
       for (uint32_t j = 0; j < ITEMS; ++j)
-        if (tid * ITEMS + j < n) skeys[atomicAdd(&sbin[bk_of(k[j])], 1u)] = k[j];
+        if (j * kSelB + tid < n) skeys[atomicAdd(&sbin[bk_of(k[j])], 1u)] = k[j];
       __syncthreads();
-      // this thread's buckets are the contiguous range [excl, excl + sum); keys
-      // of earlier buckets are smaller, so an insertion sort of the range only
-      // moves keys within their bucket
-      for (uint32_t i = excl + 1; i < excl + sum; ++i) {
-        const uint64_t key = skeys[i];
-        uint32_t j = i;
-        while (j > excl && skeys[j - 1] > key) {
-          skeys[j] = skeys[j - 1];
-          --j;
-        }
-        skeys[j] = key;
+      FSTAMP(2);
+      // this thread's buckets are the contiguous range [excl, excl + sum), ~2.7
+      // keys per bucket: each bucket is sorted in registers by a sorting network
+      // (8 keys, or 16 for the ~0.3% of buckets above 8; kBkMax bounds them)
+      uint32_t packed_cnt = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < kBkPer; ++q) packed_cnt |= cb[q] << (8 * q);
+      uint32_t st = excl;
+#pragma unroll 1
+      for (uint32_t q = 0; q < kBkPer; ++q) {
+        const uint32_t c = (packed_cnt >> (8 * q)) & 255u;
+        if (c > 8) bucket_sort<16>(skeys + st, c);
+        else if (c > 1) bucket_sort<8>(skeys + st, c);
+        st += c;
       }
       __syncthreads();
+      FSTAMP(3);
 #pragma unroll
       for (uint32_t j = 0; j < ITEMS; ++j) {
         const uint32_t i = tid * ITEMS + j;
@@ -612,6 +700,7 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     mine += valid ? 1u : 0u;
     dmask |= (valid ? 0u : 1u) << j;
   }
+  FSTAMP(4);
   uint32_t distinct;
   {
     uint32_t v = mine;
@@ -624,12 +713,20 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
     for (int w = 0; w < kSelWaves; ++w) distinct += wsum[w];
     __syncthreads();
   }
+  FSTAMP(5);
   if (distinct < s_param && retry_ok[g]) {
-    if (tid == 0) res[g] = ~0ull;
+    if (tid == 0) {
+      res[g] = ~0ull;
+      if (set_sizes) set_sizes[g] = 0;
+    }
     return;
   }
   const uint64_t lim = distinct < s_param ? distinct : s_param;
-  if (tid == 0) res[g] = lim;
+  if (tid == 0) {
+    res[g] = lim;
+    if (set_sizes) set_sizes[g] = (uint32_t)lim;
+    if (set_starts) set_starts[g] = dst_off[g];
+  }
   uint64_t* dst = out + dst_off[g];
   const bool all = distinct <= lim;
   RadixSel sel{0, 0, 0, true};
@@ -648,6 +745,7 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
         },
         (uint32_t)lim, mx, hist, s_sel);
   }
+  FSTAMP(6);
   // keep (all distinct) or the selected ones, in k-mer order: the sorted keys,
   // their fmh and validity are in registers in blocked order (thread t holds
   // positions t * ITEMS ..), so two block scans place them — the ties at the
@@ -668,9 +766,15 @@ __global__ __launch_bounds__(kSelB) void k_bottom_fused(uint64_t* __restrict__ r
   for (uint32_t j = 0; j < ITEMS; ++j)
     if ((eq_m >> j) & 1u) keep_m |= (eq_rank++ < sel.kk ? 1u : 0u) << j;
   uint32_t pos = block_excl_scan((uint32_t)__builtin_popcount(keep_m), wsum);
+  // the kept keys go through LDS (the sorted keys' array is free again) so the
+  // global writes are coalesced and each expansion runs once per kept key
+  uint64_t* skept = reinterpret_cast<uint64_t*>(smem);
 #pragma unroll
   for (uint32_t j = 0; j < ITEMS; ++j)
-    if ((keep_m >> j) & 1u) dst[pos++] = runs_expand(k[j], runs);
+    if ((keep_m >> j) & 1u) skept[pos++] = k[j];
+  __syncthreads();
+  for (uint32_t i = tid; i < (uint32_t)lim; i += kSelB) dst[i] = runs_expand(skept[i], runs);
+  FSTAMP(7);
 }
 
 template <int FLAVOUR>
@@ -710,21 +814,17 @@ hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d
 
 BitRuns bit_runs(uint64_t mask) {
   BitRuns r;
-  int at = 0;
-  for (int b = 0; b < 64;) {
-    if (!((mask >> b) & 1)) {
-      ++b;
-      continue;
-    }
-    int e = b;
-    while (e < 64 && ((mask >> e) & 1)) ++e;
-    const int len = e - b;
-    r.src[r.n] = (uint8_t)b;
-    r.dst[r.n] = (uint8_t)at;
-    r.bits[r.n] = len == 64 ? ~0ull : ((1ull << len) - 1);
-    ++r.n;
-    at += len;
-    b = e;
+  for (int b = 0; b < 64; ++b)  // runs = set bits whose lower neighbour is clear
+    if (((mask >> b) & 1) && (b == 0 || !((mask >> (b - 1)) & 1))) ++r.n;
+  r.mask = mask;
+  uint64_t m = mask, mk = ~m << 1;  // Hacker's Delight 7-4: bits to move by 2^i
+  for (int i = 0; i < 6; ++i) {
+    uint64_t mp = mk ^ (mk << 1);
+    for (int sh = 2; sh < 64; sh <<= 1) mp ^= mp << sh;  // parallel prefix (zeros to the right)
+    const uint64_t mv = mp & m;
+    r.mv[i] = mv;
+    m = (m ^ mv) | (mv >> (1 << i));
+    mk &= ~mp;
   }
   return r;
 }
@@ -910,14 +1010,26 @@ hipError_t launch_bottom_fused(uint64_t* rec, const uint64_t* d_src_off, const u
                                const uint64_t* d_retry_ok, const uint64_t* d_dst_off,
                                uint32_t n_seg, uint64_t max_cnt, uint64_t s_param, int key_bits,
                                const BitRuns& runs, uint64_t kconst, int flavour, uint64_t* out,
-                               uint64_t* d_res, hipStream_t s) {
+                               uint64_t* d_res, hipStream_t s, const uint64_t* d_cap, uint32_t* set_sizes,
+                               uint64_t* set_starts) {
   if (n_seg == 0) return hipSuccess;
+  if (max_cnt > kFuseCap) return hipErrorInvalidValue;
   auto go = [&](auto kernel, size_t lds) -> hipError_t {
     const hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (a != hipSuccess) return a;
     hipLaunchKernelGGL(kernel, dim3(n_seg), dim3(kSelB), lds, s, rec, d_src_off, d_cnt, d_retry_ok,
-                       d_dst_off, s_param, key_bits, runs, kconst, out, d_res);
+                       d_dst_off, s_param, key_bits, runs, kconst, out, d_res, d_cap, set_sizes, set_starts);
+#ifdef SKS_FUSE_STAMPS
+    {
+      unsigned long long h[10] = {0};
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fuse_stamps), sizeof h);
+      fprintf(stderr, "[k_bottom_fused stamps] n_seg %u max_cnt %llu: zero %llu count %llu scatter %llu isort %llu "
+              "hash %llu distinct %llu select %llu write %llu\n", n_seg, (unsigned long long)max_cnt, h[0], h[1],
+              h[2], h[3], h[4], h[5], h[6], h[7]);
+    }
+#endif
     return hipGetLastError();
   };
   if (max_cnt <= kSelB * 8)

@@ -89,21 +89,33 @@ hipError_t seg_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const uin
 // (a pext) is order-preserving and injective: the post-scan sorts then run
 // ceil(popcount / 8) radix passes instead of ceil(top bit / 8)
 // (config 3, w=31/k=21: 42 bits instead of 62, 6 passes instead of 8).
+// The gather runs as Hacker's Delight's compress / expand butterfly (7-4,
+// 7-5): six masks of bits moving right by 1, 2, 4, ... 32, computed on the host,
+// so a pack is at most six and/xor/shift/or steps on SGPR constants (a
+// 2-bit-granular k-mer mask never moves a bit by an odd amount: five).
 struct BitRuns {
-  uint32_t n = 0;           // 0: identity
-  uint8_t src[32], dst[32];  // run start in the k-mer / in the packed key
-  uint64_t bits[32];         // low-aligned run masks
+  uint32_t n = 0;    // runs of set bits of the mask; 0: not packed (identity)
+  uint64_t mask = 0;
+  uint64_t mv[6] = {0, 0, 0, 0, 0, 0};
 };
 BitRuns bit_runs(uint64_t mask);
 hipError_t launch_bits_expand(uint64_t* keys, uint64_t n, const BitRuns& runs, hipStream_t s);
 // Bottom-s post-processing per genome in one workgroup (post.hip
 // k_bottom_fused): genomes of <= bottom_fused_capacity() candidates.
+// d_res[g] = sketch size; ~0: fewer than s distinct candidates under a finite
+// threshold (retry); kBottomOverflow: d_cnt[g] > d_cap[g] (the scan dropped
+// records; d_cap may be null when the counts are known to fit).  max_cnt: a
+// bound of every d_cnt[g] (or of d_cap[g]) below the capacity.  set_sizes /
+// set_starts (may be null): the sketch set's device arrays, written per genome
+// (size, dst_off[g]) so a build needs no host round trip before them.
+constexpr uint64_t kBottomOverflow = ~1ull;
 uint32_t bottom_fused_capacity();
 hipError_t launch_bottom_fused(uint64_t* rec, const uint64_t* d_src_off, const uint64_t* d_cnt,
                                const uint64_t* d_retry_ok, const uint64_t* d_dst_off,
                                uint32_t n_seg, uint64_t max_cnt, uint64_t s_param, int key_bits,
                                const BitRuns& runs, uint64_t kconst, int flavour, uint64_t* out,
-                               uint64_t* d_res, hipStream_t s);
+                               uint64_t* d_res, hipStream_t s, const uint64_t* d_cap = nullptr,
+                               uint32_t* set_sizes = nullptr, uint64_t* set_starts = nullptr);
 
 // Compact sparse survivor regions [off[g], off[g] + cnt[g]) into dense CSR,
 // packing each value's mask bits when `pack` is given.
@@ -187,7 +199,9 @@ uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch 
 // bounds computed from these sketches; temp: join_layout_temp_bytes;
 // d_stat[0] is raised to the largest block-bucket population (entries),
 // d_stat[1] counts groups the build could not place (layout invalid).  Three
-// launches, no host synchronisation.
+// launches, no host synchronisation.  `zero`: up to three word spans the build's
+// second launch clears before the placement runs (the caller's status words,
+// count tiles, tile counters: no memset launches of their own).
 uint32_t join_layout_groups(uint32_t log_b);
 // log2 of the value groups per region a build of n_blk blocks uses (1..3)
 uint32_t join_layout_region_log(uint32_t n_blk, uint32_t log_b);
@@ -195,10 +209,15 @@ uint32_t join_layout_boff_words(uint32_t log_b);  // B + NR: one block's boff ro
 hipError_t join_layout_bounds(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                               uint32_t count, uint32_t log_b, int ew, uint64_t* bounds, hipStream_t s);
 size_t join_layout_temp_bytes(uint32_t count, uint32_t log_b, int ew);
+struct ZeroSpans {
+  uint32_t* p[3];     // 4-byte aligned, null: unused
+  uint64_t words[3];
+};
 hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const uint32_t* sizes,
                              uint32_t count, uint32_t log_b, int ew, const uint64_t* d_bounds, void* temp,
                              uint64_t* out_vals, uint64_t* out_masks, uint32_t* out_boff,
-                             uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s);
+                             uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s,
+                             const ZeroSpans* zero = nullptr);
 // Tiles of the n x n (sym: upper-triangle range [tile_begin, tile_end), or
 // with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
 // written) or rows x n matrix; tile (I, J) reads row block r_blk0 + I of

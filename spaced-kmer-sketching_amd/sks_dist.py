@@ -510,7 +510,7 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
         # one call: layout + every tile (+ the fused ANI) natively (sks_all_pairs_ani)
         nb = (n_genomes + TILE - 1) // TILE
         res.tiles = _all_tiles(nb)
-        res.counts = ops.parts(len(res.tiles), device)
+        res.counts = ops.parts(len(res.tiles), device, zeroed=False)  # the call clears them
         if n_genomes:
             ops.all_pairs(mine, mx, res.counts, ani_ones if fused else None, ani_out if fused else None)
         if dst is not None:
@@ -677,9 +677,10 @@ class GpuJoinOps:
     def stats_since(self, mark):
         return self.stats[mark:self.n_stats]
 
-    def parts(self, T, device):
-        """Zeroed packed count tiles [T, 64, 64]."""
-        return torch.zeros((max(T, 1), TILE, TILE), dtype=torch.int32, device="cuda")
+    def parts(self, T, device, zeroed=True):
+        """Packed count tiles [T, 64, 64], zeroed unless the kernels clear them."""
+        f = torch.zeros if zeroed else torch.empty
+        return f((max(T, 1), TILE, TILE), dtype=torch.int32, device="cuda")
 
     def bounds_like(self, log_b):
         return torch.empty((self.sksffi.join_layout_groups(log_b) + 1) * self.ew, dtype=torch.int64, device="cuda")

@@ -246,7 +246,7 @@ class NpJoinOps:
                         ani[i, j] = O.binomial_estimator(O.containment(x, int(sizes[i])), k)
                         ani[j, i] = O.binomial_estimator(O.containment(x, int(sizes[j])), k)
 
-    def parts(self, T, device):
+    def parts(self, T, device, zeroed=True):
         return torch.zeros((max(T, 1), 64, 64), dtype=torch.int32)
 
     def pad(self, src, stride, data, sizes):

@@ -212,9 +212,9 @@ def test_bottom_s_fused_small_k(torch_cuda, ctx, w, k):
 
 
 def test_bottom_s_unfused_paths(torch_cuda, ctx, monkeypatch):
-    """The per-genome fused post kernel is the default for builds of two or more
-    genomes of <= 16384 candidates (a single genome takes the device-wide path);
-    SKS_NO_FUSED_BOTTOM routes them through compaction + segmented sort + unique
+    """The per-genome fused post kernel is the default for genomes of <= 16384
+    candidates; SKS_NO_FUSED_BOTTOM routes a build of several genomes through
+    compaction + segmented sort + unique
     + k_bottom_select instead. Both must give the oracle's sets; both selects
     stop their radix passes early once the chosen digit's bucket is kept whole."""
     genomes = [synth.bases(3000 + 997 * i, seed=1300 + i % 3, mut_seed=1400 + i,
@@ -225,6 +225,31 @@ def test_bottom_s_unfused_paths(torch_cuda, ctx, monkeypatch):
         for s_ in (1, 300):
             ss, _ = build(torch_cuda, ctx, genomes, 31, m, "bottom", s_, flavour)
             check_against_oracle(ss, genomes, 31, m, "bottom", s_, flavour)
+
+
+def test_bottom_s_single_genome_paths(torch_cuda, ctx, monkeypatch):
+    """One genome per build (kmer_set_from_fasta_file's shape): by default the
+    single-round-trip path (scan + k_bottom_fused into the set's own arrays,
+    one read-back); SKS_NO_FAST_BOTTOM takes the general build. Tiny, ordinary,
+    A/C-only (the fused kernel's block-sort fallback), mutated and periodic
+    genomes (too few distinct candidates: the fast path falls back and the
+    threshold is raised), both flavours, each against the oracle."""
+    rng = np.random.default_rng(91)
+    ac = np.where(rng.random(150_000) < 0.5, ord("A"), ord("C")).astype(np.uint8).tobytes()
+    unit = synth.bases(37, seed=92).tobytes()
+    genomes = [synth.bases(10, seed=93).tobytes(), synth.bases(60_000, seed=94).tobytes(), ac,
+               synth.bases(400_000, seed=95, mut_seed=96, mut_rate=0.03).tobytes(), unit * 4000]
+    m = O.mask(31, 21, 0)
+    for fast in (True, False):
+        if fast:
+            monkeypatch.delenv("SKS_NO_FAST_BOTTOM", raising=False)
+        else:
+            monkeypatch.setenv("SKS_NO_FAST_BOTTOM", "1")
+        for flavour in (0, 1):
+            for s_ in (1, 700, 10000):
+                for g in genomes:
+                    ss, _ = build(torch_cuda, ctx, [g], 31, m, "bottom", s_, flavour)
+                    check_against_oracle(ss, [g], 31, m, "bottom", s_, flavour)
 
 
 def test_bottom_s_low_complexity_forces_threshold_retry(torch_cuda, ctx):

@@ -55,12 +55,29 @@ def main():
     def avj(**kw):
         return sks_dist.all_vs_all_join(n, 1, 0, src, ops, sksffi.join_layout_log_b, device="cuda", dst=None,
                                         max_size=mx, size_bound=bench.C4_S, **kw)
-    run("counts only (native, packed)", lambda: avj())
-    run("fused ANI -> host coarse (native)", lambda: avj(ani_ones=ones, ani_out=nc))
-    ops.no_native = True
-    run("counts only (python, dense)", lambda: avj())
-    run("fused ANI -> host coarse (python)", lambda: avj(ani_ones=ones, ani_out=nc))
-    ops.no_native = False
+    def interleaved(cases):  # alternate the cases rep by rep (clock drift hits all alike)
+        ms = {lab: [] for lab, _ in cases}
+        for _ in range(reps + 1):
+            for lab, fn in cases:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ms[lab].append((time.perf_counter() - t0) * 1e3)
+        for lab, _ in cases:
+            v = ms[lab][1:]
+            print(f"{lab:34s} median {statistics.median(v):.3f} ms  min {min(v):.3f}", flush=True)
+
+    def py(**kw):
+        ops.no_native = True
+        try:
+            avj(**kw)
+        finally:
+            ops.no_native = False
+    interleaved([("counts only (native, packed)", lambda: avj()),
+                 ("counts only (python, dense)", lambda: py()),
+                 ("fused ANI -> host coarse (native)", lambda: avj(ani_ones=ones, ani_out=nc)),
+                 ("fused ANI -> host coarse (python)", lambda: py(ani_ones=ones, ani_out=nc))])
     run("fused ANI -> device", lambda: avj(ani_ones=ones, ani_out=dev))
     run("fused ANI -> device + 8 MB copy", lambda: (avj(ani_ones=ones, ani_out=dev),
                                                     pinned.copy_(dev.view(-1), non_blocking=True)))

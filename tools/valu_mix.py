@@ -70,17 +70,24 @@ def main(dst=None):
         text = open(os.path.join(td, s)).read()
     a = text.index(KERNEL + ":")
     b = text.index(".Lfunc_end", a)
-    blocks, cur = [], []
+    blocks, cur, full, fcur = [], [], [], []
     for line in text[a:b].splitlines():
         if re.match(r"^(\.LBB\w+|; %bb\.\d+):", line):
             blocks.append(cur)
-            cur = []
+            full.append(fcur)
+            cur, fcur = [], [line.strip()]
             continue
         t = line.strip()
         if t.startswith("v_"):
             cur.append(t)
+        if t and not t.startswith((";", ".")):
+            fcur.append(t)
     blocks.append(cur)
-    hot = max(blocks, key=len)
+    full.append(fcur)
+    hot_i = max(range(len(blocks)), key=lambda i: len(blocks[i]))
+    hot = blocks[hot_i]
+    if os.environ.get("SKS_VALU_LISTING"):  # the hot block's whole instruction text
+        open(os.environ["SKS_VALU_LISTING"], "w").write("\n".join(full[hot_i]) + "\n")
     table, cycles = {}, 0.0
     for ins in hot:
         op = ins.split()[0]
