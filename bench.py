@@ -549,9 +549,10 @@ C2_LEN, C2_SEED, C2_S, C2_BATCH = 5_000_000, 2, 10000, 64
 def run_c2(ctx, mask, steps, warmup, inflight=2, cpu=False):
     """Config 2 of BASELINE.json: one 5 Mb bacterial-scale genome (synthetic,
     seed 2), w=31/k=21 spaced seed, bottom-s s=10000.  One such build is
-    launch/latency-bound (a few hundred microseconds of GPU work spread over a
-    dozen launches and two host syncs), so three numbers are reported, each
-    named for what it is:
+    launch/latency-bound (a metadata upload, the scan, the fused bottom-s
+    kernel writing the set's arrays and one read-back: api.cpp
+    build_bottom_single), so three numbers are reported, each named for what
+    it is:
       * single: K builds one at a time — wall time per build (k-mers/s of a
         complete sks_sketch_build) and the scan kernel's own time (hipEvents)
         with its HBM roofline fraction;

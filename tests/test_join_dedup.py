@@ -224,3 +224,48 @@ def test_layout_pass_splits_u64(torch_cuda, ctx):
         assert ctx.join_check_violations() == 0
     finally:
         ctx.set_join_check(False)
+
+
+def test_layout_invalid_flag_reaches_all_vs_all(torch_cuda, ctx, monkeypatch):
+    """128-bit values whose 64-bit layout mixes all collide (lo = C ^ (hi * K1 +
+    K2), join_common.hpp kv_mix) fill a layout slice that no hash split can cut
+    (group cap 64): the build sets status word 1 (layout invalid).
+    sks_intersect_all retries and falls back to an exact kernel (counts equal
+    numpy's); sks_dist.all_vs_all_join — the one-call native path and the
+    layout-by-layout path — reports it through JoinResult.check_layouts
+    (RuntimeError) instead of returning its counts silently."""
+    import sks_dist
+    torch = torch_cuda
+    monkeypatch.setenv("SKS_LAYOUT_GROUP_CAP", "64")
+    rng = np.random.default_rng(31)
+    n = 70
+    hi = np.arange(1000, 1300, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        lo = np.uint64(0x1234567) ^ (hi * np.uint64(0xC2B2AE3D27D4EB4F) + np.uint64(0x165667B19E3779F9))
+    coll = np.stack([lo, hi], axis=1)
+    sk = []
+    for i in range(n):
+        ex = rng.integers(2**40, 2**63, size=(300, 2), dtype=np.uint64)
+        a = np.unique(np.concatenate([coll[rng.random(len(coll)) < 0.8], ex]), axis=0)
+        sk.append(a[np.lexsort((a[:, 0], a[:, 1]))])
+    want = np.array([[_wide_count(sk[i], sk[j]) for j in range(n)] for i in range(n)])
+    sizes = np.array([len(x) for x in sk], dtype=np.uint32)
+    starts = np.zeros(n, dtype=np.uint64)
+    starts[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    flat = np.concatenate([x.reshape(-1) for x in sk])
+    d = torch.from_numpy(flat.view(np.int64)).to("cuda:0")
+    st = torch.from_numpy(starts.view(np.int64)).to("cuda:0")
+    sz = torch.from_numpy(sizes.view(np.int32)).to("cuda:0")
+    out = torch.full((n * n,), -3, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_all(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 2, n, 0, n, out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(n, n), want)
+    src = sks_dist.Sketches(d, sz, 2, starts=st)
+    ops = sks_dist.GpuJoinOps(ctx, ew=2)
+    for native in (True, False):
+        ops.no_native = not native
+        res = sks_dist.all_vs_all_join(n, 1, 0, src, ops, sksffi.join_layout_log_b, device="cuda", dst=None,
+                                       max_size=int(sizes.max()))
+        with pytest.raises(RuntimeError, match="join layout"):
+            res.check_layouts()
+    ops.no_native = False

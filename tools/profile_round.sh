@@ -31,6 +31,10 @@ SKS_BENCH_KERNELS=join timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU 
 SKS_BENCH_KERNELS=join timeout -k 10 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d $OUT/pairs/p2 -o run -- python3 $R/tools/bench_pairs.py 1000 2 > $OUT/pairs2.log 2>&1
 SKS_BENCH_KERNELS=join timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/pairs_wide/p1 -o run -- python3 $R/tools/bench_pairs.py 1000 2 family 45 > $OUT/pairsw1.log 2>&1
 SKS_BENCH_KERNELS=join timeout -k 10 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d $OUT/pairs_wide/p2 -o run -- python3 $R/tools/bench_pairs.py 1000 2 family 45 > $OUT/pairsw2.log 2>&1
+# k_join's memory side: bytes past L2 (FETCH_SIZE: L2-to-fabric requests, Infinity-Cache hits
+# included) and the L2 hit rate, one pass each
+SKS_BENCH_KERNELS=join timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pairs_mem/p1 -o run -- python3 $R/tools/bench_pairs.py 1000 2 > $OUT/pairsm1.log 2>&1
+SKS_BENCH_KERNELS=join timeout -k 10 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/pairs_mem/p2 -o run -- python3 $R/tools/bench_pairs.py 1000 2 > $OUT/pairsm2.log 2>&1
 echo "pair counters done"
 python3 $R/tools/summarize_round.py $OUT $OUT/summary $WARMUP $STEPS
 echo profile done
