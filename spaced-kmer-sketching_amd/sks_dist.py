@@ -455,9 +455,12 @@ class JoinResult:
                                "values); its counts are invalid — use sks_intersect_all")
 
 
+@functools.lru_cache(maxsize=16)
 def _all_tiles(nb):
     I, J = np.triu_indices(nb)
-    return np.stack([I, J], axis=1).astype(np.int64)
+    t = np.stack([I, J], axis=1).astype(np.int64)
+    t.flags.writeable = False  # cached: shared by every caller
+    return t
 
 
 def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None,
@@ -718,16 +721,17 @@ class GpuJoinOps:
         if self.n_stats == self.stats.shape[0]:
             self.stats = torch.cat([self.stats, torch.zeros_like(self.stats)])
         self.n_stats += 1
-        return self.stats[self.n_stats - 1].data_ptr()
+        return self.stats.data_ptr() + 8 * (self.n_stats - 1)  # row n_stats - 1: two int32
 
     def all_pairs(self, src, max_size, out, k, ani):
         """sks_all_pairs_ani: one layout of src, every upper-triangle tile into the
         packed out [T, 64, 64], and the ANI into ani when k is given."""
         ani_ptr = (ani.data_ptr() if hasattr(ani, "data_ptr") else ani.ptr) if k is not None else 0
+        d, st, sz = src.ptrs if getattr(src, "ptrs", None) else \
+            (src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr())
         _ctx_waits_for_torch(self.ctx)
-        self.ctx.all_pairs_ani(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
-                               max(int(max_size), 1), max(src.total, 1), k or 0, ani_ptr, out.data_ptr(),
-                               self._stat_slot(), elem_words=self.ew)
+        self.ctx.all_pairs_ani(d, st, sz, src.n, max(int(max_size), 1), max(src.total, 1), k or 0, ani_ptr,
+                               out.data_ptr(), self._stat_slot(), elem_words=self.ew)
         _torch_waits_for_ctx(self.ctx)
         self.keep["all_pairs"] = src
 
@@ -775,14 +779,33 @@ class GpuJoinOps:
         self.keep["ani_sizes"] = sizes
 
 
+class _SetSketches(Sketches):
+    """Sketches of a SketchSet: the device pointers at once (`ptrs`, all the
+    one-call native path needs), the zero-copy torch views built on first use."""
+
+    def __init__(self, ss):
+        self._ss, self.ew, self.n = ss, ss.elem_words, ss.n
+        self.total = int(ss.sizes().astype(np.int64).sum())
+        self.ptrs = tuple(int(p or 0) for p in ss.device_ptrs())
+        self._t = None
+
+    def _views(self):
+        if self._t is None:
+            self._t = self._ss.device_tensors(torch.cuda.current_device())
+        return self._t
+
+    data = property(lambda self: self._views()[0])
+    starts = property(lambda self: self._views()[1])
+    sizes = property(lambda self: self._views()[2])
+
+
 def sketches_of(ss, ew=None):
     """Sketches (zero-copy device views) of a SketchSet, or an empty set for None."""
     if ss is None:
         e = ew or 1
         return Sketches(torch.zeros(0, dtype=torch.int64, device="cuda"),
                         torch.zeros(0, dtype=torch.int32, device="cuda"), e)
-    d, st, sz = ss.device_tensors(torch.cuda.current_device())
-    return Sketches(d, sz, ss.elem_words, starts=st)
+    return _SetSketches(ss)
 
 
 # ---- one genome across ranks (SURVEY §8e, config 3 strong scaling) -----------------------

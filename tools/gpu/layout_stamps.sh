@@ -5,7 +5,7 @@ O=$R/gpurun_out/stamps
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for m in family indep; do
-  SKS_LIB=$R/variants/libsks_stamps.so SKS_BENCH_KERNELS=join timeout -k 10 200 python3 $R/tools/bench_pairs.py 1000 2 $m > $O/$m.txt 2>&1
+  SKS_LIB=$R/variants/libsks_lstamp.so SKS_BENCH_KERNELS=join timeout -k 10 200 python3 $R/tools/bench_pairs.py 1000 2 $m > $O/$m.txt 2>&1
 done
-SKS_LIB=$R/variants/libsks_stamps.so SKS_BENCH_KERNELS=join timeout -k 10 200 python3 $R/tools/bench_pairs.py 200 2 family > $O/c5.txt 2>&1
+SKS_LIB=$R/variants/libsks_lstamp.so SKS_BENCH_KERNELS=join timeout -k 10 200 python3 $R/tools/bench_pairs.py 200 2 family > $O/c5.txt 2>&1
 echo done
