@@ -138,6 +138,7 @@ def sum_vector_over_ranks(v, world):
 
 # all-vs-all sketch exchange between ranks (sks_dist.all_vs_all_join): p2p | allgather | broadcast
 EXCHANGE = "p2p"
+WORLD1_EXCHANGE = False  # --world1-exchange: a world-1 process group keeps the exchange path
 
 
 # ---- config 3 ---------------------------------------------------------------------
@@ -760,7 +761,7 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
                                         ani_ones=ones if with_ani else None,
                                         ani_out=host_ani if with_ani else None,
                                         max_size=int(ss.sizes().max()) if ss is not None and ss.n else None,
-                                        size_bound=C4_S, exchange=EXCHANGE)
+                                        size_bound=C4_S, exchange=EXCHANGE, world1_exchange=WORLD1_EXCHANGE)
 
     t_sketch = t_pairs = t_counts = 0.0
     timed = 0
@@ -1314,6 +1315,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--exchange", default="p2p", choices=["p2p", "allgather", "broadcast"],
                     help="config-4 sketch exchange between ranks (sks_dist.all_vs_all_join)")
+    ap.add_argument("--world1-exchange", action="store_true",
+                    help="with --dist-rehearsal: config 4 at world 1 takes the multi-rank exchange path "
+                         "(own layout + tile list + the exchange calls, which move nothing) instead of "
+                         "the one-call native path, to measure that path's fixed cost")
     ap.add_argument("--dist-rehearsal", action="store_true",
                     help="start the process group at world 1 too (under torchrun), so the "
                          "collective paths run on the backend")
@@ -1321,8 +1326,9 @@ def main():
                     help="PMC HBM traffic of the scan launches this command times "
                          "(tools/profile_round.sh; default: the newest profiles/rNN)")
     args = ap.parse_args()
-    global EXCHANGE
+    global EXCHANGE, WORLD1_EXCHANGE
     EXCHANGE = args.exchange
+    WORLD1_EXCHANGE = args.world1_exchange
 
     world, rank, local = dist_setup(args.gpus, args.dist_backend, args.dist_rehearsal)
     ctx = sksffi.Context(local)

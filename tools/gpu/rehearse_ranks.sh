@@ -15,3 +15,7 @@ timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1
   --master-port 29517 bench.py --dist-rehearsal --no-sweep --no-e2e --no-cpu-baseline --no-c2 --steps 3 --warmup 1 \
   > $O/bench_1rank_rccl.json 2> $O/bench_1rank_rccl.err
 echo "rccl world 1 done"
+timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29518 bench.py --dist-rehearsal --world1-exchange --no-sweep --no-e2e --no-cpu-baseline --no-c2 \
+  --steps 3 --warmup 1 > $O/bench_1rank_rccl_exchange.json 2> $O/bench_1rank_rccl_exchange.err
+echo "rccl world 1 exchange path done"
