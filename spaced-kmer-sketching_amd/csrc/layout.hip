@@ -293,6 +293,9 @@ __device__ unsigned long long g_layout_stamps_wg[kMaxStampWgs * 5];
 #define SKS_PLACE_DIAG 0
 #endif
 constexpr int kPB = 256;                     // threads of the placement kernel
+#ifndef SKS_LAYOUT_STAGED
+#define SKS_LAYOUT_STAGED 1  // normal-path emit through an LDS list in place order (coalesced stores)
+#endif
 constexpr int kTPS = kPB / 64;               // threads per sketch in the register path (4)
 #ifndef SKS_LAYOUT_REGPER
 #define SKS_LAYOUT_REGPER 12
@@ -502,6 +505,9 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
   __shared__ uint32_t s_bcnt[1u << jc::kGLog];
   __shared__ uint32_t s_full, s_pcnt, s_gd, s_qn, s_qd;
   __shared__ unsigned long long s_stk[2 * 72];  // slice path: (slice prefix, level) work stack (prefixes up to 64 bits)
+#if SKS_LAYOUT_STAGED
+  __shared__ uint16_t s_stage[kGCap];  // normal-path emit: the group's entries' element indices, in place order
+#endif
 
   const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
   const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b, rg), BW = jc::lay_boff_words(log_b);
@@ -634,6 +640,24 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
           maxb = max(maxb, c);
         }
         if ((uint32_t)tid < GB) boff[g * GB + tid] = cur + pre[tid];
+#if SKS_LAYOUT_STAGED
+        // representatives list their element at its place (and free their slot);
+        // the group's entries then leave with coalesced stores
+#pragma unroll
+        for (int k = 0; k < kRegPer; ++k) {
+          if (rep[k] == kTFree) continue;
+          s_stage[pre[rep[k] >> 12] + (rep[k] & 4095u)] = (uint16_t)(gj.gpre + sub + kTPS * k);
+          s_tab[h[k]] = kTFree;
+        }
+        __syncthreads();
+        for (uint32_t e = (uint32_t)tid; e < tot; e += kPB) {
+          const uint32_t i = s_stage[e];
+          const uint64_t o = base + cur + e;
+          kv_store<EW>(out_vals, o, key_at<EW>(s_key, i));
+          out_masks[o] = s_msk[i];
+          s_msk[i] = 0;
+        }
+#else
 #pragma unroll
         for (int k = 0; k < kRegPer; ++k) {
           if (rep[k] == kTFree) continue;
@@ -646,6 +670,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
           s_msk[i] = 0;
           s_tab[h[k]] = kTFree;
         }
+#endif
         cur += tot;
         done = true;
       } else {  // a bucket region overflowed: clean up, place the group in bucket passes
@@ -879,6 +904,7 @@ __global__ __launch_bounds__(kPB) void k_gl_place(const uint64_t* __restrict__ d
 // it is the first value of bucket 0 (and of the first slice of bucket 0).
 constexpr uint32_t kVLog = 8 + jc::kGLog, kVT = 1u << kVLog;  // value slots (2048)
 constexpr uint32_t kVSpt = kVT / kPB;              // slots per thread in a scan emit (8)
+
 static_assert(kGCap <= kVT, "a normal-path group fits the value table");
 #ifndef SKS_LAYOUT_HALF_AT
 #define SKS_LAYOUT_HALF_AT (kVT / 2)
@@ -934,6 +960,9 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(SKS_LAYOUT_
   __shared__ unsigned long long s_sq[72];     // pass stack: q0
   __shared__ uint32_t s_sl[72];               // pass stack: lvl << 8 | log2(span)
   __shared__ uint32_t s_w8[(1u << jc::kGLog) * (kPB / 64)];  // pass emit: per-bucket wave totals
+#if SKS_LAYOUT_STAGED
+  __shared__ uint16_t s_stage[kVT];  // normal-path emit: the group's entries' table slots, in place order
+#endif
 
   const uint32_t B = 1u << log_b, gb_log = jc::lay_gb_log(log_b), GB = 1u << gb_log;
   const uint32_t G = B >> gb_log, NR = jc::lay_regions(log_b, rg), BW = jc::lay_boff_words(log_b);
@@ -1130,6 +1159,29 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(SKS_LAYOUT_
           maxb = max(maxb, c + (b == 0 ? zero : 0u));
         }
         if ((uint32_t)tid < bn) boff[g * GB + blo + tid] = cur + (tid == 0 ? 0u : pre[blo + tid]);
+#if SKS_LAYOUT_STAGED
+        // each representative lists its table slot at its place; then the group's
+        // entries leave with coalesced stores (a wave writes 512 contiguous bytes
+        // of values and of masks) instead of one scattered 8-byte store each
+#pragma unroll
+        for (int k = 0; k < kRegPer; ++k)
+          if (rep[k] != kTFree) s_stage[pre[rep[k] >> 12] + (rep[k] & 4095u)] = (uint16_t)h[k];
+        if (tid == 0 && zero) s_stage[0] = 0xFFFFu;  // the value 0 (not in the table)
+        __syncthreads();
+        for (uint32_t e = (uint32_t)tid; e < tot; e += kPB) {
+          const uint32_t slot = s_stage[e];
+          const uint64_t o = base + cur + e;
+          if (slot == 0xFFFFu) {
+            out_vals[o] = 0ull;
+            out_masks[o] = s_zero;
+          } else {
+            out_vals[o] = s_vt[slot];
+            out_masks[o] = s_vm[slot];
+            s_vt[slot] = 0ull;
+            s_vm[slot] = 0ull;
+          }
+        }
+#else
 #pragma unroll
         for (int k = 0; k < kRegPer; ++k) {
           if (rep[k] == kTFree) continue;
@@ -1145,6 +1197,7 @@ __global__ __launch_bounds__(kPB) __attribute__((amdgpu_waves_per_eu(SKS_LAYOUT_
           out_vals[base + cur] = 0ull;
           out_masks[base + cur] = s_zero;
         }
+#endif
         cur += tot;
         dsum += tot;
         LSTAMP(3);
