@@ -26,7 +26,8 @@ extern "C" {
                               the layout entry points, sks_ctx_set_join_check; later additions
                               within 2 (new symbols only): sks_ani_rows, sks_intersect_layout_ani,
                               sks_host_alloc, sks_host_free, sks_join_layout_stat_copy,
-                              sks_sketches_export, sks_all_pairs_ani */
+                              sks_sketches_export, sks_all_pairs_ani,
+                              sks_ctx_set_layout_blocks_hint */
 
 typedef enum sks_status {
   SKS_OK = 0,
@@ -309,6 +310,12 @@ int sks_join_layout_build(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* 
  * layout is invalid (see max_block_bucket) — into d_dst (2 x u32, device), so
  * a caller that skips the read-back can check the layout after the join
  * without a stream round trip.  Call it right after the build. */
+/* Region-size hint for the next sks_join_layout_build calls on this context:
+ * the number of 64-sketch blocks that actually hold sketches (0, the default:
+ * every block does).  A build over a buffer with many empty rows — a rank's
+ * exchange buffer, a slot per rank — then picks the region size (workgroups
+ * per block) for its real work.  The layout's content does not depend on it. */
+int sks_ctx_set_layout_blocks_hint(sks_ctx* ctx, uint32_t blocks);
 int sks_join_layout_stat_copy(sks_ctx* ctx, uint32_t* d_dst);
 /* sks_intersect_sym over a join layout of n sketches: upper-triangle 64x64 tiles
  * [tile_begin, tile_end) into the n x n int32 matrix d_out (zeroed first). */

@@ -212,6 +212,7 @@ struct sks_ctx {
   int grid_override = 0;
   int intersect_algo = 0;  // sks::kIntersect*
   bool join_check = false;  // invariant-checking join / layout kernels (sks_ctx_set_join_check)
+  uint32_t layout_blocks_hint = 0;  // sks_ctx_set_layout_blocks_hint (0: every block holds sketches)
 };
 
 struct sks_kmer_list {
@@ -640,6 +641,12 @@ int sks_ctx_set_intersect_kernel(sks_ctx* c, int kind) {
   if (kind < SKS_INTERSECT_AUTO || kind > SKS_INTERSECT_GLOBAL)
     return sks::fail(SKS_E_ARG, "sks_ctx_set_intersect_kernel: unknown kernel");
   c->intersect_algo = kind;
+  return SKS_OK;
+}
+
+int sks_ctx_set_layout_blocks_hint(sks_ctx* c, uint32_t blocks) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_set_layout_blocks_hint: null ctx");
+  c->layout_blocks_hint = blocks;
   return SKS_OK;
 }
 
@@ -1667,7 +1674,8 @@ int sks_join_layout_build(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_
     SKS_HIP(hipMemsetAsync(d_out_bstart, 0, 8, c->stream));
   } else {
     SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, elem_words, d_bounds, w, d_out_vals,
-                                   d_out_masks, d_out_boff, d_out_bstart, stat, c->join_check, c->stream));
+                                   d_out_masks, d_out_boff, d_out_bstart, stat, c->join_check, c->stream, nullptr,
+                                   c->layout_blocks_hint));
   }
   if (max_block_bucket) {  // NULL: no read-back, the call does not wait for the build
     uint32_t h[2] = {0, 0};

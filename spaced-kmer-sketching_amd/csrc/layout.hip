@@ -1398,7 +1398,7 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
                              uint32_t count, uint32_t log_b, int ew, const uint64_t* d_bounds, void* temp,
                              uint64_t* out_vals, uint64_t* out_masks, uint32_t* out_boff,
                              uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s,
-                             const ZeroSpans* zero) {
+                             const ZeroSpans* zero, uint32_t blocks_hint) {
   if (log_b > jc::kMaxLogB || (ew != 1 && ew != 2)) return hipErrorInvalidValue;
   if (count == 0) return hipSuccess;
   const ZeroSpans zs = zero ? *zero : ZeroSpans{};
@@ -1414,7 +1414,9 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
   // workgroup (1024 or more workgroups), else fewer, down to 2, so a small
   // build (a rank's own blocks, config 5's four blocks) is not one long
   // sequence of groups per workgroup on a few CUs (SKS_LAYOUT_RG forces one)
-  const uint32_t rg = join_layout_region_log(n_blk, log_b);
+  // (blocks_hint: the blocks that hold sketches, when many are empty — a rank's
+  // exchange buffer — so the region size fits the work, not the row count)
+  const uint32_t rg = join_layout_region_log(blocks_hint ? std::min(blocks_hint, n_blk) : n_blk, log_b);
   const dim3 grid_place(n_blk * jc::lay_regions(log_b, rg));
   auto* masks = reinterpret_cast<unsigned long long*>(out_masks);
   if (ew == 1) {

@@ -217,7 +217,7 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
                              uint32_t count, uint32_t log_b, int ew, const uint64_t* d_bounds, void* temp,
                              uint64_t* out_vals, uint64_t* out_masks, uint32_t* out_boff,
                              uint64_t* out_bstart, uint32_t* d_stat, bool check, hipStream_t s,
-                             const ZeroSpans* zero = nullptr);
+                             const ZeroSpans* zero = nullptr, uint32_t blocks_hint = 0);
 // Tiles of the n x n (sym: upper-triangle range [tile_begin, tile_end), or
 // with d_tiles the (I, J) list entries [tile_begin, tile_end), both halves
 // written) or rows x n matrix; tile (I, J) reads row block r_blk0 + I of

@@ -225,8 +225,10 @@ def place_tiles(mat, tiles, parts, n):
 # The cross-rank tiles follow a cyclic plan (tile_plan_by_peer): rank r counts
 # every tile pairing its blocks with those of rank r + d (mod N) for
 # d = 1 .. N/2, the d = N/2 pairs (even N) split in halves between the two, so
-# a rank needs the sketches of N/2 peers, not N - 1, and builds N/2 peer
-# layouts (4 instead of 7 at N = 8).  Sketches travel padded to a common stride
+# a rank needs the sketches of N/2 peers, not N - 1.  They land in one buffer
+# holding a slot per rank (row g = genome g): ONE layout of the own and peer
+# rows (global block numbers, the other rows empty) and ONE join launch count
+# every cross tile.  Sketches travel padded to a common stride
 # (the caller's size bound, e.g. bottom-s s: no size exchange and no host
 # round trip), by one of three exchanges:
 #   "p2p"        batched send/recv, step d: send to r - d, receive from r + d
@@ -308,9 +310,8 @@ def peer_needs(n_genomes, world, rank):
 
 def peer_groups(n_genomes, world, rank):
     """(hi, lo): the peers above and below `rank` that its plan joins with,
-    ascending.  The cyclic plan's peers r + 1 .. r + N/2 (mod N) are at most two
-    runs of consecutive ranks, so each run's blocks are consecutive global
-    blocks: one layout and one join launch per run."""
+    ascending (the cyclic plan's peers r + 1 .. r + N/2 (mod N) are at most two
+    runs of consecutive ranks)."""
     need = peer_needs(n_genomes, world, rank)
     return [q for q in need if q > rank], [q for q in need if q < rank]
 
@@ -332,70 +333,64 @@ class Sketches:
         self.total = int(data.numel()) // ew
 
 
+_STRIDE_STARTS = {}
+
+
 def _strided(data, sizes, ew, stride):
     n = int(sizes.numel())
-    st = torch.arange(n, dtype=torch.int64, device=sizes.device) * stride
+    key = (n, stride, str(sizes.device))
+    st = _STRIDE_STARTS.get(key)
+    if st is None:  # the starts of a strided set depend on its shape only: built once
+        if len(_STRIDE_STARTS) > 16:
+            _STRIDE_STARTS.clear()
+        st = _STRIDE_STARTS[key] = torch.arange(n, dtype=torch.int64, device=sizes.device) * stride
     return Sketches(data[:n * stride * ew], sizes, ew, starts=st)
 
 
 def _exchange_start(own, n_genomes, world, rank, stride, ops, mode):
-    """Starts moving the sketches the cyclic plan needs, padded to `stride`
-    elements per sketch and `per` (a whole rank's block range) sketches per
-    rank, so a run of consecutive peers lands as ONE block-aligned strided set;
-    returns wait(group) -> Sketches of the peers of group "hi" / "lo"
-    (peer_groups).  With RCCL everything runs on the collective stream and
-    wait() only orders torch's current stream after it (the host does not
-    block); with gloo the data goes through host memory."""
+    """Starts moving the sketches the cyclic plan needs into ONE buffer of every
+    rank's slot — `per` rows (a whole rank's block range) of `stride` elements per
+    rank, so row g is genome g — and returns wait() -> those rows as Sketches
+    (this rank's own rows and its peers'; the rows of ranks it does not need,
+    and padding rows, hold size 0): one layout of all the rank's peers, with the
+    global block numbering.  This rank's slot is written by the export itself.
+    With RCCL everything runs on the collective stream and wait() only orders
+    torch's current stream after it (the host does not block); with gloo the
+    data goes through host memory."""
     ew, dev = own.ew, own.data.device
     nccl = dist.get_backend() == "nccl"
     bdev = dev if nccl else "cpu"
     per = block_shard(n_genomes, world, rank)[0] * TILE  # sketches of a full rank
     counts = [block_shard(n_genomes, world, q)[2] - block_shard(n_genomes, world, q)[1] for q in range(world)]
-    groups = dict(zip(("hi", "lo"), peer_groups(n_genomes, world, rank)))
-    # this rank's sketches at the common stride, `per` rows (rows past its
-    # count have size 0)
-    send = torch.full((per * stride * ew,), -1, dtype=torch.int64, device=dev)
-    send_sz = torch.zeros(per, dtype=torch.int32, device=dev)
+    row = per * stride * ew
+    full = torch.empty((world * row,), dtype=torch.int64, device=bdev)  # rows past a size are never read
+    full_sz = torch.zeros((world * per,), dtype=torch.int32, device=bdev)
+    slot = (slice(rank * row, (rank + 1) * row), slice(rank * per, (rank + 1) * per))
+    if nccl:
+        send, send_sz = full[slot[0]], full_sz[slot[1]]
+    else:  # the export runs where the sketches are; gloo sends from host memory
+        send = torch.full((row,), -1, dtype=torch.int64, device=dev)
+        send_sz = torch.zeros(per, dtype=torch.int32, device=dev)
     if own.n:
         ops.pad(own, stride, send, send_sz)
     if not nccl:
-        send, send_sz = send.cpu(), send_sz.cpu()
-    row = per * stride * ew
-    bufs = {}
-    for name, qs in groups.items():
-        if qs:
-            bufs[name] = (torch.empty(len(qs) * row, dtype=torch.int64, device=bdev),
-                          torch.zeros(len(qs) * per, dtype=torch.int32, device=bdev))
-
-    def slot(q):  # this rank's receive buffers for peer q
-        for name, qs in groups.items():
-            if q in qs:
-                i = qs.index(q)
-                d, sz = bufs[name]
-                return d[i * row:(i + 1) * row], sz[i * per:(i + 1) * per]
-        return None
+        full[slot[0]] = send.cpu()
+        full_sz[slot[1]] = send_sz.cpu()
+        send, send_sz = full[slot[0]], full_sz[slot[1]]
+    need = peer_needs(n_genomes, world, rank)
     works = []
     if mode == "allgather":
-        full = torch.empty((world * row,), dtype=torch.int64, device=bdev)
-        full_sz = torch.empty((world * per,), dtype=torch.int32, device=bdev)
-        if nccl:
+        if nccl:  # in place: this rank's input is its own slot of the output
             works = [dist.all_gather_into_tensor(full, send, async_op=True),
                      dist.all_gather_into_tensor(full_sz, send_sz, async_op=True)]
         else:
-            dist.all_gather(list(full.view(world, row).unbind(0)), send)
-            dist.all_gather(list(full_sz.view(world, per).unbind(0)), send_sz)
-        for name, qs in groups.items():  # consecutive ranks: one view each
-            if qs:
-                bufs[name] = (full[qs[0] * row:(qs[-1] + 1) * row], full_sz[qs[0] * per:(qs[-1] + 1) * per])
+            dist.all_gather(list(full.view(world, row).unbind(0)), send.clone())
+            dist.all_gather(list(full_sz.view(world, per).unbind(0)), send_sz.clone())
     elif mode == "broadcast":
         for q in range(world):
-            if not counts[q]:
-                continue
-            s_ = slot(q)
-            d, sz = (send, send_sz) if q == rank else (s_ if s_ is not None else
-                                                       (torch.empty(row, dtype=torch.int64, device=bdev),
-                                                        torch.zeros(per, dtype=torch.int32, device=bdev)))
-            works += [dist.broadcast(d, src=q, async_op=nccl), dist.broadcast(sz, src=q, async_op=nccl)]
+            if counts[q]:
+                works += [dist.broadcast(full[q * row:(q + 1) * row], src=q, async_op=nccl),
+                          dist.broadcast(full_sz[q * per:(q + 1) * per], src=q, async_op=nccl)]
     elif mode == "p2p":
         # every send and receive in one batch: all xGMI links at once (batches
         # issued one after another serialise on the communicator's stream)
@@ -404,9 +399,9 @@ def _exchange_start(own, n_genomes, world, rank, stride, ops, mode):
             to, frm = (rank - d_) % world, (rank + d_) % world
             if counts[rank] and rank in peer_needs(n_genomes, world, to):
                 ops_ += [(dist.isend, send, to), (dist.isend, send_sz, to)]
-            if frm in peer_needs(n_genomes, world, rank):
-                d, sz = slot(frm)
-                ops_ += [(dist.irecv, d, frm), (dist.irecv, sz, frm)]
+            if frm in need:
+                ops_ += [(dist.irecv, full[frm * row:(frm + 1) * row], frm),
+                         (dist.irecv, full_sz[frm * per:(frm + 1) * per], frm)]
         if ops_:
             if nccl:
                 works = dist.batch_isend_irecv([dist.P2POp(f, t, p) for f, t, p in ops_])
@@ -420,15 +415,13 @@ def _exchange_start(own, n_genomes, world, rank, stride, ops, mode):
                 w.wait()
         works = []
 
-    def wait(name):
+    def wait():
         for w in works:
             if w is not None:
                 w.wait()
         works.clear()
-        d, sz = bufs[name]
-        if not nccl:
-            d, sz = d.to(dev), sz.to(dev)
-        return _strided(d.reshape(-1), sz, ew, stride)
+        d, sz = (full, full_sz) if nccl else (full.to(dev), full_sz.to(dev))
+        return _strided(d, sz, ew, stride)
     return wait
 
 
@@ -563,25 +556,22 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     if len(local):  # the rank's own tiles while the peers' sketches travel
         count(own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
     off = len(local)
-    order = []
-    for name, qs in zip(("hi", "lo"), peer_groups(n_genomes, world, rank)):
-        if not qs:
-            continue
-        src = wait(name)  # the run of peers qs, block-aligned, one layout
-        lq = ops.build(src, log_b, gb, ("peer", name))
-        bq = block_shard(n_genomes, world, qs[0])[1] // TILE
-        tq = np.concatenate([remote[q] for q in qs]).reshape(-1, 2)
+    # every cross-rank tile of the plan in one join over one layout of the rank's
+    # own and peer rows (the exchange buffer: row g = genome g, so block numbers
+    # are global and blk0 = 0); rows the plan does not need are empty.  (One
+    # layout of the peer rows alone and two joins, own x peers and peers x own,
+    # measured 0.585 against 0.524 ms per rank at N = 8: tools/rank_sim.py)
+    tq = np.concatenate([remote[q] for q in peer_needs(n_genomes, world, rank)] +
+                        [np.zeros((0, 2), np.int64)]).reshape(-1, 2)
+    if len(tq):
+        union = wait()
+        held = sum((block_shard(n_genomes, world, q)[2] - block_shard(n_genomes, world, q)[1] + TILE - 1) // TILE
+                   for q in [rank] + peer_needs(n_genomes, world, rank))
+        lu = ops.build(union, log_b, gb, "peers", blocks_hint=held)
         if fused:
-            g_a = bq * TILE
-            g_b = min(n_genomes, g_a + src.n)
-            sizes_all[g_a:g_b] = src.sizes[:g_b - g_a]
-        if name == "hi":  # tiles (own block, peer block): rows own, columns the peers
-            count(own, g0 // TILE, lq, bq, tq, parts[off:off + len(tq)])
-        else:
-            count(lq, bq, own, g0 // TILE, tq, parts[off:off + len(tq)])
-        order.append(tq)
-        off += len(tq)
-    res.tiles = np.concatenate([local] + order).reshape(-1, 2)
+            sizes_all[:n_genomes] = union.sizes[:n_genomes]
+        count(lu, 0, lu, 0, tq, parts[off:off + len(tq)])
+    res.tiles = np.concatenate([local, tq]).reshape(-1, 2)
     res.counts = parts[:T]
     if stats_mark is not None:
         res._stats = ops.stats_since(stats_mark)
@@ -697,7 +687,10 @@ class GpuJoinOps:
         self.keep["bounds"] = src
         return b
 
-    def build(self, src, log_b, gb, key):
+    def build(self, src, log_b, gb, key, blocks_hint=0):
+        """The join layout of src (cached buffers per key).  blocks_hint: how many
+        of src's 64-sketch blocks hold sketches when most rows are empty (the
+        exchange buffer), so the build sizes its regions for the real work."""
         nb = (src.n + TILE - 1) // TILE
         shape = (max(src.total, 1), log_b, max(nb, 1))
         if self.bufs.get(key, (None,))[0] != shape:
@@ -709,9 +702,15 @@ class GpuJoinOps:
         lay = self.bufs[key][1]
         if src.n:
             _ctx_waits_for_torch(self.ctx)  # the buffers' previous readers, the source's writers
-            self.ctx.join_layout_build(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
-                                       log_b, *(t.data_ptr() for t in lay), stat=False, total=src.total,
-                                       bounds=gb.data_ptr() if gb is not None else None, elem_words=self.ew)
+            if blocks_hint:
+                self.ctx.set_layout_blocks_hint(blocks_hint)
+            try:
+                self.ctx.join_layout_build(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
+                                           log_b, *(t.data_ptr() for t in lay), stat=False, total=src.total,
+                                           bounds=gb.data_ptr() if gb is not None else None, elem_words=self.ew)
+            finally:
+                if blocks_hint:
+                    self.ctx.set_layout_blocks_hint(0)
             self.ctx.join_layout_stat_copy(self._stat_slot())
             _torch_waits_for_ctx(self.ctx)
         self.keep[key] = (src, gb)  # alive until torch's stream is past the build

@@ -49,6 +49,7 @@ EXPORTED = [
     "sks_fasta_stream", "sks_fasta_stream_bytes", "sks_fasta_runs", "sks_ctx_create",
     "sks_ctx_destroy", "sks_ctx_set_stream", "sks_ctx_synchronize", "sks_ctx_last_timings",
     "sks_sketch_build", "sks_sketch_set_free", "sks_sketch_set_free_on_stream", "sks_sketch_set_num", "sks_sketch_set_elem_words",
+    "sks_ctx_set_layout_blocks_hint",
     "sks_sketch_set_sizes", "sks_sketch_set_windows", "sks_sketch_set_device_data",
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
@@ -388,6 +389,10 @@ class Context:
                                           C.c_void_p(out_vals), C.c_void_p(out_masks), C.c_void_p(out_boff),
                                           C.c_void_p(out_bstart), C.byref(mx) if stat else None))
         return mx.value if stat else None
+
+    def set_layout_blocks_hint(self, blocks):
+        """sks_ctx_set_layout_blocks_hint: blocks that hold sketches in the next layout builds (0: all)."""
+        check(lib().sks_ctx_set_layout_blocks_hint(self.h, C.c_uint32(int(blocks))))
 
     def all_pairs_ani(self, data, starts, sizes, n, max_size, total, kmer_num_ones, ani, counts, status,
                       elem_words=1):

@@ -199,7 +199,7 @@ class NpJoinOps:
             out += [v & M64] if self.ew == 1 else [v & M64, v >> 64]
         return torch.tensor(np.array(out, dtype=np.uint64).view(np.int64))
 
-    def build(self, src, log_b, gb, key):
+    def build(self, src, log_b, gb, key, blocks_hint=0):
         G = sks_dist_groups(log_b)
         bnd = [_ival(gb, self.ew, g) for g in range(G + 1)]
         self.built.append((key, log_b, tuple(bnd)))
@@ -319,11 +319,12 @@ def _join_sketches(n_genomes, ew):
     (8, 3, 600, 1, "allgather", False)])
 def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bound):
     """Ranks build the layout of their own block-aligned genomes with rank 0's
-    bounds, count their own blocks' tiles first, then — as each peer's sketches
-    land (p2p send/recv, one all-gather, or per-source broadcasts; padded to the
-    caller's size bound, or to the all-reduced largest sketch) — build that
-    peer's layout and count the tiles of the cyclic plan pairing the two (rows
-    from the lower rank's blocks); the packed tiles go to dst (every rank for
+    bounds and count their own blocks' tiles first; once the peers' sketches
+    have landed in the rank's exchange buffer (p2p send/recv, one all-gather, or
+    per-source broadcasts; padded to the caller's size bound, or to the
+    all-reduced largest sketch) they build ONE layout of their own and peer rows
+    (global block numbers) and count every cross tile of the cyclic plan (rows
+    from the lower rank's blocks) in one join; the packed tiles go to dst (every rank for
     "all"), whose matrix equals the single-process merge counts, and the ANI
     each rank wrote for its tiles (both orientations) equals the reference
     formula, every ordered pair written by exactly one rank.  n = 200 at world
@@ -357,15 +358,13 @@ def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bou
         _, g0, _ = sks_dist.block_shard(n_genomes, world, r)
         expect = [(g0 // 64, g0 // 64, len(loc))] if len(loc) else []
         hi, lo = sks_dist.peer_groups(n_genomes, world, r)
-        for grp in (hi, lo):  # one layout and one join per run of consecutive peers
-            if grp:
-                bq = sks_dist.block_shard(n_genomes, world, grp[0])[1] // 64
-                nt = sum(len(rem[qq]) for qq in grp)
-                expect.append((g0 // 64, bq, nt) if grp is hi else (bq, g0 // 64, nt))
+        n_remote = sum(len(rem[qq]) for qq in hi + lo)
+        if n_remote:  # one layout of the own and peer rows (global blocks), one join of every cross tile
+            expect.append((0, 0, n_remote))
         assert calls == expect, (r, calls, expect)
-        # the cyclic plan: at most world // 2 peers, in at most two peer layouts per rank
+        # the cyclic plan: at most world // 2 peers, all in ONE peer layout per rank
         assert len(hi) + len(lo) <= world // 2
-        assert len([k for (k, _, _) in built if k != "own"]) <= 2
+        assert len([k for (k, _, _) in built if k != "own"]) <= 1
         for t, (I, J) in enumerate(tiles):
             for a, b in ((0, 0), (3, 7), (63, 62)):
                 i, j = I * 64 + a, J * 64 + b
