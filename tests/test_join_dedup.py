@@ -269,3 +269,42 @@ def test_layout_invalid_flag_reaches_all_vs_all(torch_cuda, ctx, monkeypatch):
         with pytest.raises(RuntimeError, match="join layout"):
             res.check_layouts()
     ops.no_native = False
+
+
+def test_layout_blocks_hint_sparse_rows(torch_cuda, ctx):
+    """A layout over rows most of which are empty (a rank's exchange buffer: a
+    slot per rank, only its own and its peers' rows filled) built with and
+    without sks_ctx_set_layout_blocks_hint: the hint only sizes the build's
+    regions, so the tiles among the filled blocks count the same — numpy's
+    intersections — either way."""
+    import sks_dist
+    torch = torch_cuda
+    rng = np.random.default_rng(41)
+    n, filled = 640, (0, 3, 7)  # 10 blocks, three hold sketches
+    base = [np.unique(rng.integers(0, 2**62, size=2500, dtype=np.uint64)) for _ in range(4)]
+    sk = []
+    for i in range(n):
+        if i // 64 in filled:
+            b = base[i % 4]
+            sk.append(np.unique(np.concatenate([b[rng.random(b.size) < 0.6],
+                                                rng.integers(0, 2**62, size=80, dtype=np.uint64)])))
+        else:
+            sk.append(np.zeros(0, np.uint64))
+    d, st, sz = _device_sketch_arrays(torch, sk)
+    src = sks_dist.Sketches(d, sz, 1, starts=st)
+    ops = sks_dist.GpuJoinOps(ctx)
+    log_b = sksffi.join_layout_log_b(max(len(x) for x in sk))
+    tiles = np.array([[0, 0], [0, 3], [0, 7], [3, 3], [3, 7], [7, 7]], dtype=np.int64)
+    got = []
+    for hint in (0, len(filled)):
+        lay = ops.build(src, log_b, None, ("hint", hint), blocks_hint=hint)
+        out = ops.parts(len(tiles), "cuda")
+        ops.count(n, log_b, lay, 0, lay, 0, tiles, out)
+        torch.cuda.synchronize()
+        got.append(out.cpu().numpy())
+    assert np.array_equal(got[0], got[1])
+    for t, (I, J) in enumerate(tiles):
+        for r in range(0, 64, 7):
+            for c in range(0, 64, 5):
+                want = np.intersect1d(sk[I * 64 + r], sk[J * 64 + c], assume_unique=True).size
+                assert got[1][t, r, c] == want, (I, J, r, c)
