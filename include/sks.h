@@ -27,7 +27,7 @@ extern "C" {
                               within 2 (new symbols only): sks_ani_rows, sks_intersect_layout_ani,
                               sks_host_alloc, sks_host_free, sks_join_layout_stat_copy,
                               sks_sketches_export, sks_all_pairs_ani,
-                              sks_ctx_set_layout_blocks_hint */
+                              sks_ctx_set_layout_blocks_hint, sks_ctx_ani_table */
 
 typedef enum sks_status {
   SKS_OK = 0,
@@ -399,6 +399,17 @@ int sks_all_pairs_ani(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_st
  * in whole lines).  No reference counterpart (the reference's result vectors
  * are plain host vectors, kmer-sketching.cpp:193). */
 int sks_host_alloc(uint64_t bytes, int coherent, void** out);
+/* ANI by shared-element count for sets of `size` elements, kept on the context:
+ * table[x] = binomial_estimator(containment(x, size), kmer_num_ones) for x in
+ * [0, size] (the same device function as the fused conversion, so the same
+ * doubles).  The fused ANI of sks_intersect_layout_ani / sks_all_pairs_ani then
+ * reads a row whose set holds `size` elements from the table instead of
+ * evaluating pow (bottom-s sets: every row).  Queued on the context stream;
+ * rebuilt only when (size, kmer_num_ones) changes; sizes above
+ * SKS_ANI_TABLE_MAX (or 0) drop the table.  sks_all_pairs_ani calls it with its
+ * max_size. */
+#define SKS_ANI_TABLE_MAX (1u << 20)
+int sks_ctx_ani_table(sks_ctx* ctx, uint32_t size, int kmer_num_ones);
 int sks_host_free(void* p);
 /* The set's sketches back to back (sizes[i] * elem_words words each, in order)
  * and its sizes, copied into caller device buffers (a send buffer). */

@@ -55,7 +55,18 @@ __global__ __launch_bounds__(kAB) void k_ani_tiles(const int32_t* __restrict__ p
   o[kTile * kTile + c * kTile + r] = i < n && j < n ? ani_of(x, sizes[j], inv_k, nullptr) : 0.0;
 }
 
+__global__ __launch_bounds__(kAB) void k_ani_root(double* __restrict__ out, uint32_t size, double inv_k) {
+  const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+  if (i <= size) out[i] = ani_of((int32_t)i, (int32_t)size, inv_k, nullptr);
+}
+
 }  // namespace
+
+hipError_t launch_ani_root(double* out, uint32_t size, int kmer_num_ones, hipStream_t s) {
+  const double inv_k = ((double)1.0) / ((double)kmer_num_ones);
+  hipLaunchKernelGGL(k_ani_root, dim3(size / kAB + 1), dim3(kAB), 0, s, out, size, inv_k);
+  return hipGetLastError();
+}
 
 hipError_t launch_ani_matrix(const int32_t* counts, uint32_t n, int kmer_num_ones, double* cont, double* ani,
                              hipStream_t s) {

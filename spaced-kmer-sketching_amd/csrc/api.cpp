@@ -213,6 +213,9 @@ struct sks_ctx {
   int intersect_algo = 0;  // sks::kIntersect*
   bool join_check = false;  // invariant-checking join / layout kernels (sks_ctx_set_join_check)
   uint32_t layout_blocks_hint = 0;  // sks_ctx_set_layout_blocks_hint (0: every block holds sketches)
+  sks::Scratch root;                // sks_ctx_ani_table: ANI by shared-element count for one set size
+  uint32_t root_size = 0;
+  int root_k = 0;                   // 0: no table
 };
 
 struct sks_kmer_list {
@@ -647,6 +650,22 @@ int sks_ctx_set_intersect_kernel(sks_ctx* c, int kind) {
 int sks_ctx_set_layout_blocks_hint(sks_ctx* c, uint32_t blocks) {
   if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_set_layout_blocks_hint: null ctx");
   c->layout_blocks_hint = blocks;
+  return SKS_OK;
+}
+
+int sks_ctx_ani_table(sks_ctx* c, uint32_t size, int kmer_num_ones) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_ctx_ani_table: null ctx");
+  if (kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_ctx_ani_table: kmer_num_ones must be positive");
+  if (size == 0 || size > SKS_ANI_TABLE_MAX) {
+    c->root_k = 0;
+    return SKS_OK;
+  }
+  if (c->root_k == kmer_num_ones && c->root_size == size) return SKS_OK;  // already built (stream order)
+  DeviceGuard g(c->device);
+  SKS_HIP(c->root.reserve(((size_t)size + 1) * sizeof(double)));
+  SKS_HIP(sks::launch_ani_root(static_cast<double*>(c->root.ptr), size, kmer_num_ones, c->stream));
+  c->root_size = size;
+  c->root_k = kmer_num_ones;
   return SKS_OK;
 }
 
@@ -1801,7 +1820,11 @@ int sks_intersect_layout_ani(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_wo
     SKS_HIP(c->tdone.reserve(nt * sizeof(uint32_t)));
     SKS_HIP(hipMemsetAsync(c->tdone.ptr, 0, nt * sizeof(uint32_t), c->stream));
     const sks::JoinLayout R{d_rvals, d_rmasks, d_rboff, d_rbstart}, C{d_cvals, d_cmasks, d_cboff, d_cbstart};
-    const sks::JoinAni A{d_ani, d_sizes, kmer_num_ones, static_cast<uint32_t*>(c->tdone.ptr)};
+    sks::JoinAni A{d_ani, d_sizes, kmer_num_ones, static_cast<uint32_t*>(c->tdone.ptr)};
+    if (c->root_k == kmer_num_ones) {  // the context's table (sks_ctx_ani_table), if for this k
+      A.root = static_cast<const double*>(c->root.ptr);
+      A.root_size = c->root_size;
+    }
     SKS_HIP(sks::join_launch(R, 0u - r_blk0, C, 0u - c_blk0, n, log_b, elem_words, true, 0, n, tile_begin,
                              tile_end, d_tiles, packed != 0, d_out, c->join_check, c->stream, &A));
   }
@@ -1864,8 +1887,15 @@ int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, elem_words, nullptr, w + o_tmp, vals, masks,
                                  boff, bst, stat, c->join_check, c->stream, &zs));
   const sks::JoinLayout L{vals, masks, boff, bst};
-  const sks::JoinAni A{d_ani, reinterpret_cast<const int32_t*>(d_sizes), kmer_num_ones,
-                       static_cast<uint32_t*>(c->tdone.ptr)};
+  sks::JoinAni A{d_ani, reinterpret_cast<const int32_t*>(d_sizes), kmer_num_ones,
+                 static_cast<uint32_t*>(c->tdone.ptr)};
+  if (ani) {  // bottom-s sets all hold max_size elements: their ANI comes from the table
+    SKS_TRY(sks_ctx_ani_table(c, max_size, kmer_num_ones));
+    if (c->root_k == kmer_num_ones) {
+      A.root = static_cast<const double*>(c->root.ptr);
+      A.root_size = c->root_size;
+    }
+  }
   // sks_ctx_last_intersect_ms: the join launch alone (the layout build before it
   // is the call's fixed part)
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));

@@ -93,6 +93,8 @@ struct JoinArgs {
   const int32_t* sizes;
   double inv_k;
   uint32_t* tile_done;  // [tile - tile_begin]
+  const double* root;   // root[x] = ani_of(x, root_size) (JoinAni::root), or null
+  uint32_t root_size;
 };
 
 template <int EW>
@@ -651,12 +653,17 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
   // with lanes over columns and (c, r) with lanes over rows, so every wave's
   // stores are one contiguous 512-byte row segment of the n x n matrix (ani may
   // be pinned host memory: PCIe writes).
+#if SKS_ANI_DIAG != 2  // (diagnostics 2: no drain; the counts the finisher reads may be short)
   __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+#endif
   __syncthreads();
   if (tid == 0)
     s_top = __hip_atomic_fetch_add(a.tile_done + (t - a.tile_begin), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT) + 1 == a.n_groups;
   __syncthreads();
+#if SKS_ANI_DIAG == 1  // (diagnostics 1: the hand-off only, no conversion)
+  if (s_top) return;
+#endif
   if (!s_top) {
     JSTAMP(6);
     JSTAMP_FLUSH();
@@ -673,16 +680,21 @@ __global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
     s_cnt[q] = x;
   }
   __syncthreads();
+  // a row whose set size has the root table (bottom-s sets: every row) reads
+  // its value there; fp64 pow (~230 instructions) for 8192 cells per tile was
+  // ~70 us of the call
+  auto conv = [&](int32_t x, int32_t size) {
+    return (a.root && (uint32_t)size == a.root_size && (uint32_t)x <= a.root_size) ? a.root[x]
+                                                                                    : ani_of(x, size, a.inv_k, nullptr);
+  };
   for (uint32_t r = tid >> 6; r < kTile; r += kJB / 64) {
     const uint32_t gr = row0 + r, gc = col0 + lane;
-    if (gr < row_lim && gc < a.n)
-      a.ani[(uint64_t)gr * a.n + gc] = ani_of(s_cnt[r * kTile + lane], a.sizes[gr], a.inv_k, nullptr);
+    if (gr < row_lim && gc < a.n) a.ani[(uint64_t)gr * a.n + gc] = conv(s_cnt[r * kTile + lane], a.sizes[gr]);
   }
   if (I != J) {
     for (uint32_t c = tid >> 6; c < kTile; c += kJB / 64) {
       const uint32_t gr = row0 + lane, gc = col0 + c;
-      if (gr < row_lim && gc < a.n)
-        a.ani[(uint64_t)gc * a.n + gr] = ani_of(s_cnt[lane * kTile + c], a.sizes[gc], a.inv_k, nullptr);
+      if (gr < row_lim && gc < a.n) a.ani[(uint64_t)gc * a.n + gr] = conv(s_cnt[lane * kTile + c], a.sizes[gc]);
     }
   }
   JSTAMP(6);
@@ -782,6 +794,8 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
     ja.ani = ani->ani;
     ja.sizes = ani->sizes;
     ja.inv_k = ((double)1.0) / ((double)ani->kmer_num_ones);
+    ja.root = ani->root;
+    ja.root_size = ani->root_size;
   }
   uint32_t* tile_done = ani ? ani->tile_done : nullptr;
   // bucket groups per tile: ~128 buckets per workgroup (a workgroup's start-up —

@@ -19,6 +19,10 @@ __device__ __forceinline__ double ani_of(int32_t inter, int32_t size_first, doub
   return c <= 0.0 ? 0.0 : pow(c, inv_k);
 }
 
+// out[i] = ani_of(i, size) for i in [0, size]: the fused ANI of a row whose set
+// holds `size` elements reads its value here instead of evaluating pow (the
+// same function, so the same doubles)
+hipError_t launch_ani_root(double* out, uint32_t size, int kmer_num_ones, hipStream_t s);
 hipError_t launch_ani_rows(const int32_t* counts, uint32_t n, uint32_t row_begin, uint32_t row_end,
                            int kmer_num_ones, double* cont, double* ani, hipStream_t s);
 }  // namespace sks

@@ -234,6 +234,8 @@ struct JoinAni {
   const int32_t* sizes;   // [n] |S_i| by global genome index
   int kmer_num_ones;      // k of binomial_estimator
   uint32_t* tile_done;    // [tile_end - tile_begin] workgroups finished per tile, zeroed
+  const double* root = nullptr;  // optional: root[i] = ANI of i shared elements for a set of root_size
+  uint32_t root_size = 0;
 };
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
                        uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,

@@ -500,6 +500,8 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     if fused and ani_out is None:
         ani_out = torch.zeros((n_genomes, n_genomes), dtype=torch.float64, device=device)
     res.ani = ani_out if fused else None
+    if fused and gmax and hasattr(ops, "ani_table"):
+        ops.ani_table(gmax, ani_ones)  # rows of gmax elements (bottom-s: all) read their ANI from a table
     stats_mark = ops.stats_mark() if hasattr(ops, "stats_mark") else None
     native = hasattr(ops, "all_pairs") and not getattr(ops, "no_native", False)
     if (solo or (world == 1 and not world1_exchange)) and native and (fused or dst is None):
@@ -760,6 +762,10 @@ class GpuJoinOps:
                                                  [t.data_ptr() for t in cols], c_blk0, tl.data_ptr(), 0,
                                                  tl.shape[0], out.dim() == 3, out.data_ptr(), elem_words=self.ew)
         _torch_waits_for_ctx(self.ctx)
+
+    def ani_table(self, size, k):
+        """sks_ctx_ani_table: the fused ANI of rows of `size` elements from a table (queued, cached)."""
+        self.ctx.ani_table(size, k)
 
     def count_ani(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, out, sizes, k, ani):
         """count + the ANI of every counted pair into ani (n * n float64: a device

@@ -49,7 +49,7 @@ EXPORTED = [
     "sks_fasta_stream", "sks_fasta_stream_bytes", "sks_fasta_runs", "sks_ctx_create",
     "sks_ctx_destroy", "sks_ctx_set_stream", "sks_ctx_synchronize", "sks_ctx_last_timings",
     "sks_sketch_build", "sks_sketch_set_free", "sks_sketch_set_free_on_stream", "sks_sketch_set_num", "sks_sketch_set_elem_words",
-    "sks_ctx_set_layout_blocks_hint",
+    "sks_ctx_set_layout_blocks_hint", "sks_ctx_ani_table",
     "sks_sketch_set_sizes", "sks_sketch_set_windows", "sks_sketch_set_device_data",
     "sks_sketch_set_device_starts", "sks_sketch_set_device_sizes", "sks_sketch_set_starts",
     "sks_sketch_set_copy", "sks_sketch_set_export", "sks_intersect_pairs", "sks_intersect_all",
@@ -152,6 +152,7 @@ def lib():
     L.sks_ani_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, vp, vp]
     L.sks_ani_tiles.argtypes = [vp, vp, vp, C.c_uint64, C.c_uint32, vp, C.c_int, vp]
     L.sks_ctx_set_join_check.argtypes = [vp, C.c_int]
+    L.sks_ctx_ani_table.argtypes = [vp, C.c_uint32, C.c_int]
     L.sks_ctx_join_check_violations.argtypes = [vp, u64p]
     L.sks_ctx_last_intersect_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.sks_ctx_last_ingress_ms.argtypes = [vp, C.POINTER(C.c_float)]
@@ -393,6 +394,10 @@ class Context:
     def set_layout_blocks_hint(self, blocks):
         """sks_ctx_set_layout_blocks_hint: blocks that hold sketches in the next layout builds (0: all)."""
         check(lib().sks_ctx_set_layout_blocks_hint(self.h, C.c_uint32(int(blocks))))
+
+    def ani_table(self, size, kmer_num_ones):
+        """sks_ctx_ani_table: ANI by shared-element count for sets of `size` elements (fused ANI reads it)."""
+        check(lib().sks_ctx_ani_table(self.h, C.c_uint32(int(size)), int(kmer_num_ones)))
 
     def all_pairs_ani(self, data, starts, sizes, n, max_size, total, kmer_num_ones, ani, counts, status,
                       elem_words=1):

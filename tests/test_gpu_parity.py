@@ -1059,3 +1059,38 @@ def test_all_vs_all_join_fused_ani_to_host(torch_cuda, ctx):
     torch.cuda.synchronize()
     assert np.abs(rows.cpu().numpy()[64:200].reshape(-1) - want.reshape(n, n)[64:200].reshape(-1)).max() <= 1e-12
     hb.free()
+
+
+def test_fused_ani_table_rows_equal_pow_rows(torch_cuda, ctx):
+    """sks_ctx_ani_table: the fused ANI of a row whose set holds max_size
+    elements (bottom-s: the full sketches) is read from the context's table,
+    the other rows (short genomes' smaller sketches) evaluate pow — both equal,
+    bit for bit, the dense sks_ani_rows kernel (ani_of with pow,
+    ani_estimation.cpp:24-42) on the same counts, and the table is rebuilt
+    when k changes."""
+    import sks_dist
+    torch = torch_cuda
+    n, s = 200, 400
+    genomes = [synth.bases(300 if i % 7 == 0 else 3000 + 11 * (i % 5), seed=70 + i % 9, mut_seed=90 + i,
+                           mut_rate=0.003 * (i % 4)).tobytes() for i in range(n)]
+    w = 31
+    ops = sks_dist.GpuJoinOps(ctx)
+    for k in (21, 17):
+        m = O.mask(w, k, 0)
+        ss, _ = build(torch, ctx, genomes, w, m, "bottom", s)
+        sizes = ss.sizes()
+        assert int(sizes.max()) == s and int(sizes.min()) < s  # both paths taken
+        res = sks_dist.all_vs_all_join(n, 1, 0, sks_dist.sketches_of(ss), ops, sksffi.join_layout_log_b,
+                                       device="cuda", dst=0, ani_ones=k)
+        torch.cuda.synchronize()
+        res.check_layouts()
+        got = res.matrix.cpu().numpy()
+        assert np.array_equal(np.diag(got), sizes.astype(got.dtype))
+        dense = torch.from_numpy(got.astype(np.int32)).cuda()
+        rows = torch.zeros((n, n), dtype=torch.float64, device="cuda")
+        ctx.ani_rows(dense.data_ptr(), n, 0, n, k, rows.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(res.ani.cpu().numpy(), rows.cpu().numpy()), k
+        size_first = np.repeat(np.diag(got).astype(np.int32), n)
+        _, want = sksffi.ani_from_counts(got.reshape(-1), size_first, k)
+        assert np.abs(res.ani.cpu().numpy().reshape(-1) - want).max() <= 1e-12

@@ -2,7 +2,7 @@
 ANI goes: timed per step (sync to sync) for the counts only (dense), the join
 with fused ANI into device memory (+ an 8 MB copy to pinned host memory), into
 coarse- and fine-grained sks_host_alloc memory and into a torch pinned tensor.
-    python tools/bench_ani_dest.py [reps]"""
+    python tools/bench_ani_dest.py [reps] [w k]   (w > 32: 128-bit k-mers)"""
 import os
 import statistics
 import sys
@@ -21,6 +21,7 @@ import bench  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    w, k = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (31, 21)
     n, L = bench.C4_GENOMES, bench.C4_LEN
     ctx = sksffi.Context(0)
     seg = [0]
@@ -31,12 +32,13 @@ def main():
         a, m, r = bench.c4_genome_seeds(g)
         ctx.synth_bases(buf.data_ptr() + seg[g], L, a, m, r)
         buf[seg[g] + L] = ord("\n")
-    mask = sksffi.mask_generate(31, 21, 0)
+    mask = sksffi.mask_generate(w, k, 0)
     ones = bin(mask).count("1") // 2
-    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, 31, mask, sksffi.SKS_BOTTOM_S, bench.C4_S)
-    src = sks_dist.sketches_of(ss)
-    ops = sks_dist.GpuJoinOps(ctx)
+    ss = ctx.sketch_build(buf.data_ptr(), seg[-1], seg, w, mask, sksffi.SKS_BOTTOM_S, bench.C4_S)
+    ops = sks_dist.GpuJoinOps(ctx, ew=2 if w > 32 else 1)
+    src = sks_dist.sketches_of(ss, ew=ops.ew)
     mx = int(ss.sizes().max())
+    print("sizes min", int(ss.sizes().min()), "max", mx, "w", w, "k", k, flush=True)
     dev = torch.zeros((n, n), dtype=torch.float64, device="cuda")
     pinned = torch.zeros(n * n, dtype=torch.float64, pin_memory=True)
     nc = sksffi.HostBuffer(n * n * 8, coherent=False)
