@@ -55,7 +55,10 @@ constexpr uint64_t kMaxGrid = 1ull << 22;
 constexpr int kJB = 512;
 constexpr int kJCap = 1024;             // column entries per chunk (10-bit entry index)
 constexpr int kJMade = kJCap / kJB;     // column entries per thread per chunk
-constexpr int kJRowPf = 1536 / kJB;     // row entries per thread held in registers per chunk
+#ifndef SKS_JOIN_ROWPF
+#define SKS_JOIN_ROWPF 1
+#endif
+constexpr int kJRowPf = SKS_JOIN_ROWPF;   // row entries per thread held in registers per chunk
 // buckets per window: a workgroup stages the bucket offsets of 64 buckets at a
 // time; a window may hold several layout regions (each region's entries are
 // contiguous, with a gap before the next region: chunks map their entries
@@ -65,7 +68,10 @@ constexpr uint32_t kJPieces = 4;
 // 16 planes hold counts below 2^16 per workgroup; a carry out of the top plane
 // (a pair sharing >= 65536 values in one workgroup's buckets) is added to the
 // output directly
-constexpr int kPlanes = 16;
+#ifndef SKS_JOIN_PLANES
+#define SKS_JOIN_PLANES 12
+#endif
+constexpr int kPlanes = SKS_JOIN_PLANES;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 // hit items with more rows than this are spread over the wave's lanes (rows_add)
 constexpr uint32_t kLight = 2;
@@ -232,7 +238,10 @@ __device__ unsigned long long g_join_stamps_wg[kMaxJoinStampWgs * 8];
 // u64 values — a build of 82 dropped the kernel to two workgroups per CU and
 // ran 20% slower; 128-bit values need more registers and take two
 template <int EW, bool CHECK, bool PIECES>
-__global__ __launch_bounds__(kJB, EW == 1 ? 3 : 2) void k_join(JoinArgs a) {
+#ifndef SKS_JOIN_WPE1
+#define SKS_JOIN_WPE1 8
+#endif
+__global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : 2) void k_join(JoinArgs a) {
   __shared__ uint32_t s_slot[kFSlots];
   __shared__ uint64_t s_ev[kJCap * EW];          // staged column entries: values
   __shared__ unsigned long long s_em[kJCap];     // ... and column masks

@@ -308,3 +308,39 @@ def test_layout_blocks_hint_sparse_rows(torch_cuda, ctx):
             for c in range(0, 64, 5):
                 want = np.intersect1d(sk[I * 64 + r], sk[J * 64 + c], assume_unique=True).size
                 assert got[1][t, r, c] == want, (I, J, r, c)
+
+
+def test_join_plane_carry_out(torch_cuda, ctx):
+    """Pairs sharing more values in one join workgroup's buckets than the
+    bit-sliced counters hold (2^12 per workgroup: join.hip kPlanes) carry out
+    of the top plane into the output: four sketches of up to 5 M values (two
+    identical, a half, a partial overlap) counted by sks_all_pairs_ani (one
+    k_join launch, ~4.9k shared values per workgroup on the identical pair)
+    and sks_intersect_sym equal numpy's intersections (kmer_set.cpp:143-184)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    a = np.unique(rng.integers(1, 2**63, size=5_100_000, dtype=np.uint64))[:5_000_000]
+    other = np.unique(rng.integers(1, 2**63, size=2_000_000, dtype=np.uint64))
+    d_part = np.unique(np.concatenate([a[1::3], other]))
+    sk = [a, a.copy(), a[::2].copy(), d_part]
+    n = len(sk)
+    want = np.array([[np.intersect1d(sk[i], sk[j], assume_unique=True).size for j in range(n)] for i in range(n)])
+    sizes = np.array([len(x) for x in sk], dtype=np.uint32)
+    starts = np.zeros(n, dtype=np.uint64)
+    starts[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    flat = np.concatenate(sk + [np.zeros(1, np.uint64)])
+    d = torch.from_numpy(flat.view(np.int64)).to("cuda:0")
+    st = torch.from_numpy(starts.view(np.int64)).to("cuda:0")
+    sz = torch.from_numpy(sizes.view(np.int32)).to("cuda:0")
+    cnt = torch.full((64 * 64,), -7, dtype=torch.int32, device="cuda:0")
+    stat = torch.zeros(2, dtype=torch.int32, device="cuda:0")
+    ctx.all_pairs_ani(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, int(sizes.max()), int(sizes.sum()), 21, 0,
+                      cnt.data_ptr(), stat.data_ptr())
+    torch.cuda.synchronize()
+    assert int(stat.cpu()[1]) == 0
+    got = cnt.cpu().numpy().reshape(64, 64)[:n, :n]
+    assert want[0, 1] == 5_000_000 and np.array_equal(got, want)
+    o = torch.full((n * n,), 9, dtype=torch.int32, device="cuda:0")
+    ctx.intersect_sym(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, sksffi.intersect_sym_tiles(n), o.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(o.cpu().numpy().reshape(n, n), want)
