@@ -19,6 +19,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <cstdint>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include <rocprim/rocprim.hpp>
@@ -398,6 +400,22 @@ hipError_t launch_intersect_all_global(const uint64_t* data, const uint64_t* sta
 
 namespace sks {
 
+// bucket counts learned per largest-sketch size: a join whose layout had
+// buckets above the table's capacity makes later calls on that size start with
+// more buckets (the call itself keeps its exact sub-chunked counts)
+static std::mutex g_log_b_mu;
+static std::unordered_map<uint32_t, uint32_t> g_log_b_min;
+static uint32_t start_log_b(uint32_t max_size) {
+  std::lock_guard<std::mutex> lk(g_log_b_mu);
+  const auto it = g_log_b_min.find(max_size);
+  return std::max(join_log_b(max_size), it == g_log_b_min.end() ? 0u : it->second);
+}
+static void bump_log_b(uint32_t max_size, uint32_t log_b) {
+  std::lock_guard<std::mutex> lk(g_log_b_mu);
+  uint32_t& x = g_log_b_min[max_size];
+  x = std::max(x, log_b);
+}
+
 // Tiled all-pairs (ew = 1: u64 k-mers, join or merge tiles; ew = 2: 128-bit
 // k-mers, join only).  Host-synchronous (reads the sizes and the layout's
 // statistics back to pick the bucket count).  mode: sym (upper-triangle tiles
@@ -482,7 +500,7 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
     uint64_t r_total = 0;
     if (sep_rows)
       for (uint32_t i = row_begin; i < row_end; ++i) r_total += h_sizes[i];
-    uint32_t log_b = join_log_b(max_size);
+    uint32_t log_b = start_log_b(max_size);
     for (;;) {
       const uint32_t BW = jc::lay_boff_words(log_b), G = jc::lay_groups(log_b);
       const size_t tmp_c = join_layout_temp_bytes(n, log_b, ew);
@@ -521,27 +539,30 @@ hipError_t launch_intersect_tiled(const uint64_t* data, const uint64_t* starts, 
       };
       if ((e = build_layout(0, n, cl)) != hipSuccess) return e;
       if (sep_rows && (e = build_layout(row_begin, rn, rl)) != hipSuccess) return e;
+      // the join runs right behind the build (no host round trip between them);
+      // the build's status words are read back after it: an invalid layout (a
+      // group the build could not place: adversarial 128-bit values) discards
+      // the counts and retries with more buckets.  Buckets above the table's
+      // capacity are joined in sub-chunks (exact; their row entries are probed
+      // once per sub-chunk) and only make the next call on these sizes start
+      // with more buckets.
+      const uint32_t r_blk0 = sep_rows ? 0 : (sym ? 0 : row_begin / kTile);
+      if ((e = join_launch(rl, r_blk0, cl, 0, n, log_b, ew, sym, row_begin, row_end, tile_begin, tile_end,
+                           nullptr, false, out, check, s)) != hipSuccess)
+        return e;
       uint32_t h_stat[2] = {0, 0};
       if ((e = pinned_d2h(h_stat, stat, 8, s)) != hipSuccess) return e;
       if (dbg)
         fprintf(stderr, "[sks intersect] join n=%u ew=%d B=%u max block bucket %u invalid %u tiles=%llu\n", n, ew,
                 1u << log_b, h_stat[0], h_stat[1], (unsigned long long)tiles);
-      if (h_stat[1]) {  // a layout group the build could not place (adversarial 128-bit values)
+      if (h_stat[1]) {
+        if ((e = hipMemsetAsync(out, 0, out_words * sizeof(int32_t), s)) != hipSuccess) return e;
         if (log_b < jc::kMaxLogB) { ++log_b; continue; }
         break;
       }
-      // buckets above the table's capacity are joined in sub-chunks (exact, but
-      // the bucket's row entries are probed once per sub-chunk), so more
-      // buckets are tried first while the count matrix allows
-      if (h_stat[0] <= join_cap() || log_b >= jc::kMaxLogB) {
-        const uint32_t r_blk0 = sep_rows ? 0 : (sym ? 0 : row_begin / kTile);
-        if ((e = join_launch(rl, r_blk0, cl, 0, n, log_b, ew, sym, row_begin, row_end, tile_begin, tile_end,
-                             nullptr, false, out, check, s)) != hipSuccess)
-          return e;
-        *used_tiles = true;
-        return hipSuccess;
-      }
-      ++log_b;
+      if (h_stat[0] > join_cap() && log_b < jc::kMaxLogB) bump_log_b(max_size, log_b + 1);
+      *used_tiles = true;
+      return hipSuccess;
     }
   }
   if (ew != 1) return hipSuccess;  // the merge tiles take u64 k-mers: one wavefront per pair

@@ -199,7 +199,7 @@ def place_tiles(mat, tiles, parts, n):
     if key not in _PLACE_CACHE:
         if len(_PLACE_CACHE) > 4:
             _PLACE_CACHE.clear()
-        t = torch.as_tensor(tiles, device=dev)
+        t = torch.as_tensor(tiles.copy(), device=dev)  # (a cached tile list is read-only)
         ar = torch.arange(TILE, device=dev, dtype=torch.int64)
         gr = (t[:, 0:1] * TILE + ar.view(1, -1)).view(-1, TILE, 1).expand(-1, TILE, TILE)
         gc = (t[:, 1:2] * TILE + ar.view(1, -1)).view(-1, 1, TILE).expand(-1, TILE, TILE)

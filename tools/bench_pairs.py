@@ -1,6 +1,8 @@
 """A/B of the all-pairs intersection kernels on config 4 (1000 x 5 Mb, bottom-s
 10000) or config 5's 200 genomes: sketches once, then times sks_intersect_sym
-over all tiles per kernel (median of reps) and checks the matrices agree.
+over all tiles per kernel (median of reps) and checks the matrices agree;
+"onecall" (SKS_BENCH_KERNELS=join,onecall) times sks_all_pairs_ani's counts
+(layout + every tile in one native call, no host round trip) sync to sync.
     python tools/bench_pairs.py [n_genomes] [reps] [family|indep|same] [w]"""
 import os
 import statistics
@@ -42,16 +44,31 @@ def main():
     ref = None
     kernels = (("merge", sksffi.INTERSECT_MERGE), ("join", sksffi.INTERSECT_JOIN)) if ew == 1 else \
         (("join", sksffi.INTERSECT_JOIN),)
-    only = os.environ.get("SKS_BENCH_KERNELS")
-    if only:
-        kernels = tuple(x for x in kernels if x[0] in only.split(","))
+    kernels = kernels + (("onecall", None),)
+    only = os.environ.get("SKS_BENCH_KERNELS", "merge,join")
+    kernels = tuple(x for x in kernels if x[0] in only.split(","))
     for name, k in kernels:
-        ctx.set_intersect_kernel(k)
         out = torch.empty((n, n), dtype=torch.int32, device="cuda")
         ms = []
-        for _ in range(reps + 1):
-            ctx.intersect_sym(data, starts, sizes, ew, n, 0, T, out.data_ptr())
-            ms.append(ctx.last_intersect_ms())
+        if name == "onecall":
+            import time
+            import sks_dist
+            hs = ss.sizes()
+            cnt = torch.empty(T * 4096, dtype=torch.int32, device="cuda")
+            for _ in range(reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                ctx.all_pairs_ani(data, starts, sizes, n, int(hs.max()), int(hs.sum()), 0, 0, cnt.data_ptr(), 0,
+                                  elem_words=ew)
+                torch.cuda.synchronize()
+                ms.append((time.perf_counter() - t0) * 1e3)
+            out.zero_()
+            sks_dist.place_tiles(out, sks_dist._all_tiles((n + 63) // 64), cnt.view(T, 64, 64), n)
+        else:
+            ctx.set_intersect_kernel(k)
+            for _ in range(reps + 1):
+                ctx.intersect_sym(data, starts, sizes, ew, n, 0, T, out.data_ptr())
+                ms.append(ctx.last_intersect_ms())
         got = out.cpu()
         if ref is None:
             ref = got
