@@ -54,7 +54,16 @@ constexpr uint64_t kMaxGrid = 1ull << 22;
 // 24 waves per CU hide the LDS round trips of the insert and probe chains
 constexpr int kJB = 512;
 constexpr int kJCap = 1024;             // column entries per chunk (10-bit entry index)
-constexpr int kJMade = kJCap / kJB;     // column entries per thread per chunk
+#ifndef SKS_JOIN_CAP2
+#define SKS_JOIN_CAP2 1024
+#endif
+// column entries per chunk by value width (128-bit values: a smaller chunk
+// can buy LDS for another workgroup per CU), and per thread
+template <int EW>
+constexpr int jcap() { return EW == 1 ? kJCap : SKS_JOIN_CAP2; }
+template <int EW>
+constexpr int jmade() { return jcap<EW>() / kJB; }
+static_assert(SKS_JOIN_CAP2 % kJB == 0 && SKS_JOIN_CAP2 <= kJCap, "128-bit chunk capacity");
 #ifndef SKS_JOIN_ROWPF
 #define SKS_JOIN_ROWPF 1
 #endif
@@ -63,7 +72,11 @@ constexpr int kJRowPf = SKS_JOIN_ROWPF;   // row entries per thread held in regi
 // time; a window may hold several layout regions (each region's entries are
 // contiguous, with a gap before the next region: chunks map their entries
 // piecewise, at most kJPieces regions per chunk)
-constexpr int kJWinLog = 6, kJWin = 1 << kJWinLog;
+#ifndef SKS_JOIN_WINLOG
+#define SKS_JOIN_WINLOG 6
+#endif
+constexpr int kJWinLog = SKS_JOIN_WINLOG, kJWin = 1 << kJWinLog;
+static_assert(kJWinLog <= 6, "a window's buckets are scanned by one wave");
 constexpr uint32_t kJPieces = 4;
 // 16 planes hold counts below 2^16 per workgroup; a carry out of the top plane
 // (a pair sharing >= 65536 values in one workgroup's buckets) is added to the
@@ -74,7 +87,10 @@ constexpr uint32_t kJPieces = 4;
 constexpr int kPlanes = SKS_JOIN_PLANES;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 // hit items with more rows than this are spread over the wave's lanes (rows_add)
-constexpr uint32_t kLight = 2;
+#ifndef SKS_JOIN_LIGHT
+#define SKS_JOIN_LIGHT 2
+#endif
+constexpr uint32_t kLight = SKS_JOIN_LIGHT;
 static_assert(kJCap == 1024, "entry index: 10 bits of the slot word");
 static_assert(kFSlots >= kTile * kTile, "the fused ANI stages a tile's counts in the slot table");
 
@@ -105,8 +121,8 @@ struct JoinArgs {
 
 template <int EW>
 struct JoinChunk {
-  KV cv[kJMade];
-  unsigned long long cm[kJMade];  // 0: no entry
+  KV cv[jmade<EW>()];
+  unsigned long long cm[jmade<EW>()];  // 0: no entry
   KV rv[kJRowPf];
   unsigned long long rm[kJRowPf];
 };
@@ -135,14 +151,14 @@ __device__ __forceinline__ void join_fetch(const uint64_t* __restrict__ cvals,
     const unsigned long long* cm = cmasks + cp.d0;
     const uint64_t* cv = cvals + (uint64_t)cp.d0 * EW;
 #pragma unroll
-    for (int u = 0; u < kJMade; ++u) {
+    for (int u = 0; u < jmade<EW>(); ++u) {
       const uint32_t k = cs + tid + kJB * u;
       c.cv[u] = k < ce ? kv_load<EW>(cv, k) : KV{0, 0};
       c.cm[u] = k < ce ? cm[k] : 0ull;
     }
   } else {
 #pragma unroll
-    for (int u = 0; u < kJMade; ++u) {
+    for (int u = 0; u < jmade<EW>(); ++u) {
       const uint32_t k = cs + tid + kJB * u, q = phys(cp, k);
       c.cv[u] = k < ce ? kv_load<EW>(cvals, q) : KV{0, 0};
       c.cm[u] = k < ce ? cmasks[q] : 0ull;
@@ -241,10 +257,13 @@ template <int EW, bool CHECK, bool PIECES>
 #ifndef SKS_JOIN_WPE1
 #define SKS_JOIN_WPE1 8
 #endif
-__global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : 2) void k_join(JoinArgs a) {
+#ifndef SKS_JOIN_WPE2
+#define SKS_JOIN_WPE2 2
+#endif
+__global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : SKS_JOIN_WPE2) void k_join(JoinArgs a) {
   __shared__ uint32_t s_slot[kFSlots];
-  __shared__ uint64_t s_ev[kJCap * EW];          // staged column entries: values
-  __shared__ unsigned long long s_em[kJCap];     // ... and column masks
+  __shared__ uint64_t s_ev[jcap<EW>() * EW];          // staged column entries: values
+  __shared__ unsigned long long s_em[jcap<EW>()];     // ... and column masks
   __shared__ unsigned long long s_pl[kPlanes * kTile];  // plane b of row r at [b * 64 + r]
   __shared__ uint32_t s_roff[kJWin + 1], s_coff[kJWin + 1];  // block positions of the window's buckets
   __shared__ uint32_t s_rv[kJWin + 1], s_cv[kJWin + 1];      // ... and their virtual starts
@@ -413,9 +432,9 @@ __global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : 2) void k_join(JoinA
     JSTAMP(7);
   } else {
     // ---- off-diagonal tile: chunks of the column block's entries -----------------------------
-    uint32_t made[kJMade];  // slots this thread created in the current chunk
+    uint32_t made[jmade<EW>()];  // slots this thread created in the current chunk
 #pragma unroll
-    for (int u = 0; u < kJMade; ++u) made[u] = kNoSlot;
+    for (int u = 0; u < jmade<EW>(); ++u) made[u] = kNoSlot;
     for (uint32_t wb = b0; wb < b1;) {
       uint32_t we = min(b1, ((wb >> kJWinLog) + 1) << kJWinLog);
       if constexpr (!PIECES) we = min(we, min(((wb >> c_rb) + 1) << c_rb, ((wb >> r_rb) + 1) << r_rb));
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : 2) void k_join(JoinA
         // 0) free the previous chunk's slots (its probes are done: barrier below
         //    the probe loop) and stage this chunk's entries
 #pragma unroll
-        for (int u = 0; u < kJMade; ++u) {
+        for (int u = 0; u < jmade<EW>(); ++u) {
           if (made[u] != kNoSlot) s_slot[made[u]] = kFFree;
           made[u] = kNoSlot;
           const uint32_t e = tid + kJB * u;
@@ -536,7 +555,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : 2) void k_join(JoinA
         // 1) insert: the chunk's values are distinct, so a compare-swap walk to
         //    the first free slot
 #pragma unroll
-        for (int u = 0; u < kJMade; ++u) {
+        for (int u = 0; u < jmade<EW>(); ++u) {
           if (!cur.cm[u]) continue;
           const uint32_t e = tid + kJB * u;
           const uint32_t word = (fp_tag<EW>(cur.cv[u]) << 10) | e;
@@ -552,7 +571,7 @@ __global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : 2) void k_join(JoinA
         JSTAMP(3);
         if (CHECK) {  // every inserted value is found, naming its own entry
 #pragma unroll
-          for (int u = 0; u < kJMade; ++u) {
+          for (int u = 0; u < jmade<EW>(); ++u) {
             if (!cur.cm[u]) continue;
             const uint32_t h = fp_slot<EW>(cur.cv[u]);
             const uint32_t x = chain(cur.cv[u], h, s_slot[h]);
@@ -798,7 +817,7 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   ja.row_end = row_end;
   ja.out = out;
   ja.ld = n;
-  ja.cap = join_cap();
+  ja.cap = std::min<uint32_t>(join_cap(), ew == 2 ? (uint32_t)jcap<2>() : (uint32_t)jcap<1>());
   if (ani) {
     ja.ani = ani->ani;
     ja.sizes = ani->sizes;
