@@ -239,7 +239,20 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
   uint32_t stride = kPosStride;
   while ((uint64_t)stride * kPosSamples < sz) stride <<= 1;
   const uint32_t ns = (sz + stride - 1) / stride;  // sample k = S[k * stride]
-  for (uint32_t k = threadIdx.x; k < ns; k += kPT) kv_store<EW>(s_smp, k, kv_load<EW>(data, st + (uint64_t)k * stride));
+  if (ns) {  // every load of the thread's samples issued before the first LDS store
+    constexpr int kPer = (kPosSamples + kPT - 1) / kPT;
+    KV smp[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const uint32_t k = threadIdx.x + (uint32_t)u * kPT;
+      smp[u] = kv_load<EW>(data, st + (uint64_t)min(k, ns ? ns - 1 : 0u) * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const uint32_t k = threadIdx.x + (uint32_t)u * kPT;
+      if (k < ns) kv_store<EW>(s_smp, k, smp[u]);
+    }
+  }
   __syncthreads();
   uint32_t* out = pos + (uint64_t)i * (G + 1);
   for (uint32_t g = threadIdx.x; g <= G; g += kPT) {
@@ -255,6 +268,21 @@ __global__ __launch_bounds__(kPT) void k_gl_pos(const uint64_t* __restrict__ dat
       if (kv_lt<EW>(kv_load<EW>(s_smp, mid), x)) lo = mid + 1; else hi = mid;
     }
     uint32_t a = lo ? (lo - 1) * stride + 1 : 0, e = min(sz, lo * stride);
+    if (stride == kPosStride || a >= e) {
+      // at most stride - 1 candidates: all loaded together (clamped, no branch
+      // per load), the lower bound is a + the number below x
+      uint32_t c = 0;
+      if (a < e) {  // (an empty range, e.g. an empty sketch, loads nothing)
+#pragma unroll
+        for (uint32_t q = 0; q + 1 < kPosStride; ++q) {
+          const uint32_t m = a + q;
+          const KV y = kv_load<EW>(data, st + min(m, e - 1));
+          c += (m < e && kv_lt<EW>(y, x)) ? 1u : 0u;
+        }
+      }
+      out[g] = a + c;
+      continue;
+    }
     while (a < e) {
       const uint32_t mid = (a + e) >> 1;
       if (kv_lt<EW>(kv_load<EW>(data, st + mid), x)) a = mid + 1; else e = mid;
