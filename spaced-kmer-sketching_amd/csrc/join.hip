@@ -50,8 +50,8 @@ constexpr int kTile = 64;
 // workgroups per launch at most (HIP caps a grid at 2^32 - 1 work-items);
 // larger grids are cut into slices
 constexpr uint64_t kMaxGrid = 1ull << 22;
-// 512 threads (8 waves): with the table's LDS allowing 3 workgroups per CU,
-// 24 waves per CU hide the LDS round trips of the insert and probe chains
+// 512 threads (8 waves): four workgroups per CU for u64 values (32 waves),
+// three for 128-bit values, hide the LDS round trips of the insert and probe chains
 constexpr int kJB = 512;
 constexpr int kJCap = 1024;             // column entries per chunk (10-bit entry index)
 #ifndef SKS_JOIN_CAP2
@@ -78,9 +78,9 @@ constexpr int kJRowPf = SKS_JOIN_ROWPF;   // row entries per thread held in regi
 constexpr int kJWinLog = SKS_JOIN_WINLOG, kJWin = 1 << kJWinLog;
 static_assert(kJWinLog <= 6, "a window's buckets are scanned by one wave");
 constexpr uint32_t kJPieces = 4;
-// 16 planes hold counts below 2^16 per workgroup; a carry out of the top plane
-// (a pair sharing >= 65536 values in one workgroup's buckets) is added to the
-// output directly
+// 12 planes hold counts below 2^12 per workgroup; a carry out of the top plane
+// (a pair sharing >= 4096 values in one workgroup's buckets) is added to the
+// output directly (16 planes cost the LDS of the fourth workgroup per CU)
 #ifndef SKS_JOIN_PLANES
 #define SKS_JOIN_PLANES 12
 #endif
@@ -250,9 +250,10 @@ __device__ unsigned long long g_join_stamps_wg[kMaxJoinStampWgs * 8];
 // chunk is always contiguous (the kernel for layouts of 64-bucket regions,
 // where the piece code, never taken, still cost 8% of the join); true: windows
 // of 64 buckets across small regions, chunks mapped piecewise
-// three workgroups per CU (24 waves; LDS allows three): at most 80 VGPRs for
-// u64 values — a build of 82 dropped the kernel to two workgroups per CU and
-// ran 20% slower; 128-bit values need more registers and take two
+// u64 values: four workgroups per CU — 39.4 KB of LDS (12 planes) and 64
+// VGPRs (one prefetched row entry per thread; 8 registers spill outside the
+// chunk loop), 8% faster than three with 80; 128-bit values: three (76 VGPRs,
+// 47.4 KB; four per CU with 512-entry chunks measured equal)
 template <int EW, bool CHECK, bool PIECES>
 #ifndef SKS_JOIN_WPE1
 #define SKS_JOIN_WPE1 8
