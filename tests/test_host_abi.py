@@ -115,3 +115,11 @@ def test_context_without_gpu_fails_loudly():
     with pytest.raises(sksffi.SksError) as e:
         sksffi.Context(0)
     assert e.value.code == 2 and "no HIP device" in str(e.value)
+
+
+def test_ani_table_argument_errors():
+    """sks_ctx_ani_table rejects a null context before touching a device (no GPU
+    needed); the k check follows it (include/sks.h)."""
+    lib = sksffi.lib()
+    assert lib.sks_ctx_ani_table(None, C.c_uint32(100), 21) == 1
+    assert b"null ctx" in lib.sks_last_error()
