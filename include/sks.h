@@ -22,12 +22,16 @@
 extern "C" {
 #endif
 
-#define SKS_ABI_VERSION 2  /* 2: deduplicated join layout (masks, region ends), elem_words on
-                              the layout entry points, sks_ctx_set_join_check; later additions
-                              within 2 (new symbols only): sks_ani_rows, sks_intersect_layout_ani,
-                              sks_host_alloc, sks_host_free, sks_join_layout_stat_copy,
-                              sks_sketches_export, sks_all_pairs_ani,
-                              sks_ctx_set_layout_blocks_hint, sks_ctx_ani_table */
+#define SKS_ABI_VERSION 3  /* 3: a join layout's boff row ends with one more word, the log2 of
+                              the buckets per region, which the join reads: layouts built by
+                              an ABI-2 library (rows without that word) must not be joined by
+                              this one (round 5).  2: deduplicated join layout (masks, region
+                              ends), elem_words on the layout entry points,
+                              sks_ctx_set_join_check; later additions within 2 (new symbols
+                              only): sks_ani_rows, sks_intersect_layout_ani, sks_host_alloc,
+                              sks_host_free, sks_join_layout_stat_copy, sks_sketches_export,
+                              sks_all_pairs_ani, sks_ctx_set_layout_blocks_hint,
+                              sks_ctx_ani_table */
 
 typedef enum sks_status {
   SKS_OK = 0,
@@ -213,6 +217,23 @@ const uint64_t* sks_kmer_list_device_bits(const sks_kmer_list* list);
 /* Host copies; either pointer may be NULL. */
 int sks_kmer_list_copy(const sks_kmer_list* list, uint64_t* positions, uint64_t* bits);
 
+/* Every window of a record-stream piece, dense by start position, for a HOST
+ * predicate: the window sequence nucleotide_string_to_kmers hands to its
+ * std::function<bool(const kmer)> (kmer_sliding.cpp:144-183), without any
+ * selection.  Row i describes the window starting at byte first + i of d_seq
+ * (i < n_windows): {kmer_bits lo, hi, masked_bits lo} for window <= 32 (3
+ * words), {kmer_bits lo, hi, masked_bits lo, hi} for window > 32 (4 words);
+ * bit i % 64 of d_valid[i / 64] is set when all its bytes are ACGT (case-
+ * insensitive; any other byte ends a run, fasta_processing.cpp:144-179) — the
+ * rows of invalid windows are unspecified.  kmer_bits is the canonical window
+ * with the reference's 128-bit history (up to 64 bases of the run), so a caller
+ * cutting a stream into pieces passes min(first_of_piece, 64 - window) bytes
+ * of history before `first`.  Queued on the context stream (no host sync). */
+int sks_windows_dense(sks_ctx* ctx, const uint8_t* d_seq, uint64_t n_bytes, uint64_t first, uint64_t n_windows,
+                      int window, const uint64_t mask[2], uint64_t* d_rows, uint64_t* d_valid);
+/* Words per row of sks_windows_dense: 3 (window <= 32) or 4. */
+int sks_windows_dense_row_words(int window);
+
 /* ---- intersection: kmer_set.cpp:23-41, :143-184 ----------------------------------
  * Sketches in device memory: sketch i = d_data[d_starts[i]*elem_words ...],
  * d_sizes[i] elements, each sorted ascending and unique (as built above). */
@@ -284,7 +305,8 @@ uint32_t sks_join_layout_capacity(void);
 /* Value groups of a layout with 2^log_b buckets (bounds hold groups + 1 values). */
 uint32_t sks_join_layout_groups(uint32_t log_b);
 /* Words of one block's boff row: 2^log_b bucket starts + room for the region
- * ends + the region size word. */
+ * ends + the region size word (the row's last word, log2 of the buckets per
+ * region; added in ABI 3 — rows of ABI-2 layouts are one word shorter). */
 uint32_t sks_join_layout_boff_words(uint32_t log_b);
 /* Group bounds balanced for the set (quantiles averaged over up to 64 sample
  * sketches), queued on the context stream.  Any bounds give exact counts. */

@@ -7,11 +7,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
 #include <functional>
 #include <iostream>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -57,9 +60,9 @@ sks_ctx* ctx() {
   return g_ctx;
 }
 
-DevMem::DevMem(size_t bytes, int dev) : device(dev < 0 ? g_device : dev) {
+DevMem::DevMem(size_t n, int dev) : device(dev < 0 ? g_device : dev), bytes(n) {
   check_hip(hipSetDevice(device), "hipSetDevice");
-  check_hip(hipMalloc(&p, bytes ? bytes : 1), "hipMalloc");
+  check_hip(hipMalloc(&p, n ? n : 1), "hipMalloc");
 }
 
 DevMem::~DevMem() {
@@ -523,10 +526,26 @@ kmer canonical_kmer(kmer k) {
   return (k.masked_bits < rc.masked_bits) ? k : rc;
 }
 
+// kmer.hpp:135-149: H(masked_bits) ^ (H(mask) ^ hash<int>(w) ^ nonce).  The
+// second part depends on the mask, window and nonce only; a predicate calls
+// this once per window with the same three, so the last one is kept per thread.
 size_t frac_min_hash::operator()(const kmer& k) const {
-  uint64_t c[2] = {k.masked_bits.lo(), k.masked_bits.hi()};
-  uint64_t m[2] = {k.mask.lo(), k.mask.hi()};
-  return sks_frac_min_hash(c, m, k.window_length, nonce, flavour);
+  struct Memo {
+    uint64_t mlo = 0, mhi = 0, value = 0;
+    int w = -1, nonce = 0, flavour = -1;
+  };
+  thread_local Memo memo;
+  const uint64_t mlo = k.mask.lo(), mhi = k.mask.hi();
+  if (memo.w != k.window_length || memo.mlo != mlo || memo.mhi != mhi || memo.nonce != nonce ||
+      memo.flavour != flavour) {
+    memo.value = sks::fmh_const(mlo, mhi, k.window_length, nonce, flavour);
+    memo.mlo = mlo;
+    memo.mhi = mhi;
+    memo.w = k.window_length;
+    memo.nonce = nonce;
+    memo.flavour = flavour;
+  }
+  return sks::hash_bitset128_rt(k.masked_bits.lo(), k.masked_bits.hi(), flavour) ^ memo.value;
 }
 
 // ---- kmer_set -------------------------------------------------------------------------------------
@@ -745,43 +764,178 @@ std::vector<kmer> nucleotide_string_list_to_kmers(const std::vector<std::vector<
 namespace sks {
 namespace {
 
-std::mutex g_gpu_mu;  // the facade's context serves one build at a time
+// A worker of the host-predicate flow: its own context on its own HIP stream,
+// and double buffers (device and pinned host) for one piece of record stream
+// in and its dense window rows (sks_windows_dense) out.  Workers are pooled
+// for the process: a parallel_* call over many files takes one per thread.
+struct WindowWorker {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  sks_ctx* c = nullptr;
+  uint8_t* d_in[2] = {nullptr, nullptr};
+  uint64_t* d_rows[2] = {nullptr, nullptr};
+  uint64_t* d_valid[2] = {nullptr, nullptr};
+  uint8_t* h_in[2] = {nullptr, nullptr};
+  uint64_t* h_rows[2] = {nullptr, nullptr};
+  uint64_t* h_valid[2] = {nullptr, nullptr};
+  hipEvent_t ev_c0[2] = {nullptr, nullptr}, ev_c1[2] = {nullptr, nullptr};  // around the D2H copies
+  ~WindowWorker() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (c) sks_ctx_destroy(c);
+    for (int i = 0; i < 2; ++i) {
+      (void)hipFree(d_in[i]);
+      (void)hipFree(d_rows[i]);
+      (void)hipFree(d_valid[i]);
+      (void)hipHostFree(h_in[i]);
+      (void)hipHostFree(h_rows[i]);
+      (void)hipHostFree(h_valid[i]);
+      if (ev_c0[i]) (void)hipEventDestroy(ev_c0[i]);
+      if (ev_c1[i]) (void)hipEventDestroy(ev_c1[i]);
+    }
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// window starts per piece (SKS_FACADE_PIECE: bytes, for tests that cut small
+// inputs into many pieces); rows are at most 4 words (w > 32)
+uint64_t piece_windows() {
+  static const uint64_t p = [] {
+    const char* e = getenv("SKS_FACADE_PIECE");
+    const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return v >= 64 ? v : (uint64_t)1 << 20;
+  }();
+  return p;
+}
+constexpr uint64_t kHistory = 64;  // bytes before a piece: F's 128-bit history
+
+std::mutex g_workers_mu;
+std::vector<std::unique_ptr<WindowWorker>> g_workers;  // idle workers
+
+std::unique_ptr<WindowWorker> make_worker(int device) {
+  std::unique_ptr<WindowWorker> wk(new WindowWorker);
+  wk->device = device;
+  check_hip(hipSetDevice(device), "hipSetDevice");
+  check_hip(hipStreamCreateWithFlags(&wk->stream, hipStreamNonBlocking), "hipStreamCreate");
+  check(sks_ctx_create(device, wk->stream, &wk->c));
+  const uint64_t P = piece_windows();
+  for (int i = 0; i < 2; ++i) {
+    check_hip(hipMalloc(&wk->d_in[i], P + 2 * kHistory), "hipMalloc");
+    check_hip(hipMalloc(&wk->d_rows[i], P * 4 * 8), "hipMalloc");
+    check_hip(hipMalloc(&wk->d_valid[i], (P / 64 + 1) * 8), "hipMalloc");
+    check_hip(hipHostMalloc(&wk->h_in[i], P + 2 * kHistory, hipHostMallocDefault), "hipHostMalloc");
+    check_hip(hipHostMalloc(&wk->h_rows[i], P * 4 * 8, hipHostMallocDefault), "hipHostMalloc");
+    check_hip(hipHostMalloc(&wk->h_valid[i], (P / 64 + 1) * 8, hipHostMallocDefault), "hipHostMalloc");
+    check_hip(hipEventCreate(&wk->ev_c0[i]), "hipEventCreate");
+    check_hip(hipEventCreate(&wk->ev_c1[i]), "hipEventCreate");
+  }
+  return wk;
+}
+
+struct WorkerLease {
+  std::unique_ptr<WindowWorker> w;
+  explicit WorkerLease(int device) {
+    {
+      std::lock_guard<std::mutex> lock(g_workers_mu);
+      for (size_t i = 0; i < g_workers.size(); ++i)
+        if (g_workers[i]->device == device) {
+          w = std::move(g_workers[i]);
+          g_workers.erase(g_workers.begin() + i);
+          break;
+        }
+    }
+    if (!w) w = make_worker(device);
+  }
+  ~WorkerLease() {
+    if (!w) return;
+    (void)hipSetDevice(w->device);
+    if (hipStreamSynchronize(w->stream) != hipSuccess) return;  // a failed stream: drop the worker
+    std::lock_guard<std::mutex> lock(g_workers_mu);
+    g_workers.push_back(std::move(w));
+  }
+};
+
+std::mutex g_stats_mu;
+window_flow_stats g_stats{};
+
+double ms_between(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+  return std::chrono::duration<double, std::milli>(b - a).count();
+}
 
 // Every window of a record stream, in order (kmer_sliding.cpp:144-185 over
-// each run), as the reference's kmer objects, handed to `fn`.  The windows
-// come from the GPU list build at c = 1 (every valid window, canonical masked
-// bits and the unmasked kmer_bits); the stream is cut into pieces of kPiece
-// bytes plus a (w - 1)-byte halo, keeping the windows that start inside each
-// piece's own range, so host buffers stay bounded for any genome size.
+// each run), as the reference's kmer objects, handed to `fn`.  The stream is
+// cut into pieces of piece_windows() window starts; each piece goes to the
+// worker's device with up to 64 bytes of history in front (F's 128-bit
+// register) and w - 1 behind, sks_windows_dense writes every window's row,
+// and the rows come back to pinned memory.  Piece k + 1's copy in, kernel and
+// copy out run on the worker's stream while the host runs `fn` over piece k.
 void for_each_window(const std::vector<uint8_t>& stream, const kmer_bitset& mask, int w,
                      const std::function<void(const kmer&)>& fn) {
-  constexpr uint64_t kPiece = 2u << 20;
+  const auto t_begin = std::chrono::steady_clock::now();
   const uint64_t n = stream.size();
-  const sks_policy every{SKS_FRAC_MOD, hash_flavour(), 1, 1};
+  if (w < 1 || w > 64) throw std::invalid_argument("window length must be 1..64");
+  if (n < (uint64_t)w) return;
+  const uint64_t starts = n - w + 1, P = piece_windows();
+  const uint64_t pieces = (starts + P - 1) / P;
+  const int words = sks_windows_dense_row_words(w);
   const uint64_t m[2] = {mask.lo(), mask.hi()};
-  std::vector<uint64_t> pos, bits;
-  for (uint64_t a = 0; a < n; a += kPiece) {
-    const uint64_t own = std::min(kPiece, n - a);
-    const uint64_t len = std::min(n - a, own + (uint64_t)(w > 0 ? w - 1 : 0));
-    uint64_t cnt = 0;
-    {
-      std::lock_guard<std::mutex> lock(g_gpu_mu);
-      DevMem d(len);
-      check_hip(hipMemcpy(d.p, stream.data() + a, len, hipMemcpyHostToDevice), "hipMemcpy H2D");
-      const uint64_t seg[2] = {0, len};
-      sks_kmer_list* kl = nullptr;
-      check(sks_kmer_list_build(ctx(), d.as<uint8_t>(), len, seg, 1, w, m, &every, &kl));
-      cnt = sks_kmer_list_total(kl);
-      pos.resize(cnt);
-      bits.resize(4 * cnt);
-      const int rc = sks_kmer_list_copy(kl, pos.data(), bits.data());
-      sks_kmer_list_free(kl);
-      check(rc);
+  WorkerLease lease(g_device);
+  WindowWorker& wk = *lease.w;
+  struct Piece {
+    uint64_t a, cnt;
+  };
+  auto issue = [&](uint64_t k) {
+    const int sl = (int)(k & 1);
+    const uint64_t a = k * P, cnt = std::min(P, starts - a);
+    const uint64_t h = std::min<uint64_t>(a, kHistory - w);
+    const uint64_t lo = a - h, hi = std::min(n, a + cnt + w - 1);
+    std::memcpy(wk.h_in[sl], stream.data() + lo, hi - lo);
+    check_hip(hipMemcpyAsync(wk.d_in[sl], wk.h_in[sl], hi - lo, hipMemcpyHostToDevice, wk.stream), "H2D");
+    check(sks_windows_dense(wk.c, wk.d_in[sl], hi - lo, h, cnt, w, m, wk.d_rows[sl], wk.d_valid[sl]));
+    check_hip(hipEventRecord(wk.ev_c0[sl], wk.stream), "hipEventRecord");
+    check_hip(hipMemcpyAsync(wk.h_rows[sl], wk.d_rows[sl], cnt * words * 8, hipMemcpyDeviceToHost, wk.stream),
+              "D2H");
+    check_hip(hipMemcpyAsync(wk.h_valid[sl], wk.d_valid[sl], (cnt + 63) / 64 * 8, hipMemcpyDeviceToHost,
+                             wk.stream), "D2H");
+    check_hip(hipEventRecord(wk.ev_c1[sl], wk.stream), "hipEventRecord");
+    return Piece{a, cnt};
+  };
+  window_flow_stats st{};
+  Piece cur = issue(0);
+  for (uint64_t k = 0; k < pieces; ++k) {
+    const int sl = (int)(k & 1);
+    const Piece nxt = k + 1 < pieces ? issue(k + 1) : Piece{0, 0};  // the slot of piece k - 1, done
+    const auto t_wait = std::chrono::steady_clock::now();
+    check_hip(hipEventSynchronize(wk.ev_c1[sl]), "hipEventSynchronize");
+    const auto t_run = std::chrono::steady_clock::now();
+    float copy_ms = 0;
+    (void)hipEventElapsedTime(&copy_ms, wk.ev_c0[sl], wk.ev_c1[sl]);
+    st.d2h_ms += copy_ms;
+    st.d2h_bytes += cur.cnt * words * 8 + (cur.cnt + 63) / 64 * 8;
+    st.wait_ms += ms_between(t_wait, t_run);
+    const uint64_t* rows = wk.h_rows[sl];
+    const uint64_t* valid = wk.h_valid[sl];
+    for (uint64_t vw = 0; vw < (cur.cnt + 63) / 64; ++vw) {
+      for (uint64_t bits = valid[vw]; bits; bits &= bits - 1) {
+        const uint64_t i = vw * 64 + (uint64_t)__builtin_ctzll(bits);
+        const uint64_t* r = rows + i * words;
+        fn(kmer{w, kmer_bitset(r[0], r[1]), mask, kmer_bitset(r[2], words == 4 ? r[3] : 0)});
+        ++st.windows;
+      }
     }
-    for (uint64_t i = 0; i < cnt && pos[i] < own; ++i)
-      fn(kmer{w, kmer_bitset(bits[4 * i], bits[4 * i + 1]), mask,
-              kmer_bitset(bits[4 * i + 2], bits[4 * i + 3])});
+    st.predicate_ms += ms_between(t_run, std::chrono::steady_clock::now());
+    ++st.pieces;
+    cur = nxt;
   }
+  st.wall_ms = ms_between(t_begin, std::chrono::steady_clock::now());
+  std::lock_guard<std::mutex> lock(g_stats_mu);
+  g_stats.windows += st.windows;
+  g_stats.pieces += st.pieces;
+  g_stats.d2h_bytes += st.d2h_bytes;
+  g_stats.d2h_ms += st.d2h_ms;
+  g_stats.wait_ms += st.wait_ms;
+  g_stats.predicate_ms += st.predicate_ms;
+  g_stats.wall_ms += st.wall_ms;
 }
 
 std::vector<uint8_t> file_stream(const char* path) {
@@ -806,7 +960,29 @@ kmer_set set_from_stream(const std::vector<uint8_t>& stream, const kmer_bitset& 
   return ks;
 }
 
+int g_host_threads = 0;  // set_host_threads; 0 = SKS_FACADE_THREADS, else min(16, cores)
+
 }  // namespace
+
+window_flow_stats take_window_flow_stats() {
+  std::lock_guard<std::mutex> lock(g_stats_mu);
+  window_flow_stats s = g_stats;
+  g_stats = window_flow_stats{};
+  return s;
+}
+
+void set_host_threads(int n) { g_host_threads = n > 0 ? n : 0; }
+
+int host_threads() {
+  if (g_host_threads > 0) return g_host_threads;
+  if (const char* e = getenv("SKS_FACADE_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
+  // the GPU box's share of host cores is 16 even where the machine shows more
+  return std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
+}
+
 }  // namespace sks
 
 kmer_set kmer_set_from_fasta_file(const char fasta_filename[], const kmer_bitset& mask,
@@ -837,7 +1013,10 @@ std::vector<kmer_set> parallel_kmer_sets_from_fasta_files(const int num_files, c
   std::vector<std::exception_ptr> err(n);
   std::vector<std::thread> ts;
   std::atomic<int> next{0};
-  const int workers = std::max(1, std::min<int>(n, (int)std::thread::hardware_concurrency()));
+  // one host thread per file in flight (the reference's cilk_for over files,
+  // kmer_set.cpp:124), each with its own device worker (context, stream, pinned
+  // buffers): the predicates run in parallel while the devices extract windows
+  const int workers = std::max(1, std::min<int>(n, sks::host_threads()));
   for (int t = 0; t < workers; ++t)
     ts.emplace_back([&]() {
       for (int i; (i = next.fetch_add(1)) < n;) {

@@ -20,6 +20,7 @@ sks_ctx* ctx();  // the facade's context on the selected device (set_device)
 struct DevMem {
   void* p = nullptr;
   int device = 0;
+  size_t bytes = 0;
   explicit DevMem(size_t bytes, int device = -1);
   ~DevMem();
   DevMem(const DevMem&) = delete;

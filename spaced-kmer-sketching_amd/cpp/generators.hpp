@@ -18,7 +18,7 @@ std::pair<std::vector<T>, std::vector<T>> generate_pairwise_from_vector(const st
     first.push_back(v[i]);
     second.push_back(v[(i + 1) % n]);
   }
-  return {first, second};
+  return {std::move(first), std::move(second)};
 }
 
 template <typename T>
@@ -32,5 +32,5 @@ std::pair<std::vector<T>, std::vector<T>> generate_all_pairs_from_vector(const s
       first.push_back(v[i]);
       second.push_back(v[j]);
     }
-  return {first, second};
+  return {std::move(first), std::move(second)};
 }

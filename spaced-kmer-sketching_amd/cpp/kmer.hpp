@@ -152,6 +152,24 @@ int hash_flavour();
 uint64_t bitset_hash(const kmer_bitset& b);
 }  // namespace sks
 
+// The host-predicate flow (every builder taking a std::function: the GPU
+// extracts every window, the host predicate selects): totals since the last
+// take, summed over the worker threads of a parallel_* call.  d2h_ms sums the
+// device-to-host copy durations (HIP events), wait_ms the host's waits for a
+// piece, predicate_ms the host time spent in the predicate loops.
+namespace sks {
+struct window_flow_stats {
+  uint64_t windows = 0, pieces = 0, d2h_bytes = 0;
+  double d2h_ms = 0, wait_ms = 0, predicate_ms = 0, wall_ms = 0;
+};
+window_flow_stats take_window_flow_stats();
+// Host threads of parallel_kmer_sets_from_fasta_files with a std::function
+// predicate (one device worker each); 0 restores the default
+// (SKS_FACADE_THREADS, else min(16, cores)).
+void set_host_threads(int n);
+int host_threads();
+}  // namespace sks
+
 struct kmer_hash {
   size_t operator()(const kmer& k) const {
     return sks::bitset_hash(k.masked_bits) ^ sks::bitset_hash(k.mask) ^ (size_t)k.window_length;

@@ -35,6 +35,16 @@ struct genome_batch::impl {
   std::vector<std::string> names;
   std::unique_ptr<DevMem> stream;  // record streams of all files, back to back
   std::vector<uint64_t> off;       // file i = stream[off[i], off[i+1])
+  // the all-pairs step's buffers, kept across configurations (a hipFree per
+  // configuration synchronises the device): the n x n count tiles and two
+  // status words on the device, the n x n ANI matrix in pinned host memory
+  // mapped into the device (the join writes it)
+  std::unique_ptr<DevMem> counts, status;
+  double* ani_host = nullptr;
+  std::unique_ptr<std::pair<std::vector<std::string>, std::vector<std::string>>> names_pairs[2];
+  ~impl() {
+    if (ani_host) sks_host_free(ani_host);
+  }
 };
 
 genome_batch::genome_batch(int num_files, char* filenames[]) : p_(new impl) {
@@ -66,6 +76,16 @@ genome_batch::~genome_batch() { delete p_; }
 
 size_t genome_batch::size() const { return p_->names.size(); }
 const std::vector<std::string>& genome_batch::filenames() const { return p_->names; }
+
+const std::pair<std::vector<std::string>, std::vector<std::string>>& genome_batch::pair_names(
+    pair_mode mode) const {
+  auto& slot = p_->names_pairs[mode == pair_mode::all_pairs ? 0 : 1];
+  if (!slot)
+    slot.reset(new std::pair<std::vector<std::string>, std::vector<std::string>>(
+        mode == pair_mode::all_pairs ? generate_all_pairs_from_vector(p_->names)
+                                     : generate_pairwise_from_vector(p_->names)));
+  return *slot;
+}
 uint64_t genome_batch::stream_bytes() const { return p_->off.back(); }
 
 namespace {
@@ -76,7 +96,8 @@ double ms_since(std::chrono::high_resolution_clock::time_point t0) {
 }  // namespace
 
 genome_batch::comparison genome_batch::compare(const kmer_bitset& mask, int window_size,
-                                               const sketch_policy& policy, pair_mode mode) const {
+                                               const sketch_policy& policy, pair_mode mode,
+                                               int kmer_num_ones) const {
   comparison res;
   const uint32_t n = (uint32_t)size();
   if (n == 0) return res;
@@ -96,6 +117,40 @@ genome_batch::comparison genome_batch::compare(const kmer_bitset& mask, int wind
   const uint64_t* starts = sks_sketch_set_device_starts(set);
   const uint32_t* dsizes = sks_sketch_set_device_sizes(set);
   const int ew = sks_sketch_set_elem_words(set);
+  if (mode == pair_mode::all_pairs && kmer_num_ones > 0 && n <= 16384) {
+    // kmer-sketching.cpp:185-200 in one native call: the join layout of the n
+    // sketches, every upper-triangle 64 x 64 tile in one k_join launch, and
+    // containment / ANI of both orientations written by each tile's last
+    // workgroup straight into the pinned host matrix (no count read-back, no
+    // host pow loop)
+    const uint64_t pairs = (uint64_t)n * n, tiles = sks_intersect_sym_tiles(n);
+    uint64_t total = 0;
+    uint32_t max_size = 1;
+    for (uint32_t v : sizes) {
+      total += v;
+      max_size = std::max(max_size, v);
+    }
+    if (!p_->counts || p_->counts->bytes < tiles * 4096 * 4) p_->counts.reset(new DevMem(tiles * 4096 * 4));
+    if (!p_->status) p_->status.reset(new DevMem(8));
+    if (!p_->ani_host) {
+      void* h = nullptr;
+      check(sks_host_alloc(pairs * sizeof(double), 0, &h));
+      p_->ani_host = static_cast<double*>(h);
+    }
+    check(sks_all_pairs_ani(ctx(), data, starts, dsizes, ew, n, max_size, std::max<uint64_t>(total, 1),
+                            kmer_num_ones, p_->ani_host, p_->counts->as<int32_t>(),
+                            p_->status->as<uint32_t>()));
+    check(sks_ctx_synchronize(ctx()));
+    uint32_t stat[2] = {0, 0};
+    check_hip(hipMemcpy(stat, p_->status->p, 8, hipMemcpyDeviceToHost), "D2H");
+    if (stat[1] == 0) {
+      res.ani.assign(p_->ani_host, p_->ani_host + pairs);
+      res.compare_ms = ms_since(t0);
+      return res;
+    }
+    // a layout that could not place a value group (adversarial 128-bit
+    // values): count with sks_intersect_all below, ANI on the host
+  }
   if (mode == pair_mode::all_pairs) {
     const uint64_t pairs = (uint64_t)n * n;
     DevMem d_out(pairs * 4);
@@ -131,14 +186,16 @@ void ani_sweep_config(const genome_batch& batch, pair_mode mode, int window_size
                       const sketch_policy& policy) {
   const kmer_bitset mask = generate_random_spaced_seed_mask(window_size, kmer_size);
   const int kmer_num_indices = (int)(mask.count() / NUCLEOTIDE_BIT_SIZE);
-  genome_batch::comparison c = batch.compare(mask, window_size, policy, mode);
+  genome_batch::comparison c = batch.compare(mask, window_size, policy, mode, kmer_num_indices);
   log << "Time taken for sketching = " << c.sketch_ms << " ms" << std::endl;
   auto t0 = std::chrono::high_resolution_clock::now();
-  std::vector<double> ani(c.intersections.size());
-  for (size_t i = 0; i < ani.size(); ++i)
-    ani[i] = binomial_estimator(containment(c.intersections[i], c.first_sizes[i]), kmer_num_indices);
-  auto names = mode == pair_mode::all_pairs ? generate_all_pairs_from_vector(batch.filenames())
-                                            : generate_pairwise_from_vector(batch.filenames());
+  std::vector<double> ani = std::move(c.ani);
+  if (ani.empty()) {  // the counts came back instead (adjacent pairs, or the fallback)
+    ani.resize(c.intersections.size());
+    for (size_t i = 0; i < ani.size(); ++i)
+      ani[i] = binomial_estimator(containment(c.intersections[i], c.first_sizes[i]), kmer_num_indices);
+  }
+  const auto& names = batch.pair_names(mode);
   log << "Time taken for comparison = " << c.compare_ms + ms_since(t0) << " ms" << std::endl;
   write_to_csv(names.first, names.second, ani, window_size, mask, output_filename, is_append);
 }

@@ -43,16 +43,24 @@ class genome_batch {
 
   size_t size() const;
   const std::vector<std::string>& filenames() const;
+  // the file-name pairs of every configuration's CSV rows, generated once per
+  // batch (the reference regenerates them per configuration, :180-183)
+  const std::pair<std::vector<std::string>, std::vector<std::string>>& pair_names(pair_mode mode) const;
   uint64_t stream_bytes() const;
 
   struct comparison {
     std::vector<int> intersections;  // per pair, in generator order
     std::vector<int> first_sizes;    // kmer_set_size() of each pair's first set
+    // all_pairs: binomial_estimator(containment(...)) of every pair, written by
+    // the join itself (sks_all_pairs_ani, fp64 on the device; within 1e-9 of the
+    // host's doubles); empty when the caller computes it from the counts
+    std::vector<double> ani;
     double sketch_ms = 0, compare_ms = 0;  // host wall time of the two phases
   };
+  // kmer_num_ones > 0 asks for the ANI with the counts (all_pairs mode).
   // Sketch every genome with (mask, window, policy), then count the pairs.
   comparison compare(const kmer_bitset& mask, int window_size, const sketch_policy& policy,
-                     pair_mode mode) const;
+                     pair_mode mode, int kmer_num_ones = 0) const;
 
  private:
   struct impl;

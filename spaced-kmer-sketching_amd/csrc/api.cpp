@@ -469,6 +469,36 @@ int alloc_u64(uint64_t** p, uint64_t words, size_t* bytes_out = nullptr) {
 
 }  // namespace
 
+namespace {
+
+// The fused ANI store runs in k_join: the caller's matrix must be memory the
+// device can write — device memory, managed memory, or pinned host memory
+// mapped into the device (sks_host_alloc), whose device-side address is
+// returned.  An ordinary malloc/numpy buffer is refused (SKS_E_ARG) instead of
+// being handed to the kernel, where the store would fault (XNACK is off).
+int device_view_of_ani(double* ani, double** d_ani, const char* who) {
+  hipPointerAttribute_t at{};
+  const hipError_t e = hipPointerGetAttributes(&at, ani);
+  (void)hipGetLastError();  // an unknown pointer leaves an error behind
+  if (e != hipSuccess || at.type == hipMemoryTypeUnregistered)
+    return sks::fail(SKS_E_ARG, std::string(who) + ": the ANI matrix is neither device memory nor pinned "
+                                "host memory mapped into the device (use sks_host_alloc)");
+  if (at.type == hipMemoryTypeHost) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, ani, 0) != hipSuccess || !dp) {
+      (void)hipGetLastError();
+      return sks::fail(SKS_E_ARG, std::string(who) + ": the pinned host ANI matrix is not mapped into the "
+                                  "device (use sks_host_alloc)");
+    }
+    *d_ani = static_cast<double*>(dp);
+  } else {
+    *d_ani = ani;
+  }
+  return SKS_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int sks_abi_version(void) { return SKS_ABI_VERSION; }
@@ -567,7 +597,7 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
   c->stream = reinterpret_cast<hipStream_t>(stream);
   // every scratch buffer is used on the context's stream only
   for (sks::Scratch* sc : {&c->ingress, &c->tmp, &c->rec[0], &c->rec[1], &c->rec[2], &c->flag,
-                           &c->pos, &c->meta, &c->iwork, &c->tdone, &c->lay})
+                           &c->pos, &c->meta, &c->iwork, &c->tdone, &c->lay, &c->root})
     sc->owner = &c->stream;
   for (auto& b : c->buf) b.owner = &c->stream;
   if (hipEventCreate(&c->ev_begin) != hipSuccess || hipEventCreate(&c->ev_end) != hipSuccess ||
@@ -593,6 +623,7 @@ int sks_ctx_destroy(sks_ctx* c) {
   c->iwork.release();
   c->tdone.release();
   c->lay.release();
+  c->root.release();
   c->ingress.release();
   trim_device_cache(c->device);
   (void)hipEventDestroy(c->ev_begin);
@@ -800,14 +831,28 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   // (sks::BitRuns) and expanded again when the unique elements are scattered
   const sks::BitRuns runs = S.wide ? sks::BitRuns{} : sks::bit_runs(S.mask_lo);
   const int key_bits = S.wide ? 64 : std::max(1, __builtin_popcountll(S.mask_lo));
-  SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st, &runs));
-  // narrow bottom-s records carry the k-mer as key (its fmh is recomputed here)
-  const bool has_val = S.wide || (bottom && S.wide);
-  if (has_val) SKS_HIP(sks::compact_regions(rv, col(c, 1), d_src, d_csr, k, max_len, st));
-  if (bottom && S.wide) SKS_HIP(sks::compact_regions(rh, col(c, 2), d_src, d_csr, k, max_len, st));
-
   const int mask_lo_bits = end_bit_of(S.mask_lo);
   const int mask_hi_bits = end_bit_of(S.mask_hi);
+  // FracMinHash over several genomes: the segment index rides above the key (or,
+  // 128-bit, above the high word) and every sort below is ONE device-wide radix
+  // sort over all segments (compact_regions); a segmented sort gives each genome
+  // one workgroup (reference sweep, 64 x 5 Mb at c = 200: 0.50 ms per narrow
+  // sort, 2 x 0.68 ms per 128-bit one)
+  const int tag_bits = sks::seg_tag_bits(k);
+  const int tag_at = S.wide ? mask_hi_bits : key_bits;
+  const bool tagged = !bottom && k >= 2 && tag_at + tag_bits <= 64 && getenv("SKS_SEGMENTED_SORT") == nullptr;
+  const std::vector<uint64_t> one_seg{0, T};
+  const std::vector<uint64_t>& sort_off = tagged ? one_seg : csr;
+  const uint64_t* d_sort_off = tagged ? nullptr : d_csr;
+  const uint64_t keep = tag_at >= 64 ? ~0ull : (1ull << tag_at) - 1;  // the key bits below the tag
+  SKS_HIP(sks::compact_regions(rk, col(c, 0), d_src, d_csr, k, max_len, st, &runs,
+                               tagged && !S.wide ? key_bits : -1));
+  // narrow bottom-s records carry the k-mer as key (its fmh is recomputed here)
+  const bool has_val = S.wide || (bottom && S.wide);
+  if (has_val)
+    SKS_HIP(sks::compact_regions(rv, col(c, 1), d_src, d_csr, k, max_len, st, nullptr, tagged ? mask_hi_bits : -1));
+  if (bottom && S.wide) SKS_HIP(sks::compact_regions(rh, col(c, 2), d_src, d_csr, k, max_len, st));
+
   uint64_t max_thr = 0;
   for (uint32_t i = 0; i < k; ++i) max_thr = std::max(max_thr, thresh[ok[i]]);
 
@@ -818,16 +863,26 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
   if (!bottom) {
     const uint64_t* K;   // sorted unique columns source
     const uint64_t* K2 = nullptr;
-    if (!S.wide) {
-      SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, csr, d_csr, key_bits, c->tmp, st));
+    if (!S.wide && (tagged || k < 2 || getenv("SKS_SEGMENTED_SORT"))) {
+      SKS_HIP(sks::seg_sort_keys(col(c, 0), col(c, 3), T, sort_off, d_sort_off,
+                                 key_bits + (tagged ? tag_bits : 0), c->tmp, st));
       K = col(c, 3);
+    } else if (!S.wide) {
+      // keys too wide for a tag above them (2k + tag bits > 64): two stable
+      // device-wide passes, by key with the segment as value, then by segment
+      SKS_HIP(sks::launch_seg_ids(col(c, 1), d_csr, k, max_len, st));
+      SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), T, one_seg, nullptr, key_bits,
+                                  c->tmp, st));
+      SKS_HIP(sks::seg_sort_pairs(col(c, 4), col(c, 5), col(c, 3), col(c, 6), T, one_seg, nullptr,
+                                  std::max(1, tag_bits), c->tmp, st));
+      K = col(c, 6);
     } else {
       // (lo, hi) -> sort by lo, then stable by hi  => ascending 128-bit order
-      SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), T, csr, d_csr, 64,
-                                  c->tmp, st));
-      SKS_HIP(sks::seg_sort_pairs(col(c, 4), col(c, 5), col(c, 3), col(c, 6), T, csr, d_csr,
-                                  mask_hi_bits, c->tmp, st));
-      K = col(c, 5);   // hi
+      SKS_HIP(sks::seg_sort_pairs(col(c, 0), col(c, 3), col(c, 1), col(c, 4), T, sort_off, d_sort_off,
+                                  mask_lo_bits, c->tmp, st));
+      SKS_HIP(sks::seg_sort_pairs(col(c, 4), col(c, 5), col(c, 3), col(c, 6), T, sort_off, d_sort_off,
+                                  mask_hi_bits + (tagged ? tag_bits : 0), c->tmp, st));
+      K = col(c, 5);   // hi (tagged)
       K2 = col(c, 6);  // lo
     }
     SKS_HIP(sks::seg_unique_scan(K, K2, T, max_len, d_csr, k, d_flag, d_pos, d_uniq, c->tmp, st));
@@ -837,10 +892,10 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
     SKS_TRY(alloc_u64(&po.d, U * S.ew, &po.bytes));
     if (!S.wide) {
       SKS_HIP(sks::seg_unique_scatter(K, nullptr, T, max_len, d_csr, k, d_flag, d_pos, nullptr, nullptr,
-                                      po.d, nullptr, st, &runs));
+                                      po.d, nullptr, st, &runs, keep));
     } else {
       SKS_HIP(sks::seg_unique_scatter(K2, K, T, max_len, d_csr, k, d_flag, d_pos, nullptr, nullptr,
-                                      col(c, 7), col(c, 8), st));
+                                      col(c, 7), col(c, 8), st, nullptr, ~0ull, keep));
       SKS_HIP(sks::launch_interleave(col(c, 7), col(c, 8), U, po.d, st));
     }
     for (uint32_t i = 0; i < k; ++i) final_size_local[ok[i]] = uniq[i];
@@ -1554,6 +1609,21 @@ int sks_kmer_list_copy(const sks_kmer_list* kl, uint64_t* positions, uint64_t* b
   return SKS_OK;
 }
 
+int sks_windows_dense_row_words(int window) { return window > 32 ? 4 : 3; }
+
+int sks_windows_dense(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, uint64_t first, uint64_t n_windows,
+                      int window, const uint64_t mask[2], uint64_t* d_rows, uint64_t* d_valid) {
+  if (!c || !mask) return sks::fail(SKS_E_ARG, "sks_windows_dense: null argument");
+  if (window < 1 || window > 64) return sks::fail(SKS_E_ARG, "sks_windows_dense: window must be 1..64");
+  if (first > n_bytes) return sks::fail(SKS_E_ARG, "sks_windows_dense: first beyond the buffer");
+  if (n_windows == 0) return SKS_OK;
+  if (!d_seq || !d_rows || !d_valid) return sks::fail(SKS_E_ARG, "sks_windows_dense: null buffer");
+  DeviceGuard g(c->device);
+  SKS_HIP(sks::launch_windows_dense(d_seq, n_bytes, first, n_windows, window, mask[0], mask[1], d_rows, d_valid,
+                                    c->stream));
+  return SKS_OK;
+}
+
 // ---- intersections ----------------------------------------------------------------------------
 
 int sks_intersect_pairs(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts,
@@ -1805,15 +1875,7 @@ int sks_intersect_layout_ani(sks_ctx* c, uint32_t n, uint32_t log_b, int elem_wo
   DeviceGuard g(c->device);
   // the ANI matrix may be host memory: the kernel needs its device-side address
   double* d_ani = ani;
-  if (tile_end > tile_begin) {
-    hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, ani) == hipSuccess && at.type == hipMemoryTypeHost) {
-      void* dp = nullptr;
-      SKS_HIP(hipHostGetDevicePointer(&dp, ani, 0));
-      d_ani = static_cast<double*>(dp);
-    }
-    (void)hipGetLastError();  // an unregistered pointer leaves an error behind; use it as is
-  }
+  if (tile_end > tile_begin) SKS_TRY(device_view_of_ani(ani, &d_ani, "sks_intersect_layout_ani"));
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   if (n && tile_end > tile_begin) {
     const uint64_t nt = tile_end - tile_begin;
@@ -1842,15 +1904,7 @@ int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   if (total >= (1ull << 32)) return sks::fail(SKS_E_UNSUPPORTED, "sks_all_pairs_ani: >= 2^32 elements");
   DeviceGuard g(c->device);
   double* d_ani = ani;
-  if (ani && n) {
-    hipPointerAttribute_t at{};
-    if (hipPointerGetAttributes(&at, ani) == hipSuccess && at.type == hipMemoryTypeHost) {
-      void* dp = nullptr;
-      SKS_HIP(hipHostGetDevicePointer(&dp, ani, 0));
-      d_ani = static_cast<double*>(dp);
-    }
-    (void)hipGetLastError();
-  }
+  if (ani && n) SKS_TRY(device_view_of_ani(ani, &d_ani, "sks_all_pairs_ani"));
   if (n == 0) {
     if (d_status) SKS_HIP(hipMemsetAsync(d_status, 0, 8, c->stream));
     SKS_HIP(hipEventRecord(c->ev_begin, c->stream));

@@ -95,8 +95,15 @@ static_assert(kJCap == 1024, "entry index: 10 bits of the slot word");
 static_assert(kFSlots >= kTile * kTile, "the fused ANI stages a tile's counts in the slot table");
 
 // s_waitcnt immediate for gfx9 "vmcnt(0)" with expcnt / lgkmcnt left at their
-// maxima: vmcnt = imm[3:0] | imm[15:14] << 4, expcnt = imm[6:4], lgkmcnt = imm[11:8]
+// maxima: vmcnt = imm[3:0] | imm[15:14] << 4, expcnt = imm[6:4], lgkmcnt = imm[11:8].
+// The fused ANI's fence-free hand-off (a wave drains its count atomics with this
+// wait, then the workgroup bumps the tile counter) relies on gfx9 counting
+// no-return atomics in vmcnt; gfx10+ counts them in vscnt, where this wait would
+// not cover them.  This file is built for gfx950 only: refuse anything else.
 constexpr int kWaitVmcnt0 = 0x0F70;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "join.hip: the fused ANI hand-off (kWaitVmcnt0) is written for gfx950 (gfx9 vmcnt semantics)"
+#endif
 
 struct JoinArgs {
   JoinLayout r, c;          // row blocks (tile row I = block r_blk0 + I) and column blocks

@@ -121,6 +121,10 @@ __device__ __forceinline__ uint64_t runs_pack(uint64_t x, const BitRuns& r) {
 }
 
 __device__ __forceinline__ uint64_t runs_expand(uint64_t x, const BitRuns& r) {
+  // a packed key holds popcount(mask) bits; anything above them (a segment tag,
+  // compact_regions) is not part of the k-mer
+  const int width = __popcll(r.mask);
+  if (width < 64) x &= (1ull << width) - 1;
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     const uint64_t mv = r.mv[i];
@@ -132,12 +136,13 @@ __device__ __forceinline__ uint64_t runs_expand(uint64_t x, const BitRuns& r) {
 template <bool PACK>
 __global__ void k_compact(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
                           const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ dst_off,
-                          const BitRuns runs) {
+                          const BitRuns runs, int tag_shift) {
   const uint32_t g = blockIdx.y;
   const uint64_t len = dst_off[g + 1] - dst_off[g];
   const uint64_t so = src_off[g], d0 = dst_off[g];
+  const uint64_t tag = tag_shift >= 0 ? (uint64_t)g << tag_shift : 0;  // the segment above the key bits
   for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < len; i += (uint64_t)gridDim.x * kB)
-    dst[d0 + i] = PACK ? runs_pack(src[so + i], runs) : src[so + i];
+    dst[d0 + i] = (PACK ? runs_pack(src[so + i], runs) : src[so + i]) | tag;
 }
 
 __global__ void k_bits_expand(uint64_t* __restrict__ keys, uint64_t n, const BitRuns runs) {
@@ -166,16 +171,16 @@ __global__ void k_scatter(const uint64_t* __restrict__ vals, const uint64_t* __r
                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ flag,
                           const uint64_t* __restrict__ pos, const uint64_t* __restrict__ limit,
                           const uint64_t* __restrict__ dst_off, uint64_t* __restrict__ out,
-                          uint64_t* __restrict__ out2, const BitRuns runs) {
+                          uint64_t* __restrict__ out2, const BitRuns runs, uint64_t keep, uint64_t keep2) {
   const uint32_t g = blockIdx.y;
   const uint64_t b = off[g], e = off[g + 1];
   const uint64_t p0 = pos[b], lim = limit ? limit[g] : ~0ull, d0 = dst_off ? dst_off[g] : p0;
   for (uint64_t i = b + (uint64_t)blockIdx.x * kB + threadIdx.x; i < e; i += (uint64_t)gridDim.x * kB) {
     if (!flag[i]) continue;
     uint64_t r = pos[i] - p0;
-    if (r < lim) {
-      out[d0 + r] = EXPAND ? runs_expand(vals[i], runs) : vals[i];
-      if (out2) out2[d0 + r] = vals2[i];
+    if (r < lim) {  // keep / keep2 drop a segment tag (compact_regions)
+      out[d0 + r] = EXPAND ? runs_expand(vals[i], runs) : vals[i] & keep;
+      if (out2) out2[d0 + r] = vals2[i] & keep2;
     }
   }
 }
@@ -221,6 +226,13 @@ __global__ void k_interleave(const uint64_t* __restrict__ lo, const uint64_t* __
     out[2 * i] = lo[i];
     out[2 * i + 1] = hi[i];
   }
+}
+
+__global__ void k_seg_ids(uint64_t* __restrict__ out, const uint64_t* __restrict__ off) {
+  const uint32_t g = blockIdx.y;
+  const uint64_t b = off[g], len = off[g + 1] - b;
+  for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < len; i += (uint64_t)gridDim.x * kB)
+    out[b + i] = g;
 }
 
 __global__ void k_iota(uint64_t* __restrict__ out, uint64_t n) {
@@ -801,15 +813,27 @@ hipError_t seg_sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const uin
 
 hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d_src_off,
                            const uint64_t* d_dst_off, uint32_t n_seg, uint64_t max_len,
-                           hipStream_t s, const BitRuns* pack) {
+                           hipStream_t s, const BitRuns* pack, int tag_shift) {
   if (n_seg == 0 || max_len == 0) return hipSuccess;
   if (pack && pack->n)
     hipLaunchKernelGGL(k_compact<true>, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, src, dst,
-                       d_src_off, d_dst_off, *pack);
+                       d_src_off, d_dst_off, *pack, tag_shift);
   else
     hipLaunchKernelGGL(k_compact<false>, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, src, dst,
-                       d_src_off, d_dst_off, BitRuns{});
+                       d_src_off, d_dst_off, BitRuns{}, tag_shift);
   return hipGetLastError();
+}
+
+hipError_t launch_seg_ids(uint64_t* out, const uint64_t* d_off, uint32_t n_seg, uint64_t max_len, hipStream_t s) {
+  if (n_seg == 0 || max_len == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_seg_ids, dim3(grid_for(max_len), n_seg), dim3(kB), 0, s, out, d_off);
+  return hipGetLastError();
+}
+
+int seg_tag_bits(uint32_t n_seg) {
+  int b = 0;
+  while (b < 32 && (1ull << b) < n_seg) ++b;
+  return b;
 }
 
 BitRuns bit_runs(uint64_t mask) {
@@ -866,15 +890,15 @@ hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint6
                               const uint32_t* d_flag,
                               const uint64_t* d_pos, const uint64_t* d_limit,
                               const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
-                              hipStream_t s, const BitRuns* expand) {
+                              hipStream_t s, const BitRuns* expand, uint64_t keep, uint64_t keep2) {
   if (n_seg == 0 || total == 0) return hipSuccess;
   const dim3 grid(grid_for(std::min<uint64_t>(max_len, 1ull << 24)), n_seg);
   if (expand && expand->n)
     hipLaunchKernelGGL(k_scatter<true>, grid, dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos,
-                       d_limit, d_dst_off, out, out2, *expand);
+                       d_limit, d_dst_off, out, out2, *expand, keep, keep2);
   else
     hipLaunchKernelGGL(k_scatter<false>, grid, dim3(kB), 0, s, vals, vals2, d_off, d_flag, d_pos,
-                       d_limit, d_dst_off, out, out2, BitRuns{});
+                       d_limit, d_dst_off, out, out2, BitRuns{}, keep, keep2);
   return hipGetLastError();
 }
 

@@ -118,10 +118,21 @@ hipError_t launch_bottom_fused(uint64_t* rec, const uint64_t* d_src_off, const u
                                uint32_t* set_sizes = nullptr, uint64_t* set_starts = nullptr);
 
 // Compact sparse survivor regions [off[g], off[g] + cnt[g]) into dense CSR,
-// packing each value's mask bits when `pack` is given.
+// packing each value's mask bits when `pack` is given.  tag_shift >= 0 ORs the
+// segment index in above the key bits, (g << tag_shift) | key: the segments of a
+// many-genome build then sort as ONE device-wide radix sort over
+// tag_shift + seg_tag_bits(n_seg) bits (each segment keeps its CSR range, as the
+// counts per tag are the segment sizes) instead of a segmented sort, whose one
+// workgroup per segment left most of the chip idle (64 genomes of 25k keys:
+// 0.5 ms per sort).  The tag is dropped on output (seg_unique_scatter's keep
+// masks; runs_expand keeps only the packed width).
 hipError_t compact_regions(const uint64_t* src, uint64_t* dst, const uint64_t* d_src_off,
                            const uint64_t* d_dst_off, uint32_t n_seg, uint64_t max_len,
-                           hipStream_t s, const BitRuns* pack = nullptr);
+                           hipStream_t s, const BitRuns* pack = nullptr, int tag_shift = -1);
+int seg_tag_bits(uint32_t n_seg);  // ceil(log2(n_seg))
+// out[off[g] .. off[g+1]) = g: the segment of every element (a segment tag
+// that does not fit above the key rides as a sort value instead)
+hipError_t launch_seg_ids(uint64_t* out, const uint64_t* d_off, uint32_t n_seg, uint64_t max_len, hipStream_t s);
 
 // Per-segment unique of sorted keys (optionally by a (key, key2) pair):
 // writes d_flag_pos (exclusive scan of "first of run" flags) and per-segment
@@ -144,7 +155,14 @@ hipError_t seg_unique_scatter(const uint64_t* vals, const uint64_t* vals2, uint6
                               const uint32_t* d_flag,
                               const uint64_t* d_pos, const uint64_t* d_limit,
                               const uint64_t* d_dst_off, uint64_t* out, uint64_t* out2,
-                              hipStream_t s, const BitRuns* expand = nullptr);
+                              hipStream_t s, const BitRuns* expand = nullptr, uint64_t keep = ~0ull,
+                              uint64_t keep2 = ~0ull);
+
+// Every window of a piece dense by start (windows.hip): rows[i] = {kmer_bits
+// lo, hi, masked lo(, masked hi for w > 32)} of the window starting at
+// first + i, valid[i / 64] bit i % 64 set when that window is all ACGT.
+hipError_t launch_windows_dense(const uint8_t* seq, uint64_t n_bytes, uint64_t first, uint64_t n_win, int w,
+                                uint64_t m_lo, uint64_t m_hi, uint64_t* rows, uint64_t* valid, hipStream_t s);
 
 // ---- intersection (intersect.hip) ---------------------------------------------------
 hipError_t launch_intersect_pairs(const uint64_t* data, const uint64_t* starts,

@@ -670,7 +670,9 @@ class GpuJoinOps:
         return 0
 
     def stats_since(self, mark):
-        return self.stats[mark:self.n_stats]
+        """The call's status rows as a copy (queued on torch's stream), so a later
+        call reusing the log's rows cannot change an earlier JoinResult's view."""
+        return self.stats[mark:self.n_stats].clone()
 
     def parts(self, T, device, zeroed=True):
         """Packed count tiles [T, 64, 64], zeroed unless the kernels clear them."""

@@ -20,6 +20,10 @@ FLAVOUR_BOOST_MIX = 0
 FLAVOUR_BOOST_LEGACY = 1
 
 
+# sks_status (include/sks.h)
+SKS_OK, SKS_E_ARG, SKS_E_HIP, SKS_E_IO, SKS_E_NOMEM, SKS_E_UNSUPPORTED, SKS_E_LENGTH = range(7)
+
+
 class SksError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"sks error {code}: {msg}")
@@ -65,7 +69,7 @@ EXPORTED = [
     "sks_ctx_set_join_check", "sks_ctx_join_check_violations", "sks_intersect_layout_pair_tiles",
     "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_rows", "sks_ani_tiles",
     "sks_intersect_layout_ani", "sks_host_alloc", "sks_host_free", "sks_join_layout_stat_copy",
-    "sks_sketches_export", "sks_all_pairs_ani",
+    "sks_sketches_export", "sks_all_pairs_ani", "sks_windows_dense", "sks_windows_dense_row_words",
 ]
 
 _lib = None
@@ -166,6 +170,8 @@ def lib():
     L.sks_sketch_set_concat.argtypes = [vp, vp, C.c_uint32, C.POINTER(vp)]
     L.sks_kmer_list_build.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_int, u64p,
                                       C.POINTER(Policy), C.POINTER(vp)]
+    L.sks_windows_dense.argtypes = [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, u64p, vp, vp]
+    L.sks_windows_dense_row_words.argtypes = [C.c_int]
     L.sks_kmer_list_free.argtypes = [vp]
     L.sks_kmer_list_total.argtypes = [vp]
     L.sks_kmer_list_total.restype = C.c_uint64
@@ -557,6 +563,13 @@ class Context:
         finally:
             lib().sks_kmer_list_free(h)
         return pos[:n], bits[:4 * n].reshape(n, 4), counts[:len(seg) - 1]
+
+    def windows_dense(self, d_seq_ptr, n_bytes, first, n_windows, window, mask, d_rows, d_valid):
+        """sks_windows_dense (device pointers; queued on the context stream): every
+        window starting in [first, first + n_windows) of the piece, dense by start."""
+        check(lib().sks_windows_dense(self.h, C.c_void_p(d_seq_ptr), C.c_uint64(n_bytes), C.c_uint64(first),
+                                      C.c_uint64(n_windows), window, _mask_arr(mask), C.c_void_p(d_rows),
+                                      C.c_void_p(d_valid)))
 
     def load_sketches(self, path):
         h = C.c_void_p()

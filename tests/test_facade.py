@@ -129,14 +129,18 @@ def _odd_rule(lo):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,k,c", [(31, 21, 200), (21, 21, 50), (40, 30, 20)])
-def test_reference_shaped_caller_std_function(tmp_path, w, k, c):
+@pytest.mark.parametrize("w,k,c,piece", [(31, 21, 200, 0), (21, 21, 50, 0), (40, 30, 20, 0), (31, 21, 200, 997),
+                                         (64, 40, 20, 1500)])
+def test_reference_shaped_caller_std_function(tmp_path, w, k, c, piece):
     """tests/cpp/ref_caller.cpp uses only the reference's API names and passes
     std::function predicates (a free function like kmer-sketching.cpp:29-34 and
     lambdas) to the builders, as kmer-sketching.cpp:151-212 does.  Sets, pair
     counts and ANI equal the oracle's; the predicate runs once per window; a
     rule no sketch descriptor can express selects exactly the oracle's windows;
-    kmer_hashes iterates the set; k-mers of two masks in one set count per mask."""
+    kmer_hashes iterates the set; k-mers of two masks in one set count per mask.
+    piece > 0 cuts every stream into pieces of that many window starts
+    (SKS_FACADE_PIECE): windows whose F register carries run history from
+    before a cut keep it (the 64 bytes handed over in front of each piece)."""
     build_facade_test()
     files = []
     for i in range(3):
@@ -145,8 +149,11 @@ def test_reference_shaped_caller_std_function(tmp_path, w, k, c):
         p = tmp_path / f"r{i}.fa"
         p.write_bytes(synth.fasta_text([(f"r{i}_a", g[:11000]), (f"r{i}_b", g[11000:])], width=61))
         files.append(str(p))
+    env = dict(os.environ)
+    if piece:
+        env["SKS_FACADE_PIECE"] = str(piece)
     r = subprocess.run([REF_CALLER, str(w), str(k), str(c)] + files, capture_output=True, text=True,
-                       timeout=600)
+                       timeout=600, env=env)
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     m = O.mask(w, k, 0)

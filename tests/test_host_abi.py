@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert len(syms) >= 35
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/sks.h but not exported"
-    assert lib.sks_abi_version() == 2
+    assert lib.sks_abi_version() == 3
     for s in sksffi.EXPORTED:
         assert s in syms
 

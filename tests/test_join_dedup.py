@@ -344,3 +344,44 @@ def test_join_plane_carry_out(torch_cuda, ctx):
     ctx.intersect_sym(d.data_ptr(), st.data_ptr(), sz.data_ptr(), 1, n, 0, sksffi.intersect_sym_tiles(n), o.data_ptr())
     torch.cuda.synchronize()
     assert np.array_equal(o.cpu().numpy().reshape(n, n), want)
+
+
+def test_fused_ani_refuses_unmapped_host_memory(torch_cuda, ctx):
+    """The fused ANI store runs inside k_join, so its destination must be device
+    memory or pinned host memory mapped into the device.  An ordinary host
+    buffer (numpy) is refused with SKS_E_ARG by both entry points that take it
+    (sks_all_pairs_ani, sks_intersect_layout_ani) before any kernel runs, and the
+    context still works afterwards."""
+    import sks_dist
+    torch = torch_cuda
+    rng = np.random.default_rng(5)
+    sk = [np.unique(rng.integers(1, 2**40, size=300, dtype=np.uint64)) for _ in range(3)]
+    n = len(sk)
+    sizes = np.array([len(x) for x in sk], dtype=np.uint32)
+    starts = np.zeros(n, dtype=np.uint64)
+    starts[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    d = torch.from_numpy(np.concatenate(sk).view(np.int64)).to("cuda:0")
+    st = torch.from_numpy(starts.view(np.int64)).to("cuda:0")
+    sz = torch.from_numpy(sizes.view(np.int32)).to("cuda:0")
+    cnt = torch.zeros(64 * 64, dtype=torch.int32, device="cuda:0")
+    host = np.zeros(n * n, dtype=np.float64)  # plain pageable memory
+    with pytest.raises(sksffi.SksError) as e:
+        ctx.all_pairs_ani(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, int(sizes.max()), int(sizes.sum()), 21,
+                          host.ctypes.data, cnt.data_ptr(), 0)
+    assert e.value.code == sksffi.SKS_E_ARG
+    log_b = sksffi.join_layout_log_b(int(sizes.max()))
+    ops = sks_dist.GpuJoinOps(ctx)
+    lay = ops.build(sks_dist.Sketches(d, sz, 1, starts=st), log_b, None, "refuse")
+    with pytest.raises(sksffi.SksError) as e:
+        ctx.intersect_layout_ani(n, log_b, [t.data_ptr() for t in lay], 0, [t.data_ptr() for t in lay], 0, 0, 0,
+                                 sksffi.intersect_sym_tiles(n), True, cnt.data_ptr(), sz.data_ptr(), 21,
+                                 host.ctypes.data)
+    assert e.value.code == sksffi.SKS_E_ARG
+    # device memory is accepted and the counts are right
+    ani = torch.zeros(n * n, dtype=torch.float64, device="cuda:0")
+    ctx.all_pairs_ani(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, int(sizes.max()), int(sizes.sum()), 21,
+                      ani.data_ptr(), cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = cnt.cpu().numpy().reshape(64, 64)[:n, :n]
+    want = np.array([[np.intersect1d(sk[i], sk[j]).size for j in range(n)] for i in range(n)])
+    assert np.array_equal(got, want)

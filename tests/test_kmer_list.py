@@ -136,3 +136,51 @@ def test_facade_nucleotide_string_list_to_kmers(tmp_path):
         rows = O.kmer_list(O.fasta_runs(str(path)), w, O.mask(w, k, 0), c)
         want = [(int(a) | int(b) << 64, int(cc) | int(d) << 64) for a, b, cc, d in rows[:, :4]]
         assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,k", [(5, 5), (21, 21), (31, 21), (32, 32), (33, 25), (45, 30), (64, 40)])
+def test_windows_dense_matches_oracle(gpu, w, k):
+    """sks_windows_dense (every window, dense by start, for a host predicate)
+    against the oracle's every-window list (c = 1): the validity bits are set
+    exactly at the oracle's window starts and each row holds that window's
+    kmer_bits (with the 128-bit F history) and masked bits.  Done over the whole
+    stream and again as pieces cut at odd offsets, each given
+    min(start, 64 - w) bytes of history, as the facade's for_each_window does."""
+    torch, ctx = gpu
+    genomes = [_genome(7000, 20 + i, n_runs=i + 1) for i in range(3)] + [_genome(25, 98, 0)]
+    stream = b"".join(g.tobytes() + b"\n" for g in genomes)
+    n = len(stream)
+    m = O.mask(w, k, 2)
+    wpos, wbits, _ = expected(stream, [0, n], w, m, 1)
+    words = 3 if w <= 32 else 4
+    d = torch.frombuffer(bytearray(stream), dtype=torch.uint8).to("cuda:0")
+
+    def dense(a, b):  # window starts [a, b)
+        h = min(a, 64 - w)
+        lo, hi = a - h, min(n, b + w - 1)
+        nw = b - a
+        rows = torch.zeros(max(nw, 1) * words, dtype=torch.int64, device="cuda:0")
+        valid = torch.zeros(max((nw + 63) // 64, 1), dtype=torch.int64, device="cuda:0")
+        ctx.windows_dense(d.data_ptr() + lo, hi - lo, h, nw, w, m, rows.data_ptr(), valid.data_ptr())
+        torch.cuda.synchronize()
+        v = valid.cpu().numpy().view(np.uint64)
+        bits = np.unpackbits(v.view(np.uint8), bitorder="little")[:nw].astype(bool)
+        return bits, rows.cpu().numpy().view(np.uint64).reshape(-1, words)[:nw]
+
+    for cuts in ([0, n - w + 1], [0, 4099, 9000, 13333, n - w + 1]):
+        got_pos, got_rows = [], []
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            ok, rows = dense(a, b)
+            idx = np.nonzero(ok)[0]
+            got_pos.append(idx.astype(np.uint64) + np.uint64(a))
+            got_rows.append(rows[idx])
+        gp = np.concatenate(got_pos)
+        gr = np.concatenate(got_rows)
+        assert np.array_equal(gp, wpos)
+        assert np.array_equal(gr[:, 0], wbits[:, 0]) and np.array_equal(gr[:, 1], wbits[:, 1])
+        assert np.array_equal(gr[:, 2], wbits[:, 2])
+        if words == 4:
+            assert np.array_equal(gr[:, 3], wbits[:, 3])
+        else:
+            assert not wbits[:, 3].any()

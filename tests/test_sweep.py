@@ -116,3 +116,25 @@ def test_driver_missing_file_exits_like_reference(tmp_path):
                        timeout=60)
     assert r.returncode == 1
     assert r.stderr.startswith(f"Unable to open {missing}. \n Exiting...")
+
+
+@pytest.mark.gpu
+def test_driver_sweep_many_files_matches_oracle_csv(tmp_path):
+    """67 files (two 64-sketch blocks, the second ragged) through the drop-in
+    driver's all-pairs step — one sks_all_pairs_ani call per configuration, the
+    ANI written by the join into pinned host memory — including a file with no
+    ACGT runs (header only), an all-N record and a record shorter than most
+    windows (empty or tiny sketches: containment 0 -> ANI 0,
+    ani_estimation.cpp:24-42).  The CSV equals the oracle's rendering of the
+    reference writer byte for byte (kmer-sketching.cpp:46-81, 151-212)."""
+    files = _genome_files(tmp_path, n=64, length=6000)
+    extra = [("empty.fa", b">nothing here\n"), ("alln.fa", b">n\n" + b"N" * 500 + b"\n"),
+             ("tiny.fa", b">t\nACGTACGTTGCAACGTTAGCCA\n")]
+    for name, body in extra:
+        p = tmp_path / name
+        p.write_bytes(body)
+        files.append(str(p))
+    out = tmp_path / "ani.csv"
+    r = subprocess.run([DRIVER, str(out)] + files, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    assert out.read_text() == oracle_sweep_csv(files)
