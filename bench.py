@@ -977,7 +977,11 @@ def run_ref_sweep(ctx, cpu=False):
                     "compare_pairs_per_s": len(ix) * n * n / (c * 1e-3)}
         res = {"metric": "reference sweep (kmer-sketching main), 62 (w, k) configs",
                "genomes": n, "genome_len": C4_LEN, "pairs_per_config": n * n,
-               "driver": "spaced-kmer-sketching_amd/bin/kmer-sketching (the reference main on the facade)",
+               "driver": "spaced-kmer-sketching_amd/bin/kmer-sketching: this engine's restatement of the reference "
+                         "main (apps/kmer_sketching.cpp + cpp/sweep.cpp) - files parsed once and kept in HBM, the "
+                         "sketch step with the FracMinHash descriptor on the device (not the reference's "
+                         "std::function predicate: that flow is dropin_std_function), all pairs + ANI in one fused "
+                         "native call",
                "wall_s": wall, "csv_rows": rows,
                "sketch_ms_total": sum(sk), "compare_ms_total": sum(cp),
                "w_le_32": part(narrow), "w_gt_32": part(wide),
@@ -985,6 +989,7 @@ def run_ref_sweep(ctx, cpu=False):
                        "lines (kmer-sketching.cpp:174-175, 202-203 on the same boundaries); the files are parsed "
                        "once, on the device, before the first configuration (the reference re-parses them per "
                        "configuration); wall_s includes process start, that parse and the CSV writing"}
+        res["dropin_std_function"] = run_dropin_flow(files)
         if cpu:
             csel = REF_SWEEP_CPU_CONFIGS
             cres, T = cpu_ref_sweep(files[:REF_SWEEP_CPU_GENOMES], csel)
@@ -1024,6 +1029,11 @@ def run_ref_sweep(ctx, cpu=False):
                 ks = statistics.mean(x["cpu_sketch_kmers_per_s"] for x in xs)
                 ps = statistics.mean(x["cpu_compare_pairs_per_s"] for x in xs)
                 proj += wins[i] / ks + n * n / ps
+            for x in res["dropin_std_function"]["per_config"]:
+                c = next((y for y in per if (y["w"], y["k"]) == (x["w"], x["k"])), None)
+                if c is not None:  # the reference-style host flow at this file count, from its sampled rate
+                    x["cpu_port_sketch_ms_64_files"] = x["windows"] / c["cpu_sketch_kmers_per_s"] * 1e3
+                    x["speedup_vs_cpu_port"] = x["cpu_port_sketch_ms_64_files"] / x["std_function_ms"]
             res["cpu_baseline"] = {
                 "kind": "port", "cores": T,
                 "sample": f"the first {g} of the {n} files, configurations {list(csel)}: per configuration every file "
@@ -1037,6 +1047,41 @@ def run_ref_sweep(ctx, cpu=False):
     finally:
         import shutil
         shutil.rmtree(d, ignore_errors=True)
+
+
+def run_dropin_flow(files):
+    """The reference driver's sketching step as an UNMODIFIED caller runs it
+    (kmer-sketching.cpp:165-175): parallel_kmer_sets_from_fasta_files with the
+    reference's global-function predicate sketching_condition (:29-34) as a
+    std::function — the GPU extracts every window (sks_windows_dense), the
+    predicate runs on host threads, one pooled device worker per thread with
+    pinned double buffers — beside the same call with the device-side
+    descriptor (sketch_policy::frac(200)); bin/dropin-flow asserts the sets are
+    equal.  Per configuration: both times, the window rows' device-to-host
+    bytes, their copy time and effective rate, the host predicate time, and
+    which of the two bounds the flow."""
+    import subprocess
+    exe = os.path.join(PKG, "bin", "dropin-flow")
+    cfg = ",".join(f"{w}:{k}" for w, k in REF_SWEEP_CPU_CONFIGS)
+    p = subprocess.run([exe, cfg] + list(files), capture_output=True, text=True, timeout=900)
+    if p.returncode != 0:
+        raise RuntimeError(f"bin/dropin-flow failed ({p.returncode}): {p.stderr[-2000:]}")
+    per = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    for x in per:
+        thr = max(1, x["threads"])
+        x["d2h_GBps_effective"] = x["d2h_bytes"] / (x["std_function_ms"] * 1e-3) / 1e9
+        x["d2h_GBps_copy"] = x["d2h_bytes"] / (x["d2h_ms_sum"] * 1e-3) / 1e9 * thr if x["d2h_ms_sum"] else None
+        x["predicate_ms_per_thread"] = x["predicate_ms_sum"] / thr
+        x["predicate_ns_per_window"] = x["predicate_ms_sum"] * 1e6 / max(1, x["windows"])
+        x["bound"] = ("host predicate" if x["predicate_ms_per_thread"] >= 0.75 * x["std_function_ms"]
+                      else "device / PCIe")
+        assert x["sets_equal"]
+    return {"driver": "spaced-kmer-sketching_amd/bin/dropin-flow (apps/dropin_flow.cpp: the reference's "
+                      "sketching_condition passed to parallel_kmer_sets_from_fasta_files unchanged)",
+            "files": len(files), "per_config": per,
+            "note": "std_function_ms: wall time of the unmodified call; descriptor_ms: the same call with "
+                    "sketch_policy::frac(200) (selection on the GPU); d2h_GBps_copy: bytes over the summed "
+                    "per-worker copy durations (HIP events) x threads, i.e. the rate while copies run"}
 
 
 # ---- config 5 ------------------------------------------------------------------------

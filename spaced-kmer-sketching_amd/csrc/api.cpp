@@ -1027,7 +1027,7 @@ int post_process(BuildState& S, const std::vector<uint32_t>& seg_ids,
 // given word offsets (survivor / window counters zeroed there).
 sks::ScanParams scan_params(const BuildState& S, const uint8_t* d_seq, const MetaArena& arena, size_t o_beg,
                             size_t o_end, size_t o_tp, size_t o_thr, size_t o_cap, size_t o_off, size_t o_cnt,
-                            size_t o_win, uint32_t m, uint64_t n_tiles) {
+                            size_t o_win, uint32_t m, uint64_t n_tiles, size_t o_queue) {
   sks_ctx* c = S.c;
   sks::ScanParams p{};
   p.seq = d_seq;
@@ -1052,6 +1052,8 @@ sks::ScanParams scan_params(const BuildState& S, const uint8_t* d_seq, const Met
   p.seg_out_cap = arena.ptr(o_cap);
   p.seg_count = reinterpret_cast<unsigned long long*>(arena.ptr(o_cnt));
   p.seg_windows = reinterpret_cast<unsigned long long*>(arena.ptr(o_win));
+  static const bool static_tiles = getenv("SKS_SCAN_STATIC") != nullptr;
+  p.tile_queue = static_tiles ? nullptr : reinterpret_cast<unsigned long long*>(arena.ptr(o_queue));
   return p;
 }
 
@@ -1078,7 +1080,8 @@ int build_bottom_single(BuildState& S, const uint8_t* d_seq, const uint64_t* seg
   const size_t o_beg = arena.add({seg_off[0]}), o_end = arena.add({seg_off[1]}), o_tp = arena.add({0, n_tiles}),
                o_thr = arena.add({thresh}), o_cap = arena.add({cap}), o_off = arena.add({0}),
                o_retry = arena.add({thresh != ~0ull ? 1ull : 0ull}), o_dst = arena.add({0, slots}),
-               o_cnt = arena.add_zero(1), o_win = arena.add_zero(1), o_res = arena.add_zero(1);
+               o_cnt = arena.add_zero(1), o_win = arena.add_zero(1), o_res = arena.add_zero(1),
+               o_queue = arena.add_zero(1);
   if (o_win != o_cnt + 2 || o_res != o_win + 2) return sks::fail(SKS_E_HIP, "sks_sketch_build: arena layout");
   SKS_TRY(arena.upload());
   sks_sketch_set* set = new (std::nothrow) sks_sketch_set();
@@ -1100,7 +1103,7 @@ int build_bottom_single(BuildState& S, const uint8_t* d_seq, const uint64_t* seg
     return rc;
   }
   const sks::ScanParams p =
-      scan_params(S, d_seq, arena, o_beg, o_end, o_tp, o_thr, o_cap, o_off, o_cnt, o_win, 1, n_tiles);
+      scan_params(S, d_seq, arena, o_beg, o_end, o_tp, o_thr, o_cap, o_off, o_cnt, o_win, 1, n_tiles, o_queue);
   const sks::BitRuns runs = sks::bit_runs(S.mask_lo);
   const int kb = std::max(1, __builtin_popcountll(S.mask_lo));
   hipError_t e = hipEventRecord(c->ev_s0, st);
@@ -1266,11 +1269,11 @@ int sks_sketch_build(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, const u
     MetaArena arena(c);
     size_t o_beg = arena.add(beg), o_end = arena.add(end), o_tp = arena.add(tp),
            o_thr = arena.add(thr), o_cap = arena.add(cap), o_off = arena.add(ooff),
-           o_cnt = arena.add_zero(m), o_win = arena.add_zero(m);
+           o_cnt = arena.add_zero(m), o_win = arena.add_zero(m), o_queue = arena.add_zero(1);
     SKS_TRY(arena.upload());
 
-    const sks::ScanParams p =
-        scan_params(S, d_seq, arena, o_beg, o_end, o_tp, o_thr, o_cap, o_off, o_cnt, o_win, m, n_tiles);
+    const sks::ScanParams p = scan_params(S, d_seq, arena, o_beg, o_end, o_tp, o_thr, o_cap, o_off, o_cnt, o_win,
+                                          m, n_tiles, o_queue);
 
     SKS_HIP(hipEventRecord(c->ev_s0, st));
     SKS_HIP(sks::launch_scan(p, bottom ? sks::kModeBottom : sks::kModeFrac, policy->flavour,

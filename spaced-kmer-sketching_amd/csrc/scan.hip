@@ -282,14 +282,31 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
   // (z, c) of windows past the low-bits pre-filter, per wave (PRE only)
   __shared__ ulonglong2 s_cand[PRE ? (kBlock / 64) * kCandCap : 1];
 
+  __shared__ unsigned long long s_next;  // dynamic tiles: the next chunk's first tile
+
   const int tid = threadIdx.x;
-  const uint64_t t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
-  const uint64_t t_end = (uint64_t)(blockIdx.x + 1) * p.n_tiles / gridDim.x;
+  // Tiles: static — workgroup b streams the contiguous range b·T/grid ..; or
+  // dynamic (p.tile_queue) — a persistent grid whose workgroups take chunks of
+  // p.chunk consecutive tiles, the first one b·chunk, the rest from one global
+  // counter, so no workgroup is left with a range when the others are done
+  // (a static range's tail is up to one range: ~1/16 of the kernel).  A chunk's
+  // grab is issued by thread 0 at its first tile and published through LDS at
+  // its last, so the atomic's latency hides behind the chunk's tiles.
+  const bool dyn = p.tile_queue != nullptr;
+  uint64_t t_begin, t_end;
+  if (dyn) {
+    t_begin = (uint64_t)blockIdx.x * p.chunk;
+    t_end = min(t_begin + p.chunk, p.n_tiles);
+  } else {
+    t_begin = (uint64_t)blockIdx.x * p.n_tiles / gridDim.x;
+    t_end = (uint64_t)(blockIdx.x + 1) * p.n_tiles / gridDim.x;
+  }
   if (tid == 0) {
     q.n = 0;
     q.wins = 0;
   }
   if (t_begin >= t_end) return;
+  unsigned long long grab = 0;  // thread 0: the pending chunk grab
 
   const int w = p.w;
   // F of the window at base b is read as the 64 big-endian bits starting at
@@ -320,7 +337,7 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
   uint32_t win_count = 0;
   uint32_t count_seg = cur_seg;
 
-  for (uint64_t tile = t_begin; tile < t_end; ++tile) {
+  for (uint64_t tile = t_begin; tile < t_end;) {
     Geom g = tile_geom(p, tile, cur_seg);
     if (g.seg != count_seg) {  // segment change: publish the previous segment
       add_windows(q.wins, win_count);
@@ -330,11 +347,20 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
     }
     const uint32_t shift = align_shift(p.seq, g.win0);
     const uint64_t thresh = (MODE == kModeBottom) ? p.seg_thresh[g.seg] : 0;
+    const bool last_of_chunk = tile + 1 == t_end;
+    if (dyn && tid == 0) {
+      if (tile == t_begin)
+        grab = (unsigned long long)gridDim.x * p.chunk + atomicAdd(p.tile_queue, (unsigned long long)p.chunk);
+      if (last_of_chunk) s_next = grab;
+    }
 
     // 1) raw bytes -> LDS
     reinterpret_cast<uint4*>(s_raw)[tid] = v0;
     if (tid < kLoadVecs - kBlock) reinterpret_cast<uint4*>(s_raw)[kBlock + tid] = v1;
     __syncthreads();
+    // the next tile: the chunk's next, else the next chunk's first (read here,
+    // after the barrier; s_next is rewritten only at the next chunk's last tile)
+    const uint64_t next_tile = !last_of_chunk ? tile + 1 : dyn ? (uint64_t)s_next : p.n_tiles;
 
     // 2) pack: word i covers bases [16 i, 16 i + 16) of the tile
     {
@@ -358,8 +384,8 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
     __syncthreads();
 
     // 3) prefetch the next tile while this one is hashed
-    if (tile + 1 < t_end) {
-      Geom ng = tile_geom(p, tile + 1, pf_seg);
+    if (next_tile < (dyn ? p.n_tiles : t_end)) {
+      Geom ng = tile_geom(p, next_tile, pf_seg);
       pf_base = (int64_t)ng.win0 - align_shift(p.seq, ng.win0);
       v0 = load_vec(p.seq, pf_base, tid, (int64_t)ng.seg_end);
       if (tid < kLoadVecs - kBlock) v1 = load_vec(p.seq, pf_base, kBlock + tid, (int64_t)ng.seg_end);
@@ -508,6 +534,14 @@ __global__ __launch_bounds__(kBlock, SKS_SCAN_MIN_WAVES) void scan_kernel(ScanPa
       add_windows(q.wins, win_count);
       win_count = 0;
       flush<MODE>(p, q, g.seg);
+    }
+    if (!last_of_chunk) {
+      ++tile;
+    } else if (dyn) {  // next chunk (every thread holds the same next_tile): exits past n_tiles
+      t_begin = tile = next_tile;
+      t_end = min(next_tile + p.chunk, p.n_tiles);
+    } else {
+      break;
     }
   }
   add_windows(q.wins, win_count);
@@ -681,6 +715,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel_wide(ScanParams p) {
 }
 
 constexpr int kGridOversubscribe = 16;
+constexpr int kDynOversubscribe = 2;
 
 template <class K>
 int occupancy_grid(K kernel, int device) {
@@ -708,11 +743,37 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
     // 5.95 ms at 1x, 5.19 ms at 8x-16x before the pre-filter; with it 4.7 ms at
     // 8x and 16x (equal within noise in full benches), 5.6 ms at 32x and 9.2 at
     // 64x (per-workgroup start-up and flush costs).
+    ScanParams q = p;
+    q.tile_queue = nullptr;  // static tile ranges
     int grid = grid_override > 0 ? grid_override : kGridOversubscribe * occupancy_grid(kernel, device);
     if ((uint64_t)grid > p.n_tiles) grid = (int)p.n_tiles;
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, p);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, q);
     return hipGetLastError();
   };
+  // dynamic tiles (narrow kernels, p.tile_queue set): twice the resident
+  // workgroups (every slot filled even if the occupancy query is conservative),
+  // chunks of ~T / (16 grid) tiles, 2..16: the tail is at most one chunk, and
+  // the counter takes <= ~1 grab per 16 tiles (config 3: ~21 per microsecond,
+  // below the ~88 one word serves, MI355X_MICROARCH.md)
+  auto pick_dyn = [&](auto kernel) -> hipError_t {
+    ScanParams q = p;
+    int grid = grid_override > 0 ? grid_override : kDynOversubscribe * occupancy_grid(kernel, device);
+    const uint64_t per = p.n_tiles / ((uint64_t)grid * 16);
+    q.chunk = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(2, per));
+    const uint64_t need = (p.n_tiles + q.chunk - 1) / q.chunk;
+    if ((uint64_t)grid > need) grid = (int)need;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, q);
+    return hipGetLastError();
+  };
+  if (!wide && p.tile_queue) {
+    if (mode == kModeFrac) {
+      static const bool no_pre = getenv("SKS_NO_PREFILTER") != nullptr;
+      if (flavour == 0 && (p.low_mask & 0xFu) && !no_pre) return pick_dyn(scan_kernel<kModeFrac, 0, 1>);
+      return flavour == 0 ? pick_dyn(scan_kernel<kModeFrac, 0>) : pick_dyn(scan_kernel<kModeFrac, 1>);
+    }
+    if (mode == kModeBottom)
+      return flavour == 0 ? pick_dyn(scan_kernel<kModeBottom, 0>) : pick_dyn(scan_kernel<kModeBottom, 1>);
+  }
   if (!wide) {
     if (mode == kModeFrac) {
       static const bool no_pre = getenv("SKS_NO_PREFILTER") != nullptr;

@@ -56,6 +56,10 @@ struct ScanParams {
   const uint64_t* seg_out_cap;  // [n_seg] record capacity
   unsigned long long* seg_count;    // [n_seg] records emitted (may exceed capacity)
   unsigned long long* seg_windows;  // [n_seg] valid windows hashed
+  // dynamic tile queue (narrow scan): a zeroed counter, or null for static
+  // per-workgroup tile ranges; `chunk` (set by launch_scan) tiles per grab
+  unsigned long long* tile_queue;
+  uint32_t chunk;
 };
 
 uint64_t scan_tiles_for(uint64_t seg_bytes);
