@@ -761,7 +761,8 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
                                         ani_ones=ones if with_ani else None,
                                         ani_out=host_ani if with_ani else None,
                                         max_size=int(ss.sizes().max()) if ss is not None and ss.n else None,
-                                        size_bound=C4_S, exchange=EXCHANGE, world1_exchange=WORLD1_EXCHANGE)
+                                        size_bound=C4_S, exchange=EXCHANGE, world1_exchange=WORLD1_EXCHANGE,
+                                        bounds_mask=mask)
 
     t_sketch = t_pairs = t_counts = 0.0
     timed = 0
@@ -862,8 +863,9 @@ def run_pairs(ctx, world, rank, mask, steps, warmup, cpu_pairs=False, w=W):
                                     "blocks' 64x64 join tiles, then every tile pairing its blocks with "
                                     "ranks r+1 .. r+N/2 (the N/2 pairs split) as their sketches land",
                    "ani": "written by the join (last workgroup of each tile) into pinned host memory",
-                   "collective": (f"broadcast of rank 0's group bounds + sketch exchange '{EXCHANGE}' of "
-                                  f"sketches padded to s ({backend_label()})" if collective() else "none")},
+                   "collective": (f"sketch exchange '{EXCHANGE}' of sketches padded to s ({backend_label()}); "
+                                  f"group bounds from the mask on every rank (no broadcast)"
+                                  if collective() else "none")},
         "cpu_baseline": cpu,
         "cpu_baseline_sketch_phase": cpu_sk,
         "end_to_end_pairs_per_s": C4_GENOMES * C4_GENOMES / (t_sketch + t_pairs),

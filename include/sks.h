@@ -308,6 +308,12 @@ uint32_t sks_join_layout_groups(uint32_t log_b);
  * ends + the region size word (the row's last word, log2 of the buckets per
  * region; added in ABI 3 — rows of ABI-2 layouts are one word shorter). */
 uint32_t sks_join_layout_boff_words(uint32_t log_b);
+/* Group bounds fixed by the mask alone (host array of (groups + 1) * elem_words
+ * words): the quantiles of min(F & M, R & M) for random sequence, so every rank
+ * of a multi-GPU all-vs-all uses the same bounds without sampling or
+ * exchanging anything.  Any bounds give exact counts; these balance groups for
+ * genome-like (near-uniform) k-mers. */
+int sks_join_layout_bounds_for_mask(const uint64_t mask[2], uint32_t log_b, int elem_words, uint64_t* bounds);
 /* Group bounds balanced for the set (quantiles averaged over up to 64 sample
  * sketches), queued on the context stream.  Any bounds give exact counts. */
 int sks_join_layout_bounds(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts,
@@ -414,6 +420,23 @@ int sks_sketches_export(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_
 int sks_all_pairs_ani(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
                       int elem_words, uint32_t n, uint32_t max_size, uint64_t total, int kmer_num_ones,
                       double* ani, int32_t* d_counts, uint32_t* d_status);
+/* One rank's step of a multi-GPU all-vs-all (sks_dist.all_vs_all_join) in one
+ * call: the join layout of the n sketches (context scratch; group bounds
+ * d_bounds, or sampled when NULL; blocks_hint as sks_ctx_set_layout_blocks_hint)
+ * whose block 0 is global block blk0, then the join of the n_tiles global
+ * (I, J) tiles of d_tiles (u32 pairs, both blocks in this set) into the packed
+ * d_counts[n_tiles][64][64], and — ani non-NULL — containment / ANI of both
+ * orientations written into the n_global x n_global matrix ani (device or
+ * mapped pinned host memory), with |S_g| = d_sizes_global[g] for global genome
+ * g.  The counts, the tiles' finisher counters and the two status words
+ * (d_status, as sks_join_layout_build's: max block bucket, invalid) are
+ * cleared by the build itself: four launches, no memset, no host sync.
+ * Replaces per tile kmer_set.cpp:23-41 over kmer_set.cpp:167-184's pairs. */
+int sks_layout_tiles_ani(sks_ctx* ctx, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
+                         int elem_words, uint32_t n, uint64_t total, uint32_t log_b, const uint64_t* d_bounds,
+                         uint32_t blocks_hint, uint32_t blk0, const uint32_t* d_tiles, uint64_t n_tiles,
+                         uint32_t n_global, const int32_t* d_sizes_global, int kmer_num_ones, double* ani,
+                         int32_t* d_counts, uint32_t* d_status);
 /* Pinned host memory the device reads and writes directly (mapped into every
  * device's address space): the destination of a fused ANI matrix.  coherent:
  * fine-grained (every device store goes to the host as issued); 0: coarse-

@@ -287,6 +287,8 @@ namespace {
 // Devices of the pair count in progress: empty = the facade's own context
 // (compute_pairwise_...), else the pool (parallel_compute_pairwise_...).
 thread_local std::vector<int> g_pair_devices;
+std::mutex g_pair_stats_mu;
+pair_flow_stats g_pair_stats{};
 struct PairDevices {  // scope of a parallel_ pair count (one device keeps the facade's context)
   std::vector<int> saved;
   explicit PairDevices(std::vector<int> d) : saved(std::move(g_pair_devices)) {
@@ -395,61 +397,120 @@ std::vector<int> pair_counts_single_mask(const std::vector<const kmer_set*>& a,
   // Pair lists that cover a large part of the n x n matrix — the reference's
   // main flow intersects generate_all_pairs_from_vector's list
   // (kmer-sketching.cpp:195-200) — are counted as the whole symmetric matrix by
-  // the join kernel (sks_intersect_sym) and gathered; sparse lists go through
-  // one wavefront per pair (sks_intersect_pairs).
+  // the join (one layout of all n sketches, its 64 x 64 upper-triangle tiles)
+  // and gathered; sparse lists go through one wavefront per pair
+  // (sks_intersect_pairs).
   const bool dense = n >= 64 && n <= 16384 && a.size() * 4 >= n * n;
   // parallel_* callers spread the work over the device pool (kmer_set.cpp:
-  // 167-184's cilk_for over pairs): every device holds all sketches and counts
-  // a contiguous share of the symmetric tiles (dense) or of the pair list
+  // 167-184's cilk_for over pairs): each pool entry counts a contiguous share
+  // of the tiles (dense) or of the pair list
   const std::vector<int> devs = g_pair_devices.empty() ? std::vector<int>{g_device} : g_pair_devices;
-  // (128-bit k-mers: row blocks of sks_intersect_all, as partial symmetric tile
-  // ranges take u64 sketches only)
-  const bool by_rows = dense && ew == 2 && devs.size() > 1;
-  const uint64_t units = !dense ? a.size() : by_rows ? n : sks_intersect_sym_tiles((uint32_t)n);
+  const uint64_t T = dense ? sks_intersect_sym_tiles((uint32_t)n) : 0;
+  const uint64_t units = dense ? T : a.size();
   const size_t parts = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(devs.size(), units));
-  std::vector<std::vector<int32_t>> mats(dense ? parts : 0);
+  // The sketches cross PCIe once, to the first pool device; every other device
+  // of the pool gets a device-to-device copy (xGMI peer copy between GPUs; a
+  // pool entry repeating a device shares its copy)
+  struct Resident {
+    int device;
+    std::unique_ptr<DevMem> words, starts, sizes;
+  };
+  std::vector<Resident> res_dev;
+  auto resident_on = [&](int device) -> const Resident& {
+    for (auto& r : res_dev)
+      if (r.device == device) return r;
+    Resident r{device, std::unique_ptr<DevMem>(new DevMem(words.size() * 8, device)),
+               std::unique_ptr<DevMem>(new DevMem(starts.size() * 8, device)),
+               std::unique_ptr<DevMem>(new DevMem(sizes.size() * 4, device))};
+    const uint64_t bytes = words.size() * 8 + starts.size() * 8 + sizes.size() * 4;
+    if (res_dev.empty()) {
+      check_hip(hipMemcpy(r.words->p, words.data(), words.size() * 8, hipMemcpyHostToDevice), "H2D");
+      check_hip(hipMemcpy(r.starts->p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice), "H2D");
+      check_hip(hipMemcpy(r.sizes->p, sizes.data(), sizes.size() * 4, hipMemcpyHostToDevice), "H2D");
+      std::lock_guard<std::mutex> lock(g_pair_stats_mu);
+      g_pair_stats.h2d_bytes += bytes;
+    } else {
+      const Resident& src = res_dev.front();
+      check_hip(hipMemcpyPeer(r.words->p, device, src.words->p, src.device, words.size() * 8), "D2D");
+      check_hip(hipMemcpyPeer(r.starts->p, device, src.starts->p, src.device, starts.size() * 8), "D2D");
+      check_hip(hipMemcpyPeer(r.sizes->p, device, src.sizes->p, src.device, sizes.size() * 4), "D2D");
+      std::lock_guard<std::mutex> lock(g_pair_stats_mu);
+      g_pair_stats.d2d_bytes += bytes;
+    }
+    res_dev.push_back(std::move(r));
+    return res_dev.back();
+  };
+  std::vector<const Resident*> on(parts);
+  for (size_t k = 0; k < parts; ++k) on[k] = &resident_on(devs[k]);  // before the pool threads start
+  std::vector<int32_t> mat(dense ? n * n : 0, 0);
+  std::mutex mat_mu;
   auto job = [&](size_t k, int device, sks_ctx* c) {
     const uint64_t u0 = units * k / parts, u1 = units * (k + 1) / parts;
-    DevMem d_words(words.size() * 8, device), d_starts(starts.size() * 8, device),
-        d_sizes(sizes.size() * 4, device);
-    check_hip(hipMemcpy(d_words.p, words.data(), words.size() * 8, hipMemcpyHostToDevice), "H2D");
-    check_hip(hipMemcpy(d_starts.p, starts.data(), starts.size() * 8, hipMemcpyHostToDevice), "H2D");
-    check_hip(hipMemcpy(d_sizes.p, sizes.data(), sizes.size() * 4, hipMemcpyHostToDevice), "H2D");
-    if (by_rows) {  // rows [u0, u1) of the n x n matrix, the rest 0
-      mats[k].assign(n * n, 0);
-      if (u1 > u0) {
-        DevMem d_rows((u1 - u0) * n * 4, device);
-        check(sks_intersect_all(c, d_words.as<uint64_t>(), d_starts.as<uint64_t>(), d_sizes.as<uint32_t>(),
-                                ew, (uint32_t)n, (uint32_t)u0, (uint32_t)u1, d_rows.as<int32_t>()));
-        check(sks_ctx_synchronize(c));
-        check_hip(hipMemcpy(mats[k].data() + u0 * n, d_rows.p, (u1 - u0) * n * 4, hipMemcpyDeviceToHost),
-                  "D2H");
-      }
-    } else if (dense) {
-      DevMem d_mat(n * n * 4, device);
-      check(sks_intersect_sym(c, d_words.as<uint64_t>(), d_starts.as<uint64_t>(), d_sizes.as<uint32_t>(),
-                              ew, (uint32_t)n, u0, u1, d_mat.as<int32_t>()));
+    if (u1 <= u0) return;
+    const Resident& R = *on[k];
+    const uint64_t* dw = R.words->as<uint64_t>();
+    const uint64_t* ds = R.starts->as<uint64_t>();
+    const uint32_t* dz = R.sizes->as<uint32_t>();
+    if (dense) {
+      // the layout of all n sketches, then this part's tiles [u0, u1), packed
+      // (16 KB a tile): only its own tiles come back
+      uint32_t max_size = 1;
+      for (uint32_t v : sizes) max_size = std::max(max_size, v);
+      const uint32_t log_b = sks_join_layout_log_b(max_size);
+      const uint64_t nb = (n + 63) / 64, tot = std::max<uint64_t>(total, 1);
+      DevMem vals(tot * 8 * ew, device), masks(tot * 8, device),
+          boff(nb * sks_join_layout_boff_words(log_b) * 4, device), bst((nb + 1) * 8, device);
+      uint32_t stat = 0;
+      check(sks_join_layout_build(c, dw, ds, dz, ew, (uint32_t)n, tot, log_b, nullptr, vals.as<uint64_t>(),
+                                  masks.as<uint64_t>(), boff.as<uint32_t>(), bst.as<uint64_t>(), &stat));
+      const uint64_t nt = u1 - u0;
+      DevMem tiles_out(nt * 4096 * 4, device);
+      check_hip(hipMemset(tiles_out.p, 0, nt * 4096 * 4), "hipMemset");  // the join adds into its tiles
+      check(sks_intersect_layout_tiles(c, (uint32_t)n, log_b, ew, vals.as<uint64_t>(), masks.as<uint64_t>(),
+                                       boff.as<uint32_t>(), bst.as<uint64_t>(), 0, nullptr, u0, u1, 1,
+                                       tiles_out.as<int32_t>()));
       check(sks_ctx_synchronize(c));
-      mats[k].resize(n * n);
-      check_hip(hipMemcpy(mats[k].data(), d_mat.p, n * n * 4, hipMemcpyDeviceToHost), "D2H");
-    } else if (u1 > u0) {
+      std::vector<int32_t> h(nt * 4096);
+      check_hip(hipMemcpy(h.data(), tiles_out.p, nt * 4096 * 4, hipMemcpyDeviceToHost), "D2H");
+      std::lock_guard<std::mutex> lock(mat_mu);
+      g_pair_stats.d2h_bytes += nt * 4096 * 4;
+      for (uint64_t t = u0; t < u1; ++t) {  // upper-triangle tile t, row-major (I <= J)
+        uint64_t I = 0, r = t;
+        while (r >= nb - I) {
+          r -= nb - I;
+          ++I;
+        }
+        const uint64_t J = I + r;
+        const int32_t* tl = h.data() + (t - u0) * 4096;
+        for (uint64_t y = 0; y < 64 && I * 64 + y < n; ++y)
+          for (uint64_t x = 0; x < 64 && J * 64 + x < n; ++x) {
+            const int32_t v = tl[y * 64 + x];
+            mat[(I * 64 + y) * n + J * 64 + x] = v;
+            mat[(J * 64 + x) * n + I * 64 + y] = v;
+          }
+      }
+    } else {
       const uint64_t m = u1 - u0;
       DevMem d_a(m * 4, device), d_b(m * 4, device), d_out(m * 4, device);
       check_hip(hipMemcpy(d_a.p, ia.data() + u0, m * 4, hipMemcpyHostToDevice), "H2D");
       check_hip(hipMemcpy(d_b.p, ib.data() + u0, m * 4, hipMemcpyHostToDevice), "H2D");
-      check(sks_intersect_pairs(c, d_words.as<uint64_t>(), d_starts.as<uint64_t>(), d_sizes.as<uint32_t>(),
-                                ew, d_a.as<int32_t>(), d_b.as<int32_t>(), m, d_out.as<int32_t>()));
+      check(sks_intersect_pairs(c, dw, ds, dz, ew, d_a.as<int32_t>(), d_b.as<int32_t>(), m, d_out.as<int32_t>()));
       check(sks_ctx_synchronize(c));
       check_hip(hipMemcpy(res.data() + u0, d_out.p, m * 4, hipMemcpyDeviceToHost), "D2H");
+      std::lock_guard<std::mutex> lock(g_pair_stats_mu);
+      g_pair_stats.h2d_bytes += 2 * m * 4;
+      g_pair_stats.d2h_bytes += m * 4;
     }
   };
   if (g_pair_devices.empty()) job(0, g_device, ctx());
   else on_pool(parts, devs, job);
-  if (dense) {  // each (i, j) is written by exactly one tile / row block of one part; the rest are 0
-    for (size_t k = 1; k < parts; ++k)
-      for (uint64_t e = 0; e < n * n; ++e) mats[0][e] += mats[k][e];
-    for (size_t i = 0; i < a.size(); ++i) res[i] = mats[0][(uint64_t)ia[i] * n + ib[i]];
+  {
+    std::lock_guard<std::mutex> lock(g_pair_stats_mu);
+    ++g_pair_stats.calls;
+    g_pair_stats.devices += parts;
   }
+  if (dense)
+    for (size_t i = 0; i < a.size(); ++i) res[i] = mat[(uint64_t)ia[i] * n + ib[i]];
   for (size_t i = 0; i < a.size(); ++i) {
     const bool same = a[i]->mask == b[i]->mask || a[i]->elements.empty() || b[i]->elements.empty();
     out[i] = same ? res[i] : 0;
@@ -963,6 +1024,13 @@ kmer_set set_from_stream(const std::vector<uint8_t>& stream, const kmer_bitset& 
 int g_host_threads = 0;  // set_host_threads; 0 = SKS_FACADE_THREADS, else min(16, cores)
 
 }  // namespace
+
+pair_flow_stats take_pair_flow_stats() {
+  std::lock_guard<std::mutex> lock(g_pair_stats_mu);
+  pair_flow_stats s = g_pair_stats;
+  g_pair_stats = pair_flow_stats{};
+  return s;
+}
 
 window_flow_stats take_window_flow_stats() {
   std::lock_guard<std::mutex> lock(g_stats_mu);

@@ -163,6 +163,14 @@ struct window_flow_stats {
   double d2h_ms = 0, wait_ms = 0, predicate_ms = 0, wall_ms = 0;
 };
 window_flow_stats take_window_flow_stats();
+// Pair counts on the GPU ([parallel_]compute_pairwise_kmer_set_intersections):
+// bytes moved since the last take — the sketches cross PCIe once (h2d), reach
+// the other pool devices device to device (d2d), and each device sends back
+// only its own tiles (d2h).
+struct pair_flow_stats {
+  uint64_t calls = 0, devices = 0, h2d_bytes = 0, d2d_bytes = 0, d2h_bytes = 0;
+};
+pair_flow_stats take_pair_flow_stats();
 // Host threads of parallel_kmer_sets_from_fasta_files with a std::function
 // predicate (one device worker each); 0 restores the default
 // (SKS_FACADE_THREADS, else min(16, cores)).

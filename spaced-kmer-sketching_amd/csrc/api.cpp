@@ -1612,6 +1612,57 @@ int sks_kmer_list_copy(const sks_kmer_list* kl, uint64_t* positions, uint64_t* b
   return SKS_OK;
 }
 
+// Group bounds fixed by the mask alone (no sample of the sketches): a masked
+// canonical k-mer of random sequence is min(F & M, R & M) of two near-uniform
+// values over the mask's 2k bits, so its packed value (the mask bits gathered)
+// has CDF 1 - (1 - x)^2 and the g/G quantile is x = 1 - sqrt(1 - g/G); the
+// bound is that packed value scattered back onto the mask bits (a pdep).  Any
+// non-decreasing bounds give exact counts (layout.hip): these only balance the
+// groups, and need no device pass and no exchange between ranks.
+int sks_join_layout_bounds_for_mask(const uint64_t mask[2], uint32_t log_b, int elem_words, uint64_t* bounds) {
+  if (!mask || !bounds) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds_for_mask: null argument");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (elem_words == 1 && mask[1]) return sks::fail(SKS_E_ARG, "sks_join_layout_bounds_for_mask: a 128-bit mask "
+                                                               "needs elem_words = 2");
+  const uint32_t G = sks_join_layout_groups(log_b);
+  const int P = __builtin_popcountll(mask[0]) + __builtin_popcountll(mask[1]);
+  auto pdep = [&](uint64_t vlo, uint64_t vhi, uint64_t* lo, uint64_t* hi) {
+    *lo = *hi = 0;
+    int j = 0;  // packed bit j -> the j-th set bit of the mask
+    for (int b = 0; b < 128; ++b) {
+      if (!((b < 64 ? mask[0] >> b : mask[1] >> (b - 64)) & 1)) continue;
+      const uint64_t bit = j < 64 ? (vlo >> j) & 1 : (vhi >> (j - 64)) & 1;
+      if (bit) {
+        if (b < 64) *lo |= 1ull << b;
+        else *hi |= 1ull << (b - 64);
+      }
+      ++j;
+    }
+  };
+  for (uint32_t g = 0; g <= G; ++g) {
+    uint64_t lo = 0, hi = 0;
+    if (g == G) {
+      lo = ~0ull;
+      hi = elem_words == 2 ? ~0ull : 0;
+    } else if (g > 0 && P > 0) {
+      const long double x = 1.0L - std::sqrt(1.0L - (long double)g / (long double)G);
+      uint64_t vlo = 0, vhi = 0;
+      if (P <= 64) {
+        const long double v = std::ldexp(x, P);
+        vlo = v >= 18446744073709551615.0L ? (P == 64 ? ~0ull : (1ull << P) - 1) : (uint64_t)v;
+      } else {
+        const long double v = std::ldexp(x, P - 64);
+        vhi = (uint64_t)std::floor(v);
+        vlo = (uint64_t)std::ldexp(v - std::floor(v), 64);
+      }
+      pdep(vlo, vhi, &lo, &hi);
+    }
+    bounds[(size_t)g * elem_words] = lo;
+    if (elem_words == 2) bounds[(size_t)g * 2 + 1] = hi;
+  }
+  return SKS_OK;
+}
+
 int sks_windows_dense_row_words(int window) { return window > 32 ? 4 : 3; }
 
 int sks_windows_dense(sks_ctx* c, const uint8_t* d_seq, uint64_t n_bytes, uint64_t first, uint64_t n_windows,
@@ -1958,6 +2009,65 @@ int sks_all_pairs_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_star
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
   SKS_HIP(sks::join_launch(L, 0, L, 0, n, log_b, elem_words, true, 0, n, 0, T, nullptr, true, cnt, c->join_check,
                            c->stream, ani ? &A : nullptr));
+  SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+  return SKS_OK;
+}
+
+int sks_layout_tiles_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_starts, const uint32_t* d_sizes,
+                         int elem_words, uint32_t n, uint64_t total, uint32_t log_b, const uint64_t* d_bounds,
+                         uint32_t blocks_hint, uint32_t blk0, const uint32_t* d_tiles, uint64_t n_tiles,
+                         uint32_t n_global, const int32_t* d_sizes_global, int kmer_num_ones, double* ani,
+                         int32_t* d_counts, uint32_t* d_status) {
+  if (!c) return sks::fail(SKS_E_ARG, "sks_layout_tiles_ani: null ctx");
+  if (elem_words != 1 && elem_words != 2) return sks::fail(SKS_E_ARG, "elem_words must be 1 or 2");
+  if (ani && kmer_num_ones <= 0) return sks::fail(SKS_E_ARG, "sks_layout_tiles_ani: kmer_num_ones must be positive");
+  if (log_b > sks_join_layout_log_b(~0u)) return sks::fail(SKS_E_ARG, "sks_layout_tiles_ani: log_b too large");
+  if (n_tiles && (!d_tiles || !d_counts || (ani && !d_sizes_global)))
+    return sks::fail(SKS_E_ARG, "sks_layout_tiles_ani: null argument");
+  if (n && (!d_starts || !d_sizes)) return sks::fail(SKS_E_ARG, "sks_layout_tiles_ani: null argument");
+  if (total >= (1ull << 32)) return sks::fail(SKS_E_UNSUPPORTED, "sks_layout_tiles_ani: >= 2^32 elements");
+  DeviceGuard g(c->device);
+  double* d_ani = ani;
+  if (ani && n_tiles) SKS_TRY(device_view_of_ani(ani, &d_ani, "sks_layout_tiles_ani"));
+  if (n == 0 || n_tiles == 0) {
+    if (d_status) SKS_HIP(hipMemsetAsync(d_status, 0, 8, c->stream));
+    if (n_tiles) SKS_HIP(hipMemsetAsync(d_counts, 0, n_tiles * 4096 * 4, c->stream));
+    SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+    SKS_HIP(hipEventRecord(c->ev_end, c->stream));
+    return SKS_OK;
+  }
+  // the layout in context scratch, as sks_all_pairs_ani; its second launch
+  // clears the caller's count tiles, the tiles' finisher counters and the
+  // status words, so the whole call is four launches and no memset
+  const uint32_t nb = (n + 63) / 64;
+  const uint64_t tot = std::max<uint64_t>(total, 1);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_vals = 0, o_masks = al(o_vals + tot * 8 * elem_words), o_boff = al(o_masks + tot * 8);
+  const size_t o_bst = al(o_boff + (size_t)nb * sks::join_layout_boff_words(log_b) * 4);
+  const size_t o_stat = al(o_bst + (size_t)(nb + 1) * 8);
+  const size_t o_tmp = al(o_stat + 16);
+  const size_t need = o_tmp + sks::join_layout_temp_bytes(n, log_b, elem_words) + 256;
+  SKS_HIP(c->lay.reserve(need));
+  SKS_HIP(c->tdone.reserve(n_tiles * sizeof(uint32_t)));
+  char* w = static_cast<char*>(c->lay.ptr);
+  uint64_t* vals = reinterpret_cast<uint64_t*>(w + o_vals);
+  uint64_t* masks = reinterpret_cast<uint64_t*>(w + o_masks);
+  uint32_t* boff = reinterpret_cast<uint32_t*>(w + o_boff);
+  uint64_t* bst = reinterpret_cast<uint64_t*>(w + o_bst);
+  uint32_t* stat = d_status ? d_status : reinterpret_cast<uint32_t*>(w + o_stat);
+  const sks::ZeroSpans zs{{stat, reinterpret_cast<uint32_t*>(d_counts), ani ? static_cast<uint32_t*>(c->tdone.ptr) : nullptr},
+                          {2, n_tiles * 4096, ani ? n_tiles : 0}};
+  SKS_HIP(sks::join_layout_build(d_data, d_starts, d_sizes, n, log_b, elem_words, d_bounds, w + o_tmp, vals, masks,
+                                 boff, bst, stat, c->join_check, c->stream, &zs, blocks_hint));
+  const sks::JoinLayout L{vals, masks, boff, bst};
+  sks::JoinAni A{d_ani, d_sizes_global, kmer_num_ones, static_cast<uint32_t*>(c->tdone.ptr)};
+  if (ani && c->root_k == kmer_num_ones) {  // the context's table (sks_ctx_ani_table), if for this k
+    A.root = static_cast<const double*>(c->root.ptr);
+    A.root_size = c->root_size;
+  }
+  SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  SKS_HIP(sks::join_launch(L, 0u - blk0, L, 0u - blk0, n_global, log_b, elem_words, true, 0, n_global, 0, n_tiles,
+                           d_tiles, true, d_counts, c->join_check, c->stream, ani ? &A : nullptr));
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;
 }

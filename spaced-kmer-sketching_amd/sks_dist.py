@@ -457,7 +457,8 @@ def _all_tiles(nb):
 
 
 def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", dst=0, ani_ones=None,
-                    ani_out=None, max_size=None, size_bound=None, exchange="p2p", world1_exchange=False):
+                    ani_out=None, max_size=None, size_bound=None, exchange="p2p", world1_exchange=False,
+                    bounds_mask=None):
     """All-vs-all intersection counts (kmer_set.cpp:143-184 over the
     generate_all_pairs_from_vector list, generators.hpp:44-58), and ANI when
     ani_ones (the k of binomial_estimator) is given (kmer-sketching.cpp:195-200).
@@ -479,7 +480,10 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     (else one device reduction and a read-back).  size_bound: an upper bound of
     every rank's sketch sizes that all ranks pass alike (bottom-s: s) — the
     exchange then needs no size all-gather and no host round trip.  exchange:
-    "p2p", "allgather" or "broadcast" (see above).  One rank — with or without
+    "p2p", "allgather" or "broadcast" (see above).  bounds_mask: the k-mer
+    mask the sketches were built with; every rank then takes the value-group
+    bounds from the mask alone (ops.bounds_for_mask, sks_join_layout_bounds_for_mask)
+    instead of rank 0 sampling its sketches and broadcasting them.  One rank — with or without
     a process group — counts every tile of one layout in one native call
     (sks_all_pairs_ani); world1_exchange keeps a world-1 process group on the
     exchange path instead (the RCCL rehearsal tests).  Returns a JoinResult."""
@@ -536,43 +540,56 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
         if stats_mark is not None:
             res._stats = ops.stats_since(stats_mark)
         return res
-    # rank 0's group bounds, shared by every layout (blocks of different ranks
-    # are joined bucket by bucket)
-    gb = ops.bounds(mine, log_b) if rank == 0 else ops.bounds_like(log_b)
-    if world > 1:
-        gb = _broadcast(gb, 0, world)
+    # one set of group bounds shared by every layout (blocks of different ranks
+    # are joined bucket by bucket): fixed by the mask on every rank alike, or
+    # rank 0's sampled bounds broadcast
+    if bounds_mask is not None and hasattr(ops, "bounds_for_mask"):
+        gb = ops.bounds_for_mask(bounds_mask, log_b)
+    else:
+        gb = ops.bounds(mine, log_b) if rank == 0 else ops.bounds_like(log_b)
+        if world > 1:
+            gb = _broadcast(gb, 0, world)
     local, remote = tile_plan_by_peer(n_genomes, world, rank)
-    T = len(local) + sum(len(r) for r in remote)
-    parts = ops.parts(T, device)
-    sizes_all = torch.zeros(max(n_genomes, 1), dtype=torch.int32, device=device) if fused else None
-    if fused and mine.n:
-        sizes_all[g0:g1] = mine.sizes
+    tq, held = _cross_plan(n_genomes, world, rank)
+    T = len(local) + len(tq)
+    native = hasattr(ops, "layout_tiles_ani")  # layout + join (+ ANI) in one call, clearing its own outputs
+    parts = ops.parts(T, device, zeroed=not native)
     wait = _exchange_start(mine, n_genomes, world, rank, max(gmax, 1), ops, exchange) if world > 1 else None
-    own = ops.build(mine, log_b, gb, "own") if mine.n else None
+    if native:
+        # the rank's own tiles while the peers' sketches travel; the ANI finisher
+        # reads |S_g| by global genome g, so the own set's sizes are offset by g0
+        if len(local):
+            ops.layout_tiles_ani(mine, log_b, gb, 0, g0 // TILE, local, parts[:len(local)], _OffsetSizes(mine.sizes, g0),
+                                 n_genomes, ani_ones if fused else None, ani_out if fused else None)
+        if len(tq):
+            union = wait()
+            ops.layout_tiles_ani(union, log_b, gb, held, 0, tq, parts[len(local):T], union.sizes, n_genomes,
+                                 ani_ones if fused else None, ani_out if fused else None)
+    else:
+        sizes_all = torch.zeros(max(n_genomes, 1), dtype=torch.int32, device=device) if fused else None
+        if fused and mine.n:
+            sizes_all[g0:g1] = mine.sizes
+        own = ops.build(mine, log_b, gb, "own") if mine.n else None
 
-    def count(rows, rb, cols, cb, tiles, out):
-        if fused:
-            ops.count_ani(n_genomes, log_b, rows, rb, cols, cb, tiles, out, sizes_all, ani_ones, ani_out)
-        else:
-            ops.count(n_genomes, log_b, rows, rb, cols, cb, tiles, out)
-    if len(local):  # the rank's own tiles while the peers' sketches travel
-        count(own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
-    off = len(local)
-    # every cross-rank tile of the plan in one join over one layout of the rank's
-    # own and peer rows (the exchange buffer: row g = genome g, so block numbers
-    # are global and blk0 = 0); rows the plan does not need are empty.  (One
-    # layout of the peer rows alone and two joins, own x peers and peers x own,
-    # measured 0.585 against 0.524 ms per rank at N = 8: tools/rank_sim.py)
-    tq = np.concatenate([remote[q] for q in peer_needs(n_genomes, world, rank)] +
-                        [np.zeros((0, 2), np.int64)]).reshape(-1, 2)
-    if len(tq):
-        union = wait()
-        held = sum((block_shard(n_genomes, world, q)[2] - block_shard(n_genomes, world, q)[1] + TILE - 1) // TILE
-                   for q in [rank] + peer_needs(n_genomes, world, rank))
-        lu = ops.build(union, log_b, gb, "peers", blocks_hint=held)
-        if fused:
-            sizes_all[:n_genomes] = union.sizes[:n_genomes]
-        count(lu, 0, lu, 0, tq, parts[off:off + len(tq)])
+        def count(rows, rb, cols, cb, tiles, out):
+            if fused:
+                ops.count_ani(n_genomes, log_b, rows, rb, cols, cb, tiles, out, sizes_all, ani_ones, ani_out)
+            else:
+                ops.count(n_genomes, log_b, rows, rb, cols, cb, tiles, out)
+        if len(local):  # the rank's own tiles while the peers' sketches travel
+            count(own, g0 // TILE, own, g0 // TILE, local, parts[:len(local)])
+        off = len(local)
+        # every cross-rank tile of the plan in one join over one layout of the rank's
+        # own and peer rows (the exchange buffer: row g = genome g, so block numbers
+        # are global and blk0 = 0); rows the plan does not need are empty.  (One
+        # layout of the peer rows alone and two joins, own x peers and peers x own,
+        # measured 0.585 against 0.524 ms per rank at N = 8: tools/rank_sim.py)
+        if len(tq):
+            union = wait()
+            lu = ops.build(union, log_b, gb, "peers", blocks_hint=held)
+            if fused:
+                sizes_all[:n_genomes] = union.sizes[:n_genomes]
+            count(lu, 0, lu, 0, tq, parts[off:off + len(tq)])
     res.tiles = np.concatenate([local, tq]).reshape(-1, 2)
     res.counts = parts[:T]
     if stats_mark is not None:
@@ -591,6 +608,34 @@ def all_vs_all_join(n_genomes, world, rank, mine, ops, log_b_for, device="cpu", 
     out = torch.zeros((n_genomes, n_genomes), dtype=torch.int32, device=device)
     res.matrix = place_tiles(out, tiles, got, n_genomes)
     return res
+
+
+class _OffsetSizes:
+    """The sizes of genomes [g0, g0 + n) addressed by GLOBAL genome index: the
+    device pointer moved back by g0 words (only indices in range are read)."""
+
+    def __init__(self, t, g0):
+        self.t, self.g0 = t, g0
+
+    def data_ptr(self):
+        return self.t.data_ptr() - 4 * self.g0
+
+    def __getitem__(self, g):
+        return self.t[g - self.g0]
+
+
+@functools.lru_cache(maxsize=64)
+def _cross_plan(n_genomes, world, rank):
+    """(tiles, held): the rank's cross-rank tiles in count order (its peers in
+    peer_needs order) and the 64-sketch blocks its exchange buffer holds (its own
+    and its peers'), computed once per shape."""
+    _, remote = tile_plan_by_peer(n_genomes, world, rank)
+    need = peer_needs(n_genomes, world, rank)
+    tq = np.concatenate([remote[q] for q in need] + [np.zeros((0, 2), np.int64)]).reshape(-1, 2)
+    tq.flags.writeable = False
+    held = sum((block_shard(n_genomes, world, q)[2] - block_shard(n_genomes, world, q)[1] + TILE - 1) // TILE
+               for q in [rank] + need)
+    return tq, held
 
 
 def _plan_in_count_order(n_genomes, world, rank):
@@ -682,6 +727,14 @@ class GpuJoinOps:
     def bounds_like(self, log_b):
         return torch.empty((self.sksffi.join_layout_groups(log_b) + 1) * self.ew, dtype=torch.int64, device="cuda")
 
+    def bounds_for_mask(self, mask, log_b):
+        """The mask-derived group bounds on the device (uploaded once per (mask, log_b))."""
+        key = ("mask_bounds", int(mask), log_b, self.ew)
+        if key not in self.keep:
+            h = self.sksffi.join_layout_bounds_for_mask(int(mask), log_b, self.ew)
+            self.keep[key] = torch.from_numpy(h.view(np.int64)).to("cuda")
+        return self.keep[key]
+
     def bounds(self, src, log_b):
         b = self.bounds_like(log_b)
         _ctx_waits_for_torch(self.ctx)
@@ -751,6 +804,21 @@ class GpuJoinOps:
                 self.tile_cache.clear()
             self.tile_cache[key] = torch.from_numpy(np.array(tiles, dtype=np.int32)).reshape(-1, 2).to("cuda")
         return self.tile_cache[key]
+
+    def layout_tiles_ani(self, src, log_b, gb, blocks_hint, blk0, tiles, out, sizes_global, n_global, k, ani):
+        """sks_layout_tiles_ani: the layout of src (block 0 = global block blk0) and
+        the join of the global tile list into the packed out (cleared by the call),
+        with the ANI into ani when k is given; the build's status words go to the
+        call's log."""
+        ani_ptr = (ani.data_ptr() if hasattr(ani, "data_ptr") else ani.ptr) if k is not None else 0
+        tl = self._tiles(tiles)
+        _ctx_waits_for_torch(self.ctx)
+        self.ctx.layout_tiles_ani(src.data.data_ptr(), src.starts.data_ptr(), src.sizes.data_ptr(), src.n,
+                                  max(src.total, 1), log_b, gb.data_ptr() if gb is not None else 0, blocks_hint, blk0,
+                                  tl.data_ptr(), tl.shape[0], n_global, sizes_global.data_ptr() if k is not None else 0,
+                                  k or 0, ani_ptr, out.data_ptr(), self._stat_slot(), elem_words=self.ew)
+        _torch_waits_for_ctx(self.ctx)
+        self.keep[("lt", blk0)] = (src, gb, sizes_global)
 
     def count(self, n, log_b, rows, r_blk0, cols, c_blk0, tiles, out):
         _ctx_waits_for_torch(self.ctx)

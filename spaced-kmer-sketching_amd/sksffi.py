@@ -70,6 +70,7 @@ EXPORTED = [
     "sks_sketch_set_export_csr", "sks_ani_matrix", "sks_ani_rows", "sks_ani_tiles",
     "sks_intersect_layout_ani", "sks_host_alloc", "sks_host_free", "sks_join_layout_stat_copy",
     "sks_sketches_export", "sks_all_pairs_ani", "sks_windows_dense", "sks_windows_dense_row_words",
+    "sks_join_layout_bounds_for_mask", "sks_layout_tiles_ani",
 ]
 
 _lib = None
@@ -151,6 +152,8 @@ def lib():
     L.sks_sketches_export.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, vp, C.c_uint64, vp]
     L.sks_all_pairs_ani.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, vp, vp,
                                     vp]
+    L.sks_layout_tiles_ani.argtypes = [vp, vp, vp, vp, C.c_int, C.c_uint32, C.c_uint64, C.c_uint32, vp,
+                                       C.c_uint32, C.c_uint32, vp, C.c_uint64, C.c_uint32, vp, C.c_int, vp, vp, vp]
     L.sks_sketch_set_export_csr.argtypes = [vp, vp, vp]
     L.sks_ani_matrix.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, vp]
     L.sks_ani_rows.argtypes = [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, vp, vp]
@@ -172,6 +175,7 @@ def lib():
                                       C.POINTER(Policy), C.POINTER(vp)]
     L.sks_windows_dense.argtypes = [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, u64p, vp, vp]
     L.sks_windows_dense_row_words.argtypes = [C.c_int]
+    L.sks_join_layout_bounds_for_mask.argtypes = [u64p, C.c_uint32, C.c_int, vp]
     L.sks_kmer_list_free.argtypes = [vp]
     L.sks_kmer_list_total.argtypes = [vp]
     L.sks_kmer_list_total.restype = C.c_uint64
@@ -247,6 +251,14 @@ def join_layout_capacity():
 
 def join_layout_groups(log_b):
     return int(lib().sks_join_layout_groups(log_b))
+
+
+def join_layout_bounds_for_mask(mask, log_b, elem_words=1):
+    """sks_join_layout_bounds_for_mask: the mask-derived group bounds, a uint64 array
+    of (join_layout_groups(log_b) + 1) * elem_words words (host)."""
+    out = np.zeros((join_layout_groups(log_b) + 1) * elem_words, dtype=np.uint64)
+    check(lib().sks_join_layout_bounds_for_mask(_mask_arr(mask), log_b, elem_words, out.ctypes.data))
+    return out
 
 
 def join_layout_boff_words(log_b):
@@ -412,6 +424,15 @@ class Context:
         check(lib().sks_all_pairs_ani(self.h, C.c_void_p(data), C.c_void_p(starts), C.c_void_p(sizes), elem_words,
                                       n, max_size, total, kmer_num_ones, C.c_void_p(ani) if ani else None,
                                       C.c_void_p(counts) if counts else None, C.c_void_p(status) if status else None))
+
+    def layout_tiles_ani(self, data, starts, sizes, n, total, log_b, bounds, blocks_hint, blk0, tiles, n_tiles,
+                         n_global, sizes_global, kmer_num_ones, ani, counts, status, elem_words=1):
+        """sks_layout_tiles_ani (device pointers; ani: device or pinned host pointer,
+        or 0 for counts only): layout + join of a global tile list in one call."""
+        v = lambda p: C.c_void_p(p) if p else None  # noqa: E731
+        check(lib().sks_layout_tiles_ani(self.h, v(data), v(starts), v(sizes), elem_words, n, total, log_b,
+                                         v(bounds), blocks_hint, blk0, v(tiles), n_tiles, n_global,
+                                         v(sizes_global), kmer_num_ones, v(ani), v(counts), v(status)))
 
     def sketches_export(self, data, starts, sizes, n, dst, stride, dst_sizes, elem_words=1):
         """sks_sketches_export (device pointers): sketches padded to a fixed stride."""

@@ -46,7 +46,9 @@ static int sketch(int argc, char** argv) {
   std::vector<kmer_set*> ptrs;
   for (auto& s : data) ptrs.push_back(&s);
   auto pairs = generate_all_pairs_from_vector<kmer_set*>(ptrs);
+  (void)sks::take_pair_flow_stats();
   std::vector<int> inter = parallel_compute_pairwise_kmer_set_intersections(pairs.first, pairs.second);
+  const sks::pair_flow_stats pst = sks::take_pair_flow_stats();
   std::vector<int> inter2 = compute_pairwise_kmer_set_intersections(pairs.first, pairs.second);
 
   std::printf("{\"mask\":\"%016llx%016llx\",\"k\":%d,\"sets\":[", (unsigned long long)mask.hi(),
@@ -59,6 +61,9 @@ static int sketch(int argc, char** argv) {
   for (int i = 0; i < n; ++i) same = same && data[i].elements == serial[i].elements;
   std::printf("],\"serial_equal\":%s,\"devices\":%d,", same ? "true" : "false",
               (int)sks::parallel_devices().size());
+  std::printf("\"pair_stats\":{\"calls\":%llu,\"devices\":%llu,\"h2d\":%llu,\"d2d\":%llu,\"d2h\":%llu},",
+              (unsigned long long)pst.calls, (unsigned long long)pst.devices, (unsigned long long)pst.h2d_bytes,
+              (unsigned long long)pst.d2d_bytes, (unsigned long long)pst.d2h_bytes);
   if (!same) {  // diagnostics: the serial build's sets
     std::printf("\"serial_sets\":[");
     for (int i = 0; i < n; ++i) {

@@ -199,6 +199,11 @@ class NpJoinOps:
             out += [v & M64] if self.ew == 1 else [v & M64, v >> 64]
         return torch.tensor(np.array(out, dtype=np.uint64).view(np.int64))
 
+    def bounds_for_mask(self, mask, log_b):
+        """sks_join_layout_bounds_for_mask (host; every rank computes the same)"""
+        import sksffi
+        return torch.from_numpy(sksffi.join_layout_bounds_for_mask(mask, log_b, self.ew).view(np.int64))
+
     def build(self, src, log_b, gb, key, blocks_hint=0):
         G = sks_dist_groups(log_b)
         bnd = [_ival(gb, self.ew, g) for g in range(G + 1)]
@@ -247,7 +252,20 @@ class NpJoinOps:
                         ani[j, i] = O.binomial_estimator(O.containment(x, int(sizes[j])), k)
 
     def parts(self, T, device, zeroed=True):
-        return torch.zeros((max(T, 1), 64, 64), dtype=torch.int32)
+        # (uncleared tiles for layout_tiles_ani, which clears them itself)
+        f = torch.zeros if zeroed else (lambda *a, **k: torch.full(*a, -99, **k))
+        return f((max(T, 1), 64, 64), dtype=torch.int32)
+
+    def layout_tiles_ani(self, src, log_b, gb, blocks_hint, blk0, tiles, out, sizes_global, n_global, k, ani):
+        """sks_layout_tiles_ani's contract: the layout of src (its block 0 is global
+        block blk0), the global tiles joined into out (cleared first), and with k
+        the ANI of both orientations (|S_g| by global g)."""
+        lay = self.build(src, log_b, gb, "own" if not blocks_hint else "peers", blocks_hint)
+        out.zero_()
+        if k is None:
+            self.count(n_global, log_b, lay, blk0, lay, blk0, tiles, out)
+        else:
+            self.count_ani(n_global, log_b, lay, blk0, lay, blk0, tiles, out, sizes_global, k, ani)
 
     def pad(self, src, stride, data, sizes):
         """the sketches at a fixed stride, padded with ~0 words (sks_sketches_export)"""
@@ -268,7 +286,7 @@ def sks_dist_groups(log_b):
     return 1 << (log_b - 3) if log_b > 3 else 1
 
 
-def _join_worker(rank, world, port, q, dst, n_genomes, ew, exchange, bound):
+def _join_worker(rank, world, port, q, dst, n_genomes, ew, exchange, bound, mask_bounds=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -281,7 +299,9 @@ def _join_worker(rank, world, port, q, dst, n_genomes, ew, exchange, bound):
     ops = NpJoinOps(ew, rank)
     res = sks_dist.all_vs_all_join(n_genomes, world, rank, src, ops, lambda m: 5, dst=dst, ani_ones=21,
                                    exchange=exchange,
-                                   size_bound=max(len(x) for x in sk) + 3 if bound else None)
+                                   size_bound=max(len(x) for x in sk) + 3 if bound else None,
+                                   bounds_mask=(O.mask(21, 21, 0) if ew == 1 else O.mask(40, 30, 0))
+                                   if mask_bounds else None)
     q.put((rank, None if res.matrix is None else res.matrix.numpy(), ops.built, ops.calls,
            res.tiles, res.counts.numpy(), res.ani.numpy()))
     dist.destroy_process_group()
@@ -312,12 +332,13 @@ def _join_sketches(n_genomes, ew):
     return out
 
 
-@pytest.mark.parametrize("world,dst,n_genomes,ew,exchange,bound", [
-    (2, 0, N_GENOMES, 1, "p2p", True), (3, "all", N_GENOMES, 1, "p2p", False),
-    (2, 1, 200, 1, "allgather", True), (3, 0, 200, 1, "broadcast", True), (3, 0, 200, 1, "p2p", True),
-    (3, 0, 130, 2, "allgather", False), (4, "all", 200, 1, "p2p", True), (8, 0, 600, 1, "p2p", True),
-    (8, 3, 600, 1, "allgather", False)])
-def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bound):
+@pytest.mark.parametrize("world,dst,n_genomes,ew,exchange,bound,mask_bounds", [
+    (2, 0, N_GENOMES, 1, "p2p", True, False), (3, "all", N_GENOMES, 1, "p2p", False, False),
+    (2, 1, 200, 1, "allgather", True, True), (3, 0, 200, 1, "broadcast", True, False),
+    (3, 0, 200, 1, "p2p", True, True), (3, 0, 130, 2, "allgather", False, True),
+    (4, "all", 200, 1, "p2p", True, False), (8, 0, 600, 1, "p2p", True, True),
+    (8, 3, 600, 1, "allgather", False, False)])
+def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bound, mask_bounds):
     """Ranks build the layout of their own block-aligned genomes with rank 0's
     bounds and count their own blocks' tiles first; once the peers' sketches
     have landed in the rank's exchange buffer (p2p send/recv, one all-gather, or
@@ -327,14 +348,17 @@ def test_all_vs_all_join_exchanges_gloo(world, dst, n_genomes, ew, exchange, bou
     from the lower rank's blocks) in one join; the packed tiles go to dst (every rank for
     "all"), whose matrix equals the single-process merge counts, and the ANI
     each rank wrote for its tiles (both orientations) equals the reference
-    formula, every ordered pair written by exactly one rank.  n = 200 at world
+    formula, every ordered pair written by exactly one rank.  mask_bounds:
+    every rank takes the group bounds from the mask
+    (sks_join_layout_bounds_for_mask) instead of rank 0's broadcast.  n = 200 at world
     3 and 4 leaves ranks without genomes; ew = 2 moves 128-bit (lo, hi) k-mers
     (w = 40); world 8 over 600 genomes (10 blocks) is the N = 8 plan with
     ragged block ranges."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes, ew, exchange, bound))
+    procs = [ctx.Process(target=_join_worker, args=(r, world, port, q, dst, n_genomes, ew, exchange, bound,
+                                                    mask_bounds))
              for r in range(world)]
     for p in procs:
         p.start()

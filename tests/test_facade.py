@@ -99,8 +99,9 @@ def test_facade_sketch_and_ani(facade_bin, tmp_path, w, k, seed, param, kind, po
 @pytest.mark.parametrize("w,k,param", [(31, 21, 10), (40, 30, 5)])
 def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param, pool):
     """70 sets: the all-pairs list of generate_all_pairs_from_vector covers the
-    whole matrix, so the facade counts it with the symmetric join
-    (sks_intersect_sym) and gathers; counts and ANI equal the oracle's."""
+    whole matrix, so the facade counts it with the join (one layout of the 70
+    sketches, each pool entry's share of the upper-triangle tiles, packed) and
+    gathers; counts and ANI equal the oracle's."""
     files = []
     for i in range(70):
         g = synth.bases(3000, seed=900 + i % 5, mut_seed=950 + i, mut_rate=0.02 * (i % 3))
@@ -119,6 +120,14 @@ def test_facade_all_pairs_matrix_path(facade_bin, tmp_path, w, k, param, pool):
     assert out["inter_serial_equal"]
     if pool:
         assert out["devices"] == 3
+    # the sketches crossed PCIe once (not once per pool entry), every pool entry
+    # of the one device shared that copy (no device-to-device bytes), and only
+    # the 3 upper-triangle 64 x 64 tiles came back (16 KB each)
+    ps = out["pair_stats"]
+    ew = 2 if any(int(x) for s_ in sk for x in (s_[:, 1] if s_.ndim == 2 else [])) else 1
+    want_h2d = sum(len(s_) for s_ in sk) * 8 * ew + n * 8 + n * 4
+    assert ps["calls"] == 1 and ps["h2d"] == want_h2d and ps["d2d"] == 0, ps
+    assert ps["d2h"] == 3 * 64 * 64 * 4 and ps["devices"] == (3 if pool else 1), ps
 
 
 REF_CALLER = os.path.join(ROOT, "tests", "cpp", "build", "ref_caller")

@@ -123,3 +123,44 @@ def test_ani_table_argument_errors():
     lib = sksffi.lib()
     assert lib.sks_ctx_ani_table(None, C.c_uint32(100), 21) == 1
     assert b"null ctx" in lib.sks_last_error()
+
+
+@pytest.mark.parametrize("w,k", [(31, 21), (21, 21), (32, 32), (45, 30), (64, 40), (12, 0)])
+def test_join_layout_bounds_for_mask(w, k):
+    """sks_join_layout_bounds_for_mask: (G + 1) non-decreasing bounds that hold
+    only mask bits, bounds[0] = 0 and bounds[G] = all ones; on simulated
+    canonical k-mers (min of two uniform masked values) the G value groups are
+    balanced."""
+    import sksffi
+    m = sksffi.mask_generate(w, k, 3)
+    ew = 1 if w <= 32 else 2
+    log_b = 12
+    G = sksffi.join_layout_groups(log_b)
+    b = sksffi.join_layout_bounds_for_mask(m, log_b, ew)
+    assert len(b) == (G + 1) * ew
+    vals = [int(b[g * ew]) | (int(b[g * ew + 1]) << 64 if ew == 2 else 0) for g in range(G + 1)]
+    assert vals[0] == 0 and vals[G] == (2 ** (64 * ew) - 1)
+    assert all(x <= y for x, y in zip(vals, vals[1:]))
+    assert all(v & ~m == 0 for v in vals[1:G])
+    if k == 0:
+        return
+    P = 2 * k
+    rng = np.random.default_rng(1)
+    n = 200_000
+    a = rng.integers(0, 2 ** min(P, 62), size=n, dtype=np.uint64).astype(object)
+    c = rng.integers(0, 2 ** min(P, 62), size=n, dtype=np.uint64).astype(object)
+    if P > 62:  # widen to P bits
+        a = [int(x) << (P - 62) for x in a]
+        c = [int(x) << (P - 62) for x in c]
+    packed_bounds = []
+    for v in vals[1:G]:  # pext of each bound
+        x, j = 0, 0
+        for bit in range(128):
+            if (m >> bit) & 1:
+                x |= ((v >> bit) & 1) << j
+                j += 1
+        packed_bounds.append(x)
+    mins = np.sort(np.array([min(int(x), int(y)) for x, y in zip(a, c)], dtype=object))
+    idx = np.searchsorted(mins, np.array(packed_bounds, dtype=object))
+    counts = np.diff(np.concatenate([[0], idx, [n]]))
+    assert counts.max() < 1.5 * n / G + 40

@@ -1,11 +1,13 @@
 """One rank of an N-GPU config-4 all-vs-all, replayed on one GPU (no process
 group): sks_dist.all_vs_all_join runs its multi-rank path for `rank` of `world`
-exactly as on N GPUs — rank 0's group bounds, the rank's own layout and tiles,
-then one layout per run of peers and the plan's tiles, fused ANI into pinned host
-memory — except that the exchange is replaced by copying the peers' sketches out
-of the full set already on this GPU (what the exchange would deliver, padded to
-the same stride).  The exchange itself is not timed here (its bytes per rank are
-in DESIGN.md §7).  Also times the sketch phase of the rank's genomes.
+exactly as on N GPUs — the group bounds from the mask, the rank's own export,
+layout and tiles, then one layout of the own and peer rows and the plan's cross
+tiles, fused ANI into pinned host memory — except that the exchange itself is
+replaced: the peers' padded rows (what the exchange delivers, the peers' own
+exports) are prepared once outside the timed calls, and each call writes only
+the rank's own slot (its export, as on N GPUs) and hands over the buffer.  The
+exchange's transfer is not timed here (its bytes per rank are in DESIGN.md §7).
+Also times the sketch phase of the rank's genomes.
     python tools/rank_sim.py [world ...]      (default 2 4 8)
 Prints, per world: every rank's pair-step time (median of reps) and the max."""
 import os
@@ -59,25 +61,31 @@ def main():
     for world in worlds:
         hb.array[:] = -1.0
         per = sks_dist.block_shard(n, world, 0)[0] * TILE
-        _, a0, b0 = sks_dist.block_shard(n, world, 0)
-        gb0 = ops.bounds(sub(a0, b0), log_b)  # rank 0's value-group bounds, as the broadcast delivers them
+        # every rank's padded rows, as the peers' exports produce them (prepared
+        # once, outside the timed calls); per rank the sizes of the rows its
+        # exchange would leave filled (its own and its peers'; the rest size 0)
+        xbuf = torch.empty((world * per * S,), dtype=torch.int64, device="cuda")
+        full_sz_all = torch.zeros(world * per, dtype=torch.int32, device="cuda")
+        for q in range(world):
+            _, a, b = sks_dist.block_shard(n, world, q)
+            if b > a:
+                ops.pad(sub(a, b), S, xbuf[q * per * S:(q + 1) * per * S], full_sz_all[q * per:(q + 1) * per])
+        rank_sz = {}
+        for r in range(world):
+            keep = torch.zeros(world * per, dtype=torch.bool, device="cuda")
+            for q in [r] + sks_dist.peer_needs(n, world, r):
+                keep[q * per:(q + 1) * per] = True
+            rank_sz[r] = torch.where(keep, full_sz_all, torch.zeros_like(full_sz_all))
         torch.cuda.synchronize()
-        sks_dist._broadcast = lambda t, src, world_: t.copy_(gb0)
 
         def fake_exchange(own, n_genomes, world_, rank, stride, ops_, mode):
-            # what the exchange leaves: every rank's slot of `per` rows, the own and
-            # the peers' rows filled (the rest size 0)
-            full = torch.empty((world_ * per * stride,), dtype=torch.int64, device="cuda")
-            full_sz = torch.zeros(world_ * per, dtype=torch.int32, device="cuda")
-            for q in [rank] + sks_dist.peer_needs(n_genomes, world_, rank):
-                _, a, b = sks_dist.block_shard(n_genomes, world_, q)
-                if b > a:
-                    ops_.pad(sub(a, b), stride, full[q * per * stride:(q + 1) * per * stride],
-                             full_sz[q * per:(q + 1) * per])
-            torch.cuda.synchronize()  # the "exchange" is outside the timed region
+            # the rank's own slot: its export, exactly as the real exchange writes
+            # it before sending; the peers' rows are already in place
+            sz = rank_sz[rank]
+            ops_.pad(own, stride, xbuf[rank * per * stride:(rank + 1) * per * stride], sz[rank * per:(rank + 1) * per])
 
             def wait():
-                return sks_dist._strided(full, full_sz, 1, stride)
+                return sks_dist._strided(xbuf, sz, 1, stride)
             return wait
         sks_dist._exchange_start = fake_exchange
         times, sketch_ms = [], []
@@ -92,7 +100,8 @@ def main():
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 res = sks_dist.all_vs_all_join(n, world, rank, mine, ops, sksffi.join_layout_log_b, device="cuda",
-                                               dst=None, ani_ones=ones, ani_out=hb, max_size=mx, size_bound=S)
+                                               dst=None, ani_ones=ones, ani_out=hb, max_size=mx, size_bound=S,
+                                               bounds_mask=mask)
                 torch.cuda.synchronize()
                 ms.append((time.perf_counter() - t0) * 1e3)
             res.check_layouts()
