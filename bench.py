@@ -975,9 +975,14 @@ def run_ref_sweep(ctx, cpu=False):
         def part(ix):
             s, c = sum(sk[i] for i in ix), sum(cp[i] for i in ix)
             return {"configs": len(ix), "sketch_ms_per_config": s / len(ix), "compare_ms_per_config": c / len(ix),
+                    "sketch_ms_median": statistics.median(sk[i] for i in ix),
+                    "compare_ms_median": statistics.median(cp[i] for i in ix),
+                    "sketch_ms_max": max(sk[i] for i in ix), "compare_ms_max": max(cp[i] for i in ix),
                     "sketch_kmers_per_s": sum(wins[i] for i in ix) / (s * 1e-3),
                     "compare_pairs_per_s": len(ix) * n * n / (c * 1e-3)}
         res = {"metric": "reference sweep (kmer-sketching main), 62 (w, k) configs",
+               "per_config_ms": [{"w": w_, "k": k_, "sketch": round(sk[i], 4), "compare": round(cp[i], 4)}
+                                 for i, (w_, k_) in enumerate(cfg)],
                "genomes": n, "genome_len": C4_LEN, "pairs_per_config": n * n,
                "driver": "spaced-kmer-sketching_amd/bin/kmer-sketching: this engine's restatement of the reference "
                          "main (apps/kmer_sketching.cpp + cpp/sweep.cpp) - files parsed once and kept in HBM, the "

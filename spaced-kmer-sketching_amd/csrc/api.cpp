@@ -2066,8 +2066,11 @@ int sks_layout_tiles_ani(sks_ctx* c, const uint64_t* d_data, const uint64_t* d_s
     A.root_size = c->root_size;
   }
   SKS_HIP(hipEventRecord(c->ev_begin, c->stream));
+  // the layout's region log, as join_layout_build picks it: a tile list over
+  // this one layout joins without cross-region windows when regions hold 64 buckets
+  const int rg = (int)sks::join_layout_region_log(blocks_hint ? std::min(blocks_hint, nb) : nb, log_b);
   SKS_HIP(sks::join_launch(L, 0u - blk0, L, 0u - blk0, n_global, log_b, elem_words, true, 0, n_global, 0, n_tiles,
-                           d_tiles, true, d_counts, c->join_check, c->stream, ani ? &A : nullptr));
+                           d_tiles, true, d_counts, c->join_check, c->stream, ani ? &A : nullptr, rg));
   SKS_HIP(hipEventRecord(c->ev_end, c->stream));
   return SKS_OK;
 }

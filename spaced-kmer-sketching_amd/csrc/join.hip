@@ -795,7 +795,7 @@ unsigned long long join_check_take() {
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
                        uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
-                       int32_t* out, bool check, hipStream_t s, const JoinAni* ani) {
+                       int32_t* out, bool check, hipStream_t s, const JoinAni* ani, int layout_rg) {
   if (log_b > jc::kMaxLogB || (ew != 1 && ew != 2)) return hipErrorInvalidValue;
   if (ani && !sym && !d_tiles) return hipErrorInvalidValue;  // ANI of whole tiles only
   const uint32_t n_cb = (n + kTile - 1) / kTile;
@@ -854,8 +854,10 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
   // known only for one layout covering all n sketches (the build picks its
   // region size from its block count, join_layout_region_log); a tile list
   // joins per-rank layouts, small ones
-  const bool big = !d_tiles && r_blk0 == 0 && c_blk0 == 0 && rows.vals == cols.vals &&
-                   jc::lay_rb_log(log_b, join_layout_region_log(n_cb, log_b)) >= (uint32_t)kJWinLog;
+  const bool one_layout = rows.vals == cols.vals && rows.boff == cols.boff;
+  const bool big = (!d_tiles && r_blk0 == 0 && c_blk0 == 0 && one_layout &&
+                    jc::lay_rb_log(log_b, join_layout_region_log(n_cb, log_b)) >= (uint32_t)kJWinLog) ||
+                   (layout_rg >= 0 && one_layout && jc::lay_rb_log(log_b, (uint32_t)layout_rg) >= (uint32_t)kJWinLog);
   const bool pieces = !big;
 #define SKS_JOIN_LAUNCH(E, C, P) launch_join_slices<E, C, P>(ja, tile_begin, tile_end, packed, out, tile_done, s)
   if (ew == 1) {

@@ -262,7 +262,10 @@ struct JoinAni {
 hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout& cols, uint32_t c_blk0,
                        uint32_t n, uint32_t log_b, int ew, bool sym, uint32_t row_begin, uint32_t row_end,
                        uint64_t tile_begin, uint64_t tile_end, const uint32_t* d_tiles, bool packed,
-                       int32_t* out, bool check, hipStream_t s, const JoinAni* ani = nullptr);
+                       int32_t* out, bool check, hipStream_t s, const JoinAni* ani = nullptr,
+                       int layout_rg = -1);
+// (layout_rg >= 0: rows and cols are ONE layout built with that region log, so a
+// tile list needs no cross-region windows when its regions hold 64 buckets)
 // SKS check builds: invariant violations counted since the last call (and reset)
 unsigned long long join_check_take();
 unsigned long long layout_check_take();
