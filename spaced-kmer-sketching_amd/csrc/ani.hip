@@ -93,4 +93,6 @@ hipError_t launch_ani_tiles(const int32_t* packed, const uint32_t* tiles, uint64
   return hipGetLastError();
 }
 
+SKS_CODE_OBJECT_HOOK(ani)
+
 }  // namespace sks

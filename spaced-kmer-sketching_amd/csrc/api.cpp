@@ -606,6 +606,16 @@ int sks_ctx_create(int device, void* stream, sks_ctx** out) {
     delete c;
     return sks::fail(SKS_E_HIP, "sks_ctx_create: hipEventCreate failed");
   }
+  // every code object of the library on this device, before the first build
+#define SKS_CALL_HOOK(tu) \
+  if (e == hipSuccess) e = sks::code_object_hook_##tu(c->stream);
+  e = hipSuccess;
+  SKS_TU_LIST(SKS_CALL_HOOK)
+#undef SKS_CALL_HOOK
+  if (e != hipSuccess) {
+    delete c;
+    return sks::fail(SKS_E_HIP, std::string("sks_ctx_create: code object load: ") + hipGetErrorString(e));
+  }
   *out = c;
   return SKS_OK;
 }

@@ -479,4 +479,6 @@ hipError_t fasta_parse_device(const uint8_t* raw, uint64_t n, uint8_t* out, uint
 #undef SKS_CK
 }
 
+SKS_CODE_OBJECT_HOOK(ingress)
+
 }  // namespace sks

@@ -622,4 +622,6 @@ uint64_t intersect_sym_tiles(uint32_t n) {
   return nb * (nb + 1) / 2;
 }
 
+SKS_CODE_OBJECT_HOOK(intersect)
+
 }  // namespace sks

@@ -869,4 +869,6 @@ hipError_t join_launch(const JoinLayout& rows, uint32_t r_blk0, const JoinLayout
 #undef SKS_JOIN_LAUNCH
 }
 
+SKS_CODE_OBJECT_HOOK(join)
+
 }  // namespace sks

@@ -3,7 +3,7 @@
 // mask of the block's sketches holding it, bucket by bucket.
 //
 // Buckets are two-level.  The value range is cut into G = B / 8 groups by
-// common bounds (quantiles averaged over up to 64 sample sketches), and a
+// common bounds (the median of up to 64 sample sketches' quantiles), and a
 // group's 8 buckets are chosen by a hash of the value.  The two levels serve
 // two masters:
 //   * every sketch is sorted, so its part of a value group is ONE contiguous
@@ -125,10 +125,16 @@ __device__ __forceinline__ uint32_t dd_insert(uint32_t* s_tab, const uint64_t* s
 }
 
 // Workgroups [0, nb_bounds): the group bounds, a wave per bound (bounds[g] =
-// mean over up to 64 sample sketches of their g/G quantile; bounds[0] = 0,
-// bounds[G] = the largest value).  128-bit values are averaged as doubles
-// (hi * 2^64 + lo) and split back: every step is monotonic, so the bounds are
-// non-decreasing, which is all exactness needs.  The last workgroup:
+// the lower median over up to 64 sample sketches of their g/G quantile;
+// bounds[0] = 0, bounds[G] = the largest value).  The median, not the mean: a
+// spaced mask leaves gaps in the value space (the masked-out bit positions are
+// zero), the sketches' ranks drift apart by more than a group's population, and
+// a mean of two quantiles on either side of a gap lands inside it, so that
+// group takes every sketch's values up to the gap (round 6: up to 217
+// elements of one sketch against 12 expected at (23, 13), groups above the
+// placement's capacity at w = 45).  The median is a sampled value, exact at
+// 128 bits, and an order statistic of non-decreasing sequences, so the bounds
+// are non-decreasing, which is all exactness needs.  The last workgroup:
 // bstart[k] = elements of the blocks before k (a running scan over the sizes).
 template <int EW>
 __global__ __launch_bounds__(kPT) void k_gl_prep(const uint64_t* __restrict__ data,
@@ -141,35 +147,34 @@ __global__ __launch_bounds__(kPT) void k_gl_prep(const uint64_t* __restrict__ da
     const uint32_t g = blockIdx.x * (kPT / 64) + wave;
     if (g > G) return;
     const uint32_t K = min(count, 64u);
-    double x = 0.0, used = 0.0;
+    KV q{0, 0};
+    bool have = false;
     if ((uint32_t)lane < K && g > 0 && g < G) {
       const uint32_t i = (uint32_t)((uint64_t)lane * count / K);
       const uint32_t sz = sizes[i];
       if (sz) {
-        const KV q = kv_load<EW>(data, starts[i] + (uint64_t)g * sz / G);
-        x = EW == 1 ? (double)q.lo : (double)q.hi * 18446744073709551616.0 + (double)q.lo;
-        used = 1.0;
+        q = kv_load<EW>(data, starts[i] + (uint64_t)g * sz / G);
+        have = true;
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      x += __shfl_xor(x, o, 64);
-      used += __shfl_xor(used, o, 64);
+    // rank of this lane's sample among the wave's (ties by lane)
+    const uint64_t valid = __ballot(have);
+    uint32_t rank = 0;
+    for (int j = 0; j < 64; ++j) {
+      const KV o{(uint64_t)__shfl((long long)q.lo, j, 64), (uint64_t)__shfl((long long)q.hi, j, 64)};
+      const bool below = kv_lt<EW>(o, q) || (kv_eq<EW>(o, q) && j < lane);
+      rank += ((valid >> j) & 1ull) && below ? 1u : 0u;
     }
-    if (lane) return;
+    const uint32_t used = (uint32_t)__popcll(valid);
     KV b{0, 0};
     if (g == G) {
+      if (lane) return;
       b = KV{~0ull, EW == 1 ? 0ull : ~0ull};
-    } else if (g > 0) {
-      const double m = used > 0.0 ? x / used : 0.0;
-      if (EW == 1) {
-        b.lo = m >= 18446744073709549568.0 ? ~0ull : (uint64_t)m;
-      } else {
-        const double h = floor(m * (1.0 / 18446744073709551616.0));
-        b.hi = h >= 18446744073709549568.0 ? ~0ull : (uint64_t)h;
-        const double r = m - h * 18446744073709551616.0;  // exact
-        b.lo = r >= 18446744073709549568.0 ? ~0ull : (uint64_t)r;
-      }
+    } else if (used == 0) {
+      if (lane) return;
+    } else {
+      if (!have || rank != (used - 1) / 2) return;
+      b = q;
     }
     kv_store<EW>(bounds, g, b);
     return;
@@ -1489,5 +1494,7 @@ hipError_t join_layout_build(const uint64_t* data, const uint64_t* starts, const
 #endif
   return hipGetLastError();
 }
+
+SKS_CODE_OBJECT_HOOK(layout)
 
 }  // namespace sks

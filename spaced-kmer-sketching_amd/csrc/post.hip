@@ -1084,4 +1084,6 @@ hipError_t launch_interleave(const uint64_t* lo, const uint64_t* hi, uint64_t n,
   return hipGetLastError();
 }
 
+SKS_CODE_OBJECT_HOOK(post)
+
 }  // namespace sks

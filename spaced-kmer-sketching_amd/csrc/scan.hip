@@ -788,4 +788,6 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
   return flavour == 0 ? pick(scan_kernel_wide<kModeBottom, 0>) : pick(scan_kernel_wide<kModeBottom, 1>);
 }
 
+SKS_CODE_OBJECT_HOOK(scan)
+
 }  // namespace sks

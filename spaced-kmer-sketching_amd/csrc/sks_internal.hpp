@@ -215,8 +215,8 @@ struct JoinLayout {
 uint32_t join_cap();                       // entries per join chunk (table capacity)
 uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch of max_size
 // G = 2^log_b / 8 value groups (>= 1); bounds: (G + 1) values of ew words.
-// join_layout_bounds computes the group bounds of a set (quantiles averaged
-// over up to 64 samples).  join_layout_build: the layout of sketches (data,
+// join_layout_bounds computes the group bounds of a set (the median over up
+// to 64 sample sketches of their quantiles).  join_layout_build: the layout of sketches (data,
 // starts, sizes)[0, count) with the caller's bounds, or (d_bounds null)
 // bounds computed from these sketches; temp: join_layout_temp_bytes;
 // d_stat[0] is raised to the largest block-bucket population (entries),
@@ -224,6 +224,20 @@ uint32_t join_log_b(uint32_t max_size);    // bucket count for a largest sketch 
 // launches, no host synchronisation.  `zero`: up to three word spans the build's
 // second launch clears before the placement runs (the caller's status words,
 // count tiles, tile counters: no memset launches of their own).
+// Code objects: HIP loads each .hip translation unit's code object on a device
+// at the first launch of one of its kernels (post.hip's, with the rocPRIM sorts,
+// is 14 MB and takes ~30 ms), so sks_ctx_create launches one empty kernel per
+// unit (load_code_objects, api.cpp) and a context's first build does not pay it.
+#define SKS_TU_LIST(X) X(ani) X(ingress) X(intersect) X(join) X(layout) X(post) X(scan) X(windows)
+#define SKS_DECLARE_HOOK(tu) hipError_t code_object_hook_##tu(hipStream_t s);
+SKS_TU_LIST(SKS_DECLARE_HOOK)
+#undef SKS_DECLARE_HOOK
+#define SKS_CODE_OBJECT_HOOK(tu)                                    \
+  __global__ void k_code_object_##tu() {}                           \
+  hipError_t code_object_hook_##tu(hipStream_t s) {                 \
+    hipLaunchKernelGGL(k_code_object_##tu, dim3(1), dim3(1), 0, s); \
+    return hipGetLastError();                                       \
+  }
 uint32_t join_layout_groups(uint32_t log_b);
 // log2 of the value groups per region a build of n_blk blocks uses (1..3)
 uint32_t join_layout_region_log(uint32_t n_blk, uint32_t log_b);

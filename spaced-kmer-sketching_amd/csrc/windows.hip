@@ -104,4 +104,6 @@ hipError_t launch_windows_dense(const uint8_t* seq, uint64_t n_bytes, uint64_t f
   return hipGetLastError();
 }
 
+SKS_CODE_OBJECT_HOOK(windows)
+
 }  // namespace sks

@@ -385,3 +385,50 @@ def test_fused_ani_refuses_unmapped_host_memory(torch_cuda, ctx):
     got = cnt.cpu().numpy().reshape(64, 64)[:n, :n]
     want = np.array([[np.intersect1d(sk[i], sk[j]).size for j in range(n)] for i in range(n)])
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("ew", [1, 2])
+def test_layout_bounds_are_sample_medians(torch_cuda, ctx, ew):
+    """k_gl_prep's group bounds: bounds[g] = the lower median over up to 64
+    sample sketches (sketch lane * n / 64) of their element at g * size / G,
+    bounds[0] = 0, bounds[G] = the largest value.  The values leave a gap
+    (half of each sketch below 2^40, half above 2^62, as a spaced mask's
+    masked-out positions do) and the sketch sizes differ, so a mean of the
+    samples would land inside the gap; one sketch is empty (not sampled)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    n, log_b = 100, 10
+    G = sksffi.join_layout_groups(log_b)
+    sk = []
+    for i in range(n):
+        m = 0 if i == 3 else 900 + 37 * (i % 13)
+        lo = rng.integers(0, 2**40, size=m // 2, dtype=np.uint64)
+        hi = rng.integers(2**62, 2**63, size=m - m // 2, dtype=np.uint64)
+        v = np.concatenate([lo, hi])
+        if ew == 1:
+            a = np.unique(v).reshape(-1, 1)
+        else:
+            a = np.unique(np.stack([rng.integers(0, 2**64, size=m, dtype=np.uint64), v], 1), axis=0)
+            a = a[np.lexsort((a[:, 0], a[:, 1]))]
+        sk.append(a)
+    sizes = np.array([len(x) for x in sk], dtype=np.uint32)
+    starts = np.zeros(n, dtype=np.uint64)
+    starts[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    flat = np.concatenate([x.reshape(-1) for x in sk] + [np.zeros(2, np.uint64)])
+    d = torch.from_numpy(flat.view(np.int64)).to("cuda:0")
+    st = torch.from_numpy(starts.view(np.int64)).to("cuda:0")
+    sz = torch.from_numpy(sizes.view(np.int32)).to("cuda:0")
+    out = torch.zeros((G + 1) * ew, dtype=torch.int64, device="cuda:0")
+    ctx.join_layout_bounds(d.data_ptr(), st.data_ptr(), sz.data_ptr(), n, log_b, out.data_ptr(), ew)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint64).reshape(G + 1, ew)
+    key = (lambda r: int(r[0])) if ew == 1 else (lambda r: (int(r[1]) << 64) | int(r[0]))
+    lanes = [lane * n // 64 for lane in range(64)]
+    assert [int(x) for x in got[0]] == [0] * ew and all(int(x) == 2**64 - 1 for x in got[G])
+    for g in range(1, G):
+        smp = sorted(key(sk[i][g * len(sk[i]) // G]) for i in lanes if len(sk[i]))
+        assert key(got[g]) == smp[(len(smp) - 1) // 2], g
+    # no group takes more than a few times its share of any sketch
+    b = [key(got[g]) for g in range(G + 1)]
+    worst = max(int(np.diff(np.searchsorted([key(r) for r in x], b)).max()) for x in sk if len(x))
+    assert worst <= 4 * (sizes.max() // G + 1)
