@@ -17,6 +17,9 @@
 #   ranksim [tag] [worlds...]    tools/rank_sim.py (one rank of N replayed on this GPU)
 #   sweep [tag]                  the reference main (bin/kmer-sketching) on 64 config-4 FASTA files under a
 #                                kernel trace, and the drop-in std::function flow (tools/dropin_flow)
+#   swdiag [tag] <lib dir>       the same main with the libsks.so in <lib dir> (a stamps variant from
+#                                tools/build_variant.sh, its stderr kept), then a kernel trace kept whole (gz)
+#   apitrace [tag] <script...>   HIP API + kernel trace of a python3 script, both CSVs kept (gz)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TASK=$1; shift
@@ -99,6 +102,22 @@ sweep)
   $T 600 $R/spaced-kmer-sketching_amd/bin/dropin-flow 21:21,31:31,45:35,50:40 $(cat $D/list.txt) \
     > $O/dropin.json 2> $O/dropin.err || { tail -20 $O/dropin.err; exit 1; }
   cat $O/dropin.json ;;
+swdiag)
+  O=$R/gpurun_out/${1:-swdiag}; L=$2; mkdir -p $O; cd $R
+  D=/tmp/sks_sweep_files
+  $T 300 python3 tools/sweep_files.py $D 64 > $O/files.log 2>&1 || { tail -5 $O/files.log; exit 1; }
+  LD_LIBRARY_PATH=$R/$L $T 300 $R/spaced-kmer-sketching_amd/bin/kmer-sketching /tmp/o.csv $(cat $D/list.txt) \
+    > $O/stamps_run.log 2> $O/stamps.err || { tail $O/stamps.err; exit 1; }
+  cd /tmp
+  $T 400 rocprofv3 --kernel-trace --output-format csv -d $O/t -o run -- $R/spaced-kmer-sketching_amd/bin/kmer-sketching \
+    /tmp/o2.csv $(cat $D/list.txt) > $O/trace_run.log 2>&1 || { tail $O/trace_run.log; exit 1; }
+  f=$(find $O/t -name '*kernel_trace.csv' | head -1); gzip -c $f > $O/kernel_trace.csv.gz; rm -rf $O/t ;;
+apitrace)
+  O=$R/gpurun_out/${1:-apitrace}; shift; mkdir -p $O; cd /tmp
+  $T 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $O/t -o run -- python3 "$R/$1" "${@:2}" \
+    > $O/run.log 2>&1 || { tail -20 $O/run.log; exit 1; }
+  for f in $(find $O/t -name '*.csv'); do gzip -c $f > $O/$(basename $f).gz; done; rm -rf $O/t
+  grep -v amdgpu.ids $O/run.log | tail -3 ;;
 *)
-  sed -n 2,22p "$0"; exit 2 ;;
+  sed -n 2,26p "$0"; exit 2 ;;
 esac
