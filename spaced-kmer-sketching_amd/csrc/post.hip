@@ -21,6 +21,10 @@ namespace sks {
 
 hipError_t Scratch::reserve(size_t n) {
   if (n <= bytes) return hipSuccess;
+  // grow by at least half: a caller whose need creeps up (the reference sweep's
+  // sketches grow with k over its first configurations) reallocates a few
+  // times, not once per call (a reallocation costs 0.1-1 ms of hipMalloc)
+  const size_t grown = bytes + bytes / 2;
   // queued work may still read the old buffer (metadata uploads do not wait
   // for their stream): it is reused only after the owner stream's queued work;
   // an ownerless buffer waits for the device (growth is rare)
@@ -34,7 +38,7 @@ hipError_t Scratch::reserve(size_t n) {
   }
   ptr = nullptr;
   bytes = 0;
-  size_t want = std::max<size_t>(n, 1 << 20);
+  size_t want = std::max<size_t>(std::max<size_t>(n, grown), 1 << 20);
   hipError_t e = owner ? cache_alloc(&ptr, want) : hipMalloc(&ptr, want);
   if (e == hipSuccess) bytes = want;
   return e;
