@@ -759,7 +759,11 @@ hipError_t launch_scan(const ScanParams& p, int mode, int flavour, bool wide, in
     ScanParams q = p;
     int grid = grid_override > 0 ? grid_override : kDynOversubscribe * occupancy_grid(kernel, device);
     const uint64_t per = p.n_tiles / ((uint64_t)grid * 16);
-    q.chunk = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(2, per));
+    // smallest chunk 3 (SKS_SCAN_MIN_CHUNK overrides): config 2's one 5 Mb genome
+    // (1221 tiles) scans in 27.4 us in chunks of 3 against 32.2 in chunks of 2
+    // (1: 43, 4: 30, 6: 29); 128 config-4 genomes are the same at 2 and 3
+    static const uint64_t min_chunk = getenv("SKS_SCAN_MIN_CHUNK") ? std::max(1, atoi(getenv("SKS_SCAN_MIN_CHUNK"))) : 3;
+    q.chunk = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(min_chunk, per));
     const uint64_t need = (p.n_tiles + q.chunk - 1) / q.chunk;
     if ((uint64_t)grid > need) grid = (int)need;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, q);
