@@ -110,7 +110,10 @@ int sks_fasta_runs(const sks_fasta* f, uint8_t* codes, uint64_t* run_lens, uint6
 
 /* ---- device context ---------------------------------------------------------------- */
 typedef struct sks_ctx sks_ctx;
-/* stream: a hipStream_t (may be NULL = the default stream). */
+/* stream: a hipStream_t (may be NULL = the default stream).  Creating a context
+ * loads every code object of the library on its device (one empty kernel per HIP
+ * translation unit; ~30 ms the first time in a process), so that the first build
+ * or join does not pay it inside the caller's timing. */
 int sks_ctx_create(int device, void* stream, sks_ctx** out);
 int sks_ctx_destroy(sks_ctx* ctx);
 int sks_ctx_set_stream(sks_ctx* ctx, void* stream);
