@@ -122,6 +122,7 @@ struct JoinArgs {
   const int32_t* sizes;
   double inv_k;
   uint32_t* tile_done;  // [tile - tile_begin]
+  int diag_last;        // dispatch the off-diagonal tiles first, the diagonal ones last (all sym tiles, one launch)
   const double* root;   // root[x] = ani_of(x, root_size) (JoinAni::root), or null
   uint32_t root_size;
 };
@@ -283,7 +284,28 @@ __global__ __launch_bounds__(kJB, EW == 1 ? SKS_JOIN_WPE1 : SKS_JOIN_WPE2) void 
   uint64_t js_last = __builtin_amdgcn_s_memtime();
 #endif
 
-  const uint64_t t = a.tile_begin + blockIdx.x / a.n_groups;
+  // tile of this workgroup: dispatch slot u, in tile order, or (diag_last) the
+  // off-diagonal tiles in tile order and then the diagonal ones.  A tile's ANI
+  // is written to host memory by its last workgroup, so the tiles finishing in
+  // the launch's last round of workgroups write theirs after every count is
+  // done; diagonal tiles are the cheapest (no table) and write one 64 x 64
+  // block (no mirror), so they take that round.
+  const uint64_t u = blockIdx.x / a.n_groups;
+  uint64_t t = a.tile_begin + u;
+  if (a.diag_last) {
+    const uint64_t nb = a.n_col_blocks, n_off = nb * (nb - 1) / 2;
+    const auto row_start = [nb](uint64_t i) { return i * nb - i * (i - 1) / 2; };  // tile (i, i)
+    if (u < n_off) {  // row i of the upper triangle holds nb - 1 - i off-diagonal tiles
+      uint64_t i = 0, rem = u;
+      while (rem >= nb - 1 - i) {
+        rem -= nb - 1 - i;
+        ++i;
+      }
+      t = row_start(i) + 1 + rem;
+    } else {
+      t = row_start(u - n_off);
+    }
+  }
   const uint32_t grp = blockIdx.x % a.n_groups;
   uint32_t I, J;
   if (a.tiles) {
@@ -741,6 +763,12 @@ template <int EW, bool CHECK, bool PIECES>
 hipError_t launch_join_slices(JoinArgs ja, uint64_t tile_begin, uint64_t tile_end, bool packed, int32_t* out,
                               uint32_t* tile_done, hipStream_t s) {
   const uint64_t tiles_per_launch = std::max<uint64_t>(1, kMaxGrid / ja.n_groups);
+  // diagonal tiles last: a symmetric launch of every tile (no tile list, one slice)
+  const uint64_t all_sym = (uint64_t)ja.n_col_blocks * (ja.n_col_blocks + 1) / 2;
+  ja.diag_last = ja.sym && !ja.tiles && tile_begin == 0 && tile_end == all_sym &&
+                         tile_end <= tiles_per_launch && getenv("SKS_JOIN_TILE_ORDER") == nullptr
+                     ? 1
+                     : 0;
   for (uint64_t t0 = tile_begin; t0 < tile_end; t0 += tiles_per_launch) {
     const uint64_t nt = std::min(tiles_per_launch, tile_end - t0);
     ja.tile_begin = t0;
